@@ -1,0 +1,207 @@
+/*
+ * kubecheck.h — C ABI of libkubecheck.so, the MI355X-native BFS model
+ * checker for KubeAPI.tla (JohnStrunk/tla-kubernetes).
+ *
+ * Plain C, plain pointers and sizes; no torch, no C++ types.  Every entry
+ * point returns 0 on success or a negative errno-style code (-EINVAL bad
+ * argument, -ENOMEM device memory / table full, -EIO HIP failure, -ENODEV
+ * no GPU) and leaves a thread-local message for kc_last_error().  Nothing
+ * aborts and nothing throws across this boundary.
+ *
+ * What each group replaces in the reference's hot path.  The reference's
+ * checker is TLC 2.16 (tla2tools.jar, rev cdddf55; KubeAPI.toolbox/Model_1/
+ * MC.out:2), a third-party Java jar not vendored in the reference; its
+ * plugin seams are named in the recorded run's banner (MC.out:5:
+ * "OffHeapDiskFPSet, DiskStateQueue") and selected by TLC system properties
+ * [ext-TLC].  INTEGRATION.md shows the Java (Panama FFM) binding a TLC
+ * maintainer would add over these symbols.
+ *
+ *   kc_fpset_*   tlc2.tool.fp.FPSet (abstract class; impl chosen by
+ *                -Dtlc2.tool.fp.FPSet.impl=<class>):
+ *                  put(long fp)      -> boolean "was already present"
+ *                  contains(long fp) -> boolean
+ *                  size()            -> long
+ *                  checkFPs()        -> double (collision estimate, MC.out:42)
+ *                  init/close        -> create/destroy
+ *                Batched: TLC's put() is per-state; the shim batches puts
+ *                from all -workers threads (flat combining).  Within one
+ *                batch, equal fps resolve exactly as sequential puts would:
+ *                the lowest index gets seen=0, every later one seen=1.
+ *                Fingerprints are normalised like TLC's disk FPSets: the
+ *                MSB is ignored and 0 is mapped to 1 (documented merge).
+ *   kc_squeue_*  tlc2.tool.queue.StateQueue (MC.out:5 "DiskStateQueue"):
+ *                FIFO of packed states in HBM (enqueue/dequeue batches).
+ *   kc_engine_*  tlc2.TLC's BFS ModelChecker run over Model_1-style inputs
+ *                (MC.cfg:1-16, MC.tla:1-16, KubeAPI___Model_1.launch):
+ *                counts, depth, per-action coverage and counterexamples.
+ *   kc_spec_*    host-side access to the lowered spec (canonical tuples) —
+ *                used for trace replay and by the parity tests.
+ */
+#ifndef KUBECHECK_H
+#define KUBECHECK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KC_ABI_VERSION 1
+#define KC_NACTIONS 22
+#define KC_MAX_LEVELS 4096
+
+/* ------------------------------------------------------------------ misc */
+/* Thread-local description of the last failure on this thread. */
+const char *kc_last_error(void);
+/* ABI version (KC_ABI_VERSION) and build string. */
+int kc_abi_version(void);
+const char *kc_build_info(void);
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int kc_device_count(void);
+
+/* ---------------------------------------------------------------- FPSet */
+typedef struct kc_fpset kc_fpset;
+
+/* Create a set able to hold `capacity_fps` fingerprints at <= 75% load
+ * (rounded up to whole 64-B buckets); it grows (rehash) when a batch would
+ * push it past 75%.  `device` is a HIP device ordinal. */
+int kc_fpset_create(uint64_t capacity_fps, int device, kc_fpset **out);
+void kc_fpset_destroy(kc_fpset *s);
+/* put: seen_out[i] = 1 iff fps[i] was already present (TLC FPSet.put). */
+int kc_fpset_put_batch(kc_fpset *s, const uint64_t *fps, size_t n, uint8_t *seen_out);
+/* contains: seen_out[i] = 1 iff present (TLC FPSet.contains). */
+int kc_fpset_contains_batch(kc_fpset *s, const uint64_t *fps, size_t n, uint8_t *seen_out);
+/* Device-pointer variants (HBM in and out, asynchronous on `hip_stream`,
+ * which may be NULL for the handle's own stream).  fps_dev may be rewritten
+ * (normalised in place). */
+int kc_fpset_put_batch_dev(kc_fpset *s, uint64_t *fps_dev, size_t n, uint8_t *seen_dev,
+                           void *hip_stream);
+int kc_fpset_contains_batch_dev(kc_fpset *s, uint64_t *fps_dev, size_t n, uint8_t *seen_dev,
+                                void *hip_stream);
+/* Distinct fingerprints stored. */
+uint64_t kc_fpset_size(const kc_fpset *s);
+/* Slot capacity (8 per 64-B bucket). */
+uint64_t kc_fpset_capacity(const kc_fpset *s);
+/* TLC checkFPs(): the minimum gap between any two stored fingerprints
+ * (sorted), from which TLC derives "based on the actual fingerprints"
+ * (MC.out:42).  *prob_out = 1/min_gap (TLC's estimate). */
+int kc_fpset_check_fps(kc_fpset *s, uint64_t *min_gap_out, double *prob_out);
+/* Synthetic stress: insert fingerprints
+ * splitmix64(seed + i) for i in [0, n) generated on device, in batches of
+ * `batch`; then look up n_lookup fps of which half are present.  Times are
+ * device times in seconds. */
+int kc_fpset_stress(kc_fpset *s, uint64_t seed, uint64_t n, uint64_t batch,
+                    uint64_t n_lookup, double *insert_seconds, double *lookup_seconds,
+                    uint64_t *found_out);
+
+/* ----------------------------------------------------------- StateQueue */
+typedef struct kc_squeue kc_squeue;
+/* FIFO of fixed-width packed states (words per state = `state_words`). */
+int kc_squeue_create(int state_words, uint64_t capacity_states, int device, kc_squeue **out);
+void kc_squeue_destroy(kc_squeue *q);
+int kc_squeue_enqueue(kc_squeue *q, const uint64_t *states, size_t n);
+/* dequeue up to `max_n` states into `out`; *n_out = number dequeued */
+int kc_squeue_dequeue(kc_squeue *q, uint64_t *out, size_t max_n, size_t *n_out);
+uint64_t kc_squeue_size(const kc_squeue *q);
+
+/* -------------------------------------------------------------- Engine */
+typedef struct {
+  int nc, np, ns;          /* clients, PVC controllers, API servers (Model_1: 1,1,1) */
+  int can_fail;            /* REQUESTS_CAN_FAIL  (MC.tla:5-7) */
+  int can_timeout;         /* REQUESTS_CAN_TIMEOUT (MC.tla:10-12) */
+  int check_deadlock;      /* launch:16 */
+  int variant;             /* 0 = KubeAPI.tla as written; 1 = Update w/o HasRead */
+  int device;              /* HIP device ordinal */
+  int keep_trace;          /* parent pointers (TLC's trace file); default 1 */
+  int max_levels;          /* 0 = to completion */
+  uint64_t fpset_slots;    /* initial FPSet slots; 0 = default */
+  uint64_t chunk_states;   /* parents per expansion chunk; 0 = default */
+  int verbose;             /* progress lines to stderr */
+} kc_model_config;
+
+typedef struct {
+  uint64_t init, generated, distinct, queue_left;
+  int depth;               /* BFS levels, init = level 1 (TLC msg 2194) */
+  int complete;
+  uint64_t act_gen[KC_NACTIONS];
+  uint64_t act_dist[KC_NACTIONS];
+  int nlevels;
+  uint64_t level_width[KC_MAX_LEVELS];
+  int err_kind;            /* 0 none, 1 assertion, 2 invariant, 3 deadlock */
+  int err_action;          /* action id (assertion) */
+  int err_self;            /* process index of the failing action */
+  int err_invariant;       /* 0 TypeOK, 1 OnlyOneVersion */
+  int err_level;           /* BFS level of the last trace state */
+  int trace_len;           /* states in the counterexample */
+  double seconds;          /* wall time of the BFS (device work + host loop) */
+  double collision_optimistic; /* TLC's calculated estimate d*(g-d)/2^64 */
+  uint64_t fpset_slots;
+  uint64_t peak_frontier;
+} kc_result;
+
+typedef struct kc_engine kc_engine;
+/* Fill a config with Model_1 defaults (1,1,1, both constants TRUE, deadlock on). */
+void kc_model_config_default(kc_model_config *cfg);
+int kc_engine_create(const kc_model_config *cfg, kc_engine **out);
+void kc_engine_destroy(kc_engine *e);
+/* Run BFS to completion (or error / max_levels). */
+int kc_engine_run(kc_engine *e, kc_result *res);
+/* Counterexample as TLC-style text ("State 1: ..."); returns bytes needed. */
+size_t kc_engine_trace_text(kc_engine *e, char *buf, size_t cap);
+/* Canonical tuple of trace state i (see kc_spec_tuple_words). */
+int kc_engine_trace_tuple(kc_engine *e, int i, uint64_t *out);
+/* Canonical tuples of the states of BFS level `level` (1-based) from the
+ * last run's frontier buffers, if still resident (only the final level and
+ * levels captured with kc_engine_capture_level).  Returns count or <0. */
+int64_t kc_engine_level_tuples(kc_engine *e, int level, uint64_t *out, uint64_t cap_states);
+/* Ask run() to keep a host copy of level `level`'s packed states. */
+int kc_engine_capture_level(kc_engine *e, int level);
+/* Per-kernel device timings of the last run (ms): expand, resolve, scan,
+ * emit; and the number of launches of each. */
+int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
+
+/* --------------------------------------------------- Sharded (multi-GPU) */
+/* Per-level stage API for the fingerprint-owner-sharded BFS (one process
+ * per GPU; the exchange between stages is done by the caller, e.g. RCCL
+ * all-to-all via torch.distributed).  See INTEGRATION.md. */
+int kc_shard_create(const kc_model_config *cfg, int rank, int world, kc_engine **out);
+/* Insert and adopt the init states owned by this rank. */
+int kc_shard_init(kc_engine *e, uint64_t *n_frontier);
+/* Expand the frontier; bucket candidate records by owner into the send
+ * buffer.  counts_out[r] = records for rank r (world entries). */
+int kc_shard_expand(kc_engine *e, uint64_t *counts_out);
+/* Device pointer + record size (bytes) of the send / receive buffers;
+ * the receive buffer is (re)sized to `recv_records`. */
+int kc_shard_send_buffer(kc_engine *e, void **dev_ptr, uint64_t *record_bytes);
+int kc_shard_recv_buffer(kc_engine *e, uint64_t recv_records, void **dev_ptr);
+/* Dedup + insert received records, compact the new ones into the next
+ * frontier.  Returns the local new-state count and the next level's
+ * candidate estimate; err_key_out = min local error key (or UINT64_MAX). */
+int kc_shard_insert(kc_engine *e, uint64_t recv_records, uint64_t *n_new,
+                    uint64_t *err_key_out);
+/* Totals of this shard (generated counts per action etc.). */
+int kc_shard_result(kc_engine *e, kc_result *res);
+
+/* ---------------------------------------------------------- Spec (host) */
+/* Words of the canonical tuple for a model: 1 + 19 * (nc + np + ns). */
+int kc_spec_tuple_words(int nc, int np, int ns);
+/* Words of the packed state (GPU layout) for a model. */
+int kc_spec_state_words(int nc, int np, int ns);
+/* Init states as canonical tuples; returns count. */
+int kc_spec_init(const kc_model_config *cfg, uint64_t *tuples_out, int cap);
+/* Successors of a canonical tuple in TLC order; returns count, or -2 when
+ * the state raises an Assert failure (*fail_action set), <0 on error. */
+int kc_spec_successors(const kc_model_config *cfg, const uint64_t *tuple, int *actions_out,
+                       uint64_t *succ_tuples_out, int cap, int *fail_action);
+/* TypeOK/OnlyOneVersion: -1 = both hold, 0 = TypeOK fails, 1 = OOV fails. */
+int kc_spec_check(const kc_model_config *cfg, const uint64_t *tuple);
+/* Fingerprint of the packed form of a canonical tuple. */
+int kc_spec_fingerprint(const kc_model_config *cfg, const uint64_t *tuple, uint64_t *fp_out);
+/* Packed <-> canonical conversion. */
+int kc_spec_pack(const kc_model_config *cfg, const uint64_t *tuple, uint64_t *packed_out);
+int kc_spec_unpack(const kc_model_config *cfg, const uint64_t *packed, uint64_t *tuple_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,135 @@
+/*
+ * kubeapi_oracle.h — CPU ORACLE for the KubeAPI BFS hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (tla-kubernetes_amd/)
+ * links, imports or executes this code.  It may be used only by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+ *
+ * What it is: a literal, sequential C restatement of the TLA+ translation in
+ * /root/reference/KubeAPI.tla:373-789 (Init, the 22 actions of Next, TypeOK,
+ * OnlyOneVersion) explored breadth-first with TLC's enumeration semantics
+ * (SURVEY.md Appendix A).  TLC itself (tla2tools.jar 2.16, MC.out:2) is a
+ * third-party jar that is absent from /root/reference and from this image (no
+ * JDK), so the oracle is pinned by the reference's own recorded run,
+ * KubeAPI.toolbox/Model_1/MC.out: totals (:1098), depth (:1101), the 22
+ * per-action generated counts (:78-621), the guard/branch evaluation counts
+ * and the TypeOK/OnlyOneVersion cardinality sums (:1023-1080).  See
+ * tests/golden/model1_mcout.json and tests/test_oracle_golden.py.
+ *
+ * Parameterisation (build-authored): the hard-coded process
+ * sets {"Client"}, {"PVCController"}, {"Server"} (KubeAPI.tla:161,225,268)
+ * become NC clients, NP PVC controllers and NS API servers.  NC=NP=NS=1 is
+ * exactly Model_1.
+ */
+#ifndef KUBEAPI_ORACLE_H
+#define KUBEAPI_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KO_MAXP 6          /* max processes (NC+NP+NS) */
+#define KO_NACTIONS 22
+#define KO_MAXLEVELS 4096
+#define KO_TUPLE_PER_PROC 19
+
+/* IF-branch counters pinned by MC.out coverage lines (e.g. :533, :542). */
+enum {
+  KO_B_CSTART_THEN, KO_B_CSTART_ELSE, KO_B_C1_START, KO_B_C1_C10, KO_B_C11_START,
+  KO_B_C11_c12, KO_B_C13_START, KO_B_C13_C2, KO_B_C3_START, KO_B_C3_C8, KO_B_C8_C4,
+  KO_B_C8_C6, KO_B_C7_START, KO_B_C7_C4, KO_B_PVCL_START, KO_B_PVCL_HAVE,
+  KO_B_API_CREATE, KO_B_API_FORCE, KO_B_API_FORCE_REPLACE, KO_B_API_FORCE_CREATE,
+  KO_B_API_GET, KO_B_API_GET_NOTFOUND, KO_B_API_DELETE, KO_B_API_UPDATE,
+  KO_B_API_UPDATE_OK, KO_B_API_UPDATE_ERR, KO_B_API_LIST, KO_B_API_ASSERT,
+  KO_NBRANCH
+};
+
+/* Global label / action enumerations (shared numbering with DESIGN.md). */
+enum {
+  KO_PC_NONE = 0,
+  KO_CStart, KO_C1, KO_C10, KO_C11, KO_c12, KO_C13, KO_C2, KO_C3, KO_C8,
+  KO_C6, KO_C7, KO_C4, KO_C5,
+  KO_PVCStart, KO_PVCListedPVCs, KO_PVCHavePVCs, KO_PVCDone,
+  KO_APIStart,
+  KO_DoRequest, KO_DoReply, KO_DoListRequest, KO_DoListReply,
+  KO_NPC
+};
+
+typedef struct {
+  int nc, np, ns;          /* clients, PVC controllers, API servers */
+  int can_fail;            /* REQUESTS_CAN_FAIL    (MC.tla:5-7)  */
+  int can_timeout;         /* REQUESTS_CAN_TIMEOUT (MC.tla:10-12) */
+  int check_deadlock;      /* launch:16 modelCorrectnessCheckDeadlock */
+  int keep_trace;          /* record parent pointers for counterexamples */
+  int max_levels;          /* 0 = run to completion */
+  uint64_t max_distinct;   /* 0 = unlimited; stop after the level that passes it */
+  int variant;             /* 0 = spec as written; 1 = lost-update bug (no HasRead) */
+  int fp_bits;             /* 128 (default, 0 means 128) or 64 */
+  int fpset_log2;          /* >0: presize the seen-set to 2^k entries (no growth) */
+  int progress;            /* print per-level progress to stderr */
+} ko_config;
+
+enum { KO_OK = 0, KO_ERR_ASSERT = 1, KO_ERR_INVARIANT = 2, KO_ERR_DEADLOCK = 3,
+       KO_ERR_EVAL = 4 };
+
+typedef struct {
+  uint64_t init, generated, distinct, queue_left;
+  int depth;               /* BFS levels, init = 1 (TLC msg 2194) */
+  int complete;            /* 1 if the whole reachable set was explored */
+  uint64_t act_gen[KO_NACTIONS];
+  uint64_t act_dist[KO_NACTIONS];
+  /* expression-evaluation counts pinned by MC.out (one per distinct state) */
+  uint64_t cov_api;        /* sum |apiState|          MC.out:1029 */
+  uint64_t cov_req;        /* sum |DOMAIN requests|   MC.out:1038 */
+  uint64_t cov_lreq;       /* sum |DOMAIN listReqs|   MC.out:1047 */
+  uint64_t cov_objs;       /* sum |objs|              MC.out:1059 */
+  uint64_t cov_api2;       /* sum |apiState|^2        MC.out:1080 */
+  uint64_t branch[KO_NBRANCH]; /* IF/CASE branch evaluation counts, KO_B_* */
+  uint64_t outdeg_hist[32];/* successors-per-state histogram */
+  int nlevels;
+  uint64_t level_width[KO_MAXLEVELS];
+  /* error report */
+  int err_kind;            /* KO_ERR_* */
+  int err_action;          /* action id for assertion failures */
+  int err_self;            /* process index */
+  int err_invariant;       /* 0 TypeOK, 1 OnlyOneVersion */
+  int err_level;           /* BFS level of the last state of the trace */
+  int trace_len;           /* states in the counterexample */
+  double seconds;
+} ko_result;
+
+const char *ko_action_name(int a);
+const char *ko_label_name(int pc);
+
+/* Run BFS.  Returns an opaque handle that keeps the trace (may be NULL if
+ * keep_trace==0).  Always fills *res. */
+void *ko_run(const ko_config *cfg, ko_result *res);
+/* Counterexample trace as TLA+-style text; returns bytes needed. */
+size_t ko_trace_text(void *h, char *buf, size_t cap);
+/* Canonical tuple of trace state i; returns #words. */
+int ko_trace_tuple(void *h, int i, uint64_t *out);
+void ko_free(void *h);
+
+/* Level-by-level API used by parity tests: canonical tuples of every state of
+ * BFS level `level` (1-based) in BFS order.  Returns the number of states
+ * written (or needed, if out==NULL).  Runs a fresh BFS up to that level. */
+uint64_t ko_level_tuples(const ko_config *cfg, int level, uint64_t *out, uint64_t cap_states);
+int ko_tuple_words(const ko_config *cfg);
+
+/* Successors of one canonical-tuple state, in TLC enumeration order: writes
+ * action ids and successor tuples; returns count (or -1 on assertion
+ * failure, with *fail_action set). */
+int ko_successors(const ko_config *cfg, const uint64_t *tuple, int *actions,
+                  uint64_t *succ_tuples, int cap, int *fail_action);
+
+/* Throughput sample: expand `n_states` states of the BFS starting at the
+ * first level with >= n_states states (or the widest level), timing only the
+ * expand+fingerprint+dedup work.  Used by bench.py's cpu_baseline leg. */
+double ko_bench_sample(const ko_config *cfg, double seconds_budget, uint64_t *states_done);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

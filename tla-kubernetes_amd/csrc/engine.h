@@ -1,0 +1,48 @@
+// engine.h — type-erased engine interface behind the kc_engine_* C-ABI.
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+
+#include "../../include/kubecheck.h"
+
+namespace kc {
+
+// Kernel kinds timed by the engine (kc_engine_kernel_times order).
+enum KernelKind { KK_EXPAND = 0, KK_RESOLVE = 1, KK_SCAN = 2, KK_EMIT = 3, KK_COUNT = 4 };
+
+class EngineBase {
+ public:
+  explicit EngineBase(const kc_model_config& cfg) : cfg_(cfg) {}
+  virtual ~EngineBase() = default;
+  virtual int setup() = 0;
+  virtual int run(kc_result* res) = 0;
+  virtual size_t trace_text(char* buf, size_t cap) const = 0;
+  virtual int trace_tuple(int i, uint64_t* out) const = 0;
+  virtual int64_t level_tuples(int level, uint64_t* out, uint64_t cap) = 0;
+  virtual int state_words() const = 0;
+  virtual int tuple_words() const = 0;
+  void set_capture(int level) { capture_level_ = level; }
+  void set_timing(bool on) { timing_ = on; }
+  void kernel_times(double* ms, uint64_t* launches) const {
+    for (int k = 0; k < KK_COUNT; ++k) {
+      if (ms) ms[k] = ktime_ms_[k];
+      if (launches) launches[k] = klaunch_[k];
+    }
+  }
+
+ protected:
+  kc_model_config cfg_;
+  int capture_level_ = 0;
+  bool timing_ = false;
+  double ktime_ms_[KK_COUNT] = {};
+  uint64_t klaunch_[KK_COUNT] = {};
+};
+
+std::unique_ptr<EngineBase> make_engine(const kc_model_config& cfg);
+const char* action_name(int a);
+// TLA+-style rendering of a canonical tuple (spec_abi.cpp)
+std::string format_tuple(const uint64_t* tuple, int nc, int np, int ns);
+
+}  // namespace kc

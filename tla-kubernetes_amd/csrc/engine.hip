@@ -1,0 +1,569 @@
+// engine.hip — single-GPU level-synchronous BFS model checker for KubeAPI.tla
+// (replaces TLC's BFS ModelChecker + workers, FPSet and StateQueue for this
+// spec; MC.out:5).  Host loop + C-ABI kc_engine_*.
+//
+// Per level (all on one HIP stream, one host sync per level):
+//   for each chunk of <= chunk_states parents:
+//     memset batch table; k_expand; k_resolve; hipcub exclusive scan;
+//     k_emit; k_advance
+//   read {next width, next candidates, error key} back.
+// The frontier buffers are the StateQueue: double-buffered packed states
+// in HBM, FIFO order = (parent order, TLC successor order), identical to a
+// sequential TLC -workers 1 BFS.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/kubecheck.h"
+#include "engine.h"
+#include "engine_kernels.h"
+#include "fpset_host.h"
+#include "kc_common.h"
+
+namespace kc {
+
+namespace {
+
+template <class T>
+int grow_buffer(T*& p, uint64_t& cap, uint64_t need, bool keep, hipStream_t st) {
+  if (need <= cap) return 0;
+  uint64_t nc = cap ? cap : 1024;
+  while (nc < need) nc *= 2;
+  T* np = nullptr;
+  KC_HIP_TRY(hipMalloc(&np, nc * sizeof(T)));
+  if (keep && p && cap) KC_HIP_TRY(hipMemcpyAsync(np, p, cap * sizeof(T), hipMemcpyDeviceToDevice, st));
+  if (p) {
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    KC_HIP_TRY(hipFree(p));
+  }
+  p = np;
+  cap = nc;
+  return 0;
+}
+
+const char* kActionNames[A_COUNT] = {
+    "DoRequest", "DoReply", "DoListRequest", "DoListReply", "CStart", "C1", "C10", "C11",
+    "c12", "C13", "C2", "C3", "C8", "C6", "C7", "C4", "C5", "PVCStart", "PVCListedPVCs",
+    "PVCHavePVCs", "PVCDone", "APIStart"};
+
+}  // namespace
+
+// chunk_base += (last exclusive offset + last count)
+__global__ void k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ cnt,
+                          uint64_t n, Counters* __restrict__ C) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && n > 0)
+    C->chunk_base += (unsigned long long)offsets[n - 1] + cnt[n - 1];
+}
+
+// Insert a short list of fingerprints (init states, rehash) into the FPSet.
+__global__ void k_fpset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
+                                    unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                                    int* __restrict__ result) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int r = fpset_insert(slots, nbuckets, fps[i]);
+    if (result) result[i] = r;
+  }
+}
+
+const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
+
+template <class M>
+class EngineT final : public EngineBase {
+  using State = typename M::State;
+
+ public:
+  explicit EngineT(const kc_model_config& cfg) : EngineBase(cfg) {
+    flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
+  }
+  ~EngineT() override { release(); }
+
+  int state_words() const override { return M::W; }
+  int tuple_words() const override { return M::TUPLE_WORDS; }
+
+  int setup() override {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+      set_error("kubecheck: no HIP device visible (the engine has no CPU fallback)");
+      return -ENODEV;
+    }
+    if (cfg_.device < 0 || cfg_.device >= ndev) {
+      set_error("kubecheck: bad device %d", cfg_.device);
+      return -EINVAL;
+    }
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    KC_HIP_TRY(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
+    KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
+    return 0;
+  }
+
+  int run(kc_result* res) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    memset(res, 0, sizeof *res);
+    res->err_action = res->err_self = res->err_invariant = -1;
+    trace_.clear();
+    for (auto& t : ktime_ms_) t = 0;
+    ev_kind_.clear();
+    ev_used_ = 0;
+    for (auto& c : klaunch_) c = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+
+    // ---- Init (KubeAPI.tla:455-469), on the host: 2^NC states
+    const int ni = M::num_init();
+    std::vector<State> init(ni);
+    std::vector<uint64_t> fps(ni);
+    uint64_t cand = 0;
+    for (int k = 0; k < ni; ++k) {
+      M::init_state(k, init[k]);
+      fps[k] = M::fingerprint(init[k]);
+      cand += (uint64_t)M::plan(init[k], flags_).total;
+    }
+    const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
+    KC_TRY(fps_.init(fp_slots, st_));
+    KC_TRY(grow_buffer(cur_, cur_cap_, (uint64_t)ni, false, st_));
+    KC_TRY(grow_buffer(parent_, par_cap_, (uint64_t)ni + cand, false, st_));
+    KC_TRY(grow_buffer(ord_, ord_cap_, (uint64_t)ni + cand, false, st_));
+    KC_HIP_TRY(hipMemcpyAsync(cur_, init.data(), ni * sizeof(State), hipMemcpyHostToDevice, st_));
+    uint64_t* d_fps = nullptr;
+    int* d_res = nullptr;
+    KC_HIP_TRY(hipMalloc(&d_fps, ni * 8));
+    KC_HIP_TRY(hipMalloc(&d_res, ni * sizeof(int)));
+    KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), ni * 8, hipMemcpyHostToDevice, st_));
+    hipLaunchKernelGGL(k_fpset_insert_list, dim3(1), dim3(256), 0, st_, d_fps, (uint64_t)ni,
+                       fps_.slots, fps_.nbuckets, d_res);
+    std::vector<int> ires(ni);
+    KC_HIP_TRY(hipMemcpyAsync(ires.data(), d_res, ni * sizeof(int), hipMemcpyDeviceToHost, st_));
+    std::vector<unsigned long long> ipar(ni, ~0ull);
+    std::vector<uint8_t> iord(ni);
+    for (int k = 0; k < ni; ++k) iord[k] = (uint8_t)k;
+    KC_HIP_TRY(hipMemcpyAsync(parent_, ipar.data(), ni * 8, hipMemcpyHostToDevice, st_));
+    KC_HIP_TRY(hipMemcpyAsync(ord_, iord.data(), ni, hipMemcpyHostToDevice, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    (void)hipFree(d_fps);
+    (void)hipFree(d_res);
+    for (int k = 0; k < ni; ++k) {
+      if (ires[k] != 1) {
+        set_error("kubecheck: init states not distinct");
+        return -EIO;
+      }
+    }
+    fps_.count = ni;
+    KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
+    res->init = ni;
+    res->generated = ni;
+    res->distinct = ni;
+    init_states_ = init;
+
+    uint64_t n = ni, level_gidx = 0;
+    int level = 1;
+    res->level_width[0] = n;
+    res->nlevels = 1;
+    // invariants of the initial states
+    for (int k = 0; k < ni; ++k) {
+      const int inv = M::check(init[k]);
+      if (inv >= 0) {
+        res->err_kind = E_INVARIANT;
+        res->err_invariant = inv;
+        res->err_level = 1;
+        trace_.push_back(init[k]);
+        res->trace_len = 1;
+        finish(res, t0, n);
+        return 0;
+      }
+    }
+
+    const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 21)) + 255) / 256 * 256;
+    while (n > 0) {
+      if (cfg_.max_levels && level >= cfg_.max_levels) break;
+      // capacity for this level's output (cand is exact: next_cand of the
+      // previous level)
+      KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
+      const uint64_t next_gidx = level_gidx + n;
+      if (cfg_.keep_trace) {
+        KC_TRY(grow_buffer(parent_, par_cap_, next_gidx + cand + 1, true, st_));
+        KC_TRY(grow_buffer(ord_, ord_cap_, next_gidx + cand + 1, true, st_));
+      }
+      KC_TRY(fps_.reserve(cand, st_));
+      KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
+      KC_TRY(grow_buffer(newcnt_, cnt_cap_, std::min(n, chunk), false, st_));
+      KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
+      // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
+      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
+      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
+      // multi-chunk level: exact candidate count per chunk first
+      const uint64_t nchunks = (n + chunk - 1) / chunk;
+      if (nchunks > 1) {
+        KC_TRY(grow_buffer(d_chunk_cand_, chunk_cand_cap_, nchunks, false, st_));
+        KC_HIP_TRY(hipMemsetAsync(d_chunk_cand_, 0, nchunks * 8, st_));
+        hipLaunchKernelGGL(k_count_chunks<M>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st_,
+                           cur_, n, chunk, flags_, d_chunk_cand_);
+        chunk_cand_.resize(nchunks);
+        KC_HIP_TRY(hipMemcpyAsync(chunk_cand_.data(), d_chunk_cand_, nchunks * 8,
+                                  hipMemcpyDeviceToHost, st_));
+        KC_HIP_TRY(hipStreamSynchronize(st_));
+      }
+      for (uint64_t start = 0; start < n; start += chunk) {
+        const uint64_t cn = std::min(chunk, n - start);
+        // batch table: >= 2x the chunk's candidates, a power of two
+        const uint64_t ccand = nchunks > 1 ? chunk_cand_[start / chunk] : cand;
+        const uint64_t bcap = next_pow2(2 * ccand + 256);
+        KC_TRY(bt_.ensure(bcap, st_));
+        KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
+        timed(KK_EXPAND, [&] {
+          hipLaunchKernelGGL(k_expand<M>, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, st_,
+                             cur_ + start, cn, start, flags_, cfg_.check_deadlock, bt_.t, bcap - 1,
+                             d_ctr_);
+        });
+        const unsigned grid = (unsigned)((cn + 255) / 256);
+        timed(KK_RESOLVE, [&] {
+          hipLaunchKernelGGL(k_resolve<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                             flags_, bt_.t, bcap - 1, fps_.slots, fps_.nbuckets, newmask_, newcnt_,
+                             d_ctr_);
+        });
+        size_t tmp_bytes = 0;
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt_, offsets_, (int)cn, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        hipError_t scan_err = hipSuccess;
+        timed(KK_SCAN, [&] {
+          scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt_, offsets_, (int)cn, st_);
+        });
+        KC_HIP_TRY(scan_err);
+        timed(KK_EMIT, [&] {
+          hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                             flags_, newmask_, offsets_, next_, level_gidx, next_gidx, parent_, ord_,
+                             cfg_.keep_trace, d_ctr_);
+        });
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newcnt_, cn, d_ctr_);
+      }
+      KC_HIP_TRY(hipGetLastError());
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      collect_times();
+      const Counters& c = *h_ctr_;
+      if (c.overflow) {
+        set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
+        return -ENOMEM;
+      }
+      uint64_t gen = 0;
+      for (int a = 0; a < A_COUNT; ++a) gen += c.act_gen[a];
+      res->generated = ni + gen;
+      const uint64_t n_new = c.chunk_base;
+      fps_.count += n_new;
+      res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
+      if (c.err_key != ~0ull) {
+        KC_TRY(report_error(res, c.err_key, level, level_gidx, n));
+        res->distinct += n_new;
+        finish(res, t0, 0);
+        return 0;
+      }
+      res->distinct += n_new;
+      if (cfg_.verbose)
+        fprintf(stderr, "kubecheck: level %d width %llu -> %llu new, %llu distinct, %llu generated\n",
+                level, (unsigned long long)n, (unsigned long long)n_new,
+                (unsigned long long)res->distinct, (unsigned long long)res->generated);
+      if (capture_level_ == level + 1 && n_new) {
+        captured_.resize(n_new);
+        KC_HIP_TRY(hipMemcpy(captured_.data(), next_, n_new * sizeof(State), hipMemcpyDeviceToHost));
+      }
+      level_gidx = next_gidx;
+      std::swap(cur_, next_);
+      std::swap(cur_cap_, next_cap_);
+      n = n_new;
+      cand = c.next_cand;
+      ++level;
+      if (n) {
+        if (level > KC_MAX_LEVELS) {
+          set_error("kubecheck: more than %d levels", KC_MAX_LEVELS);
+          return -ENOMEM;
+        }
+        res->level_width[level - 1] = n;
+        res->nlevels = level;
+      }
+    }
+    last_level_ = res->nlevels;
+    last_n_ = n;
+    finish(res, t0, n);
+    return 0;
+  }
+
+  size_t trace_text(char* buf, size_t cap) const override;
+  int trace_tuple(int i, uint64_t* out) const override {
+    if (i < 0 || i >= (int)trace_.size()) {
+      set_error("trace index out of range");
+      return -EINVAL;
+    }
+    M::to_tuple(trace_[i], out);
+    return M::TUPLE_WORDS;
+  }
+  int64_t level_tuples(int level, uint64_t* out, uint64_t cap) override {
+    if (level == capture_level_ && !captured_.empty()) {
+      for (uint64_t i = 0; i < captured_.size() && i < cap; ++i)
+        M::to_tuple(captured_[i], out + i * M::TUPLE_WORDS);
+      return (int64_t)captured_.size();
+    }
+    if (level == 1) {
+      for (uint64_t i = 0; i < init_states_.size() && i < cap; ++i)
+        M::to_tuple(init_states_[i], out + i * M::TUPLE_WORDS);
+      return (int64_t)init_states_.size();
+    }
+    set_error("level %d not captured", level);
+    return -EINVAL;
+  }
+
+ private:
+  template <class F>
+  void timed(int k, F&& f) {
+    if (timing_) {
+      if (ev_used_ + 2 > ev_pool_.size()) {
+        hipEvent_t a, b;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        ev_pool_.push_back(a);
+        ev_pool_.push_back(b);
+      }
+      hipEvent_t a = ev_pool_[ev_used_], b = ev_pool_[ev_used_ + 1];
+      (void)hipEventRecord(a, st_);
+      f();
+      (void)hipEventRecord(b, st_);
+      ev_kind_.push_back(k);
+      ev_used_ += 2;
+    } else {
+      f();
+    }
+    ++klaunch_[k];
+  }
+  // after the level's sync: accumulate every timed launch
+  void collect_times() {
+    for (size_t q = 0; q < ev_kind_.size(); ++q) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ev_pool_[2 * q], ev_pool_[2 * q + 1]) == hipSuccess)
+        ktime_ms_[ev_kind_[q]] += ms;
+    }
+    ev_kind_.clear();
+    ev_used_ = 0;
+  }
+
+  int report_error(kc_result* res, uint64_t key, int level, uint64_t level_gidx, uint64_t n) {
+    const int kind = (int)(key & 0xff);
+    const int pos = (int)((key >> 8) & 0xff);
+    const uint64_t pidx = key >> 16;
+    if (pidx >= n) {
+      set_error("kubecheck: bad error key");
+      return -EIO;
+    }
+    res->err_kind = kind;
+    // path to the parent through the parent pointers
+    std::vector<State> path;
+    KC_TRY(path_to(level_gidx + pidx, path));
+    const State& s = path.back();
+    const typename M::Plan pl = M::plan(s, flags_);
+    if (kind == E_ASSERT) {
+      res->err_action = M::slot_action(s, pl.fail_slot);
+      res->err_self = pl.fail_slot < M::A ? pl.fail_slot
+                      : pl.fail_slot < 2 * M::A ? pl.fail_slot - M::A
+                                               : M::A + (pl.fail_slot - 2 * M::A);
+      res->err_level = level;
+    } else if (kind == E_INVARIANT) {
+      int slot, j;
+      M::locate(pl, pos, slot, j);
+      State x;
+      M::apply(s, slot, j, flags_, x);
+      res->err_invariant = M::check(x);
+      path.push_back(x);
+      res->err_level = level + 1;
+    } else {
+      res->err_level = level;
+    }
+    trace_ = path;
+    res->trace_len = (int)path.size();
+    return 0;
+  }
+
+  // Rebuild the states on the path to global state index g by walking the
+  // parent pointers (TLC's trace file) and replaying successors on the host.
+  int path_to(uint64_t g, std::vector<State>& out) {
+    if (!cfg_.keep_trace) {
+      set_error("kubecheck: trace requested but keep_trace=0");
+      return -EINVAL;
+    }
+    std::vector<std::pair<uint64_t, uint8_t>> chain;
+    for (;;) {
+      unsigned long long p = 0;
+      uint8_t o = 0;
+      KC_HIP_TRY(hipMemcpy(&p, parent_ + g, 8, hipMemcpyDeviceToHost));
+      KC_HIP_TRY(hipMemcpy(&o, ord_ + g, 1, hipMemcpyDeviceToHost));
+      chain.push_back({g, o});
+      if (p == ~0ull) break;
+      g = p;
+      if (chain.size() > KC_MAX_LEVELS + 2) {
+        set_error("kubecheck: corrupt parent chain");
+        return -EIO;
+      }
+    }
+    std::reverse(chain.begin(), chain.end());
+    out.clear();
+    out.push_back(init_states_.at(chain[0].second));
+    for (size_t k = 1; k < chain.size(); ++k) {
+      const State& s = out.back();
+      const typename M::Plan pl = M::plan(s, flags_);
+      int slot, j;
+      M::locate(pl, chain[k].second, slot, j);
+      State x;
+      M::apply(s, slot, j, flags_, x);
+      out.push_back(x);
+    }
+    return 0;
+  }
+
+  void finish(kc_result* res, std::chrono::steady_clock::time_point t0, uint64_t left) {
+    for (int a = 0; a < A_COUNT; ++a) {
+      res->act_gen[a] = h_ctr_->act_gen[a];
+      res->act_dist[a] = h_ctr_->act_dist[a];
+    }
+    res->depth = res->nlevels;
+    res->queue_left = left;
+    res->complete = (left == 0 && res->err_kind == 0 && !(cfg_.max_levels && res->nlevels >= cfg_.max_levels && left));
+    const double d = (double)res->distinct, gg = (double)res->generated;
+    res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
+    res->fpset_slots = fps_.capacity();
+    res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  void release() {
+    (void)hipSetDevice(cfg_.device);
+    fps_.release();
+    bt_.release();
+    for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_,
+                    (void*)newcnt_, (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
+      if (p) (void)hipFree(p);
+    if (h_ctr_) (void)hipHostFree(h_ctr_);
+    for (auto& e : ev_pool_) (void)hipEventDestroy(e);
+    if (d_chunk_cand_) (void)hipFree(d_chunk_cand_);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  Flags flags_{};
+  hipStream_t st_ = nullptr;
+  DevFpset fps_;
+  DevBatchTable bt_;
+  State *cur_ = nullptr, *next_ = nullptr;
+  uint64_t cur_cap_ = 0, next_cap_ = 0;
+  unsigned long long* parent_ = nullptr;
+  uint8_t* ord_ = nullptr;
+  uint64_t par_cap_ = 0, ord_cap_ = 0;
+  uint32_t *newmask_ = nullptr, *newcnt_ = nullptr, *offsets_ = nullptr;
+  uint64_t mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
+  uint8_t* scan_tmp_ = nullptr;
+  uint64_t scan_cap_ = 0;
+  Counters* d_ctr_ = nullptr;
+  Counters* h_ctr_ = nullptr;
+  unsigned long long* d_chunk_cand_ = nullptr;
+  uint64_t chunk_cand_cap_ = 0;
+  std::vector<unsigned long long> chunk_cand_;
+  std::vector<hipEvent_t> ev_pool_;
+  std::vector<int> ev_kind_;
+  size_t ev_used_ = 0;
+  std::vector<State> init_states_, trace_, captured_;
+  uint64_t last_n_ = 0;
+  int last_level_ = 0;
+};
+
+template <class M>
+size_t EngineT<M>::trace_text(char* buf, size_t cap) const {
+  std::string s;
+  for (size_t i = 0; i < trace_.size(); ++i) {
+    s += "State " + std::to_string(i + 1) + ":\n";
+    std::vector<uint64_t> t(M::TUPLE_WORDS);
+    M::to_tuple(trace_[i], t.data());
+    s += format_tuple(t.data(), cfg_.nc, cfg_.np, cfg_.ns);
+    s += "\n";
+  }
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), k);
+    buf[k] = 0;
+  }
+  return s.size() + 1;
+}
+
+std::unique_ptr<EngineBase> make_engine(const kc_model_config& cfg) {
+#define KC_MAKE(a, b, c)                                              \
+  if (cfg.nc == a && cfg.np == b && cfg.ns == c)                      \
+    return std::unique_ptr<EngineBase>(new EngineT<Model<a, b, c>>(cfg));
+  KC_FOR_EACH_MODEL(KC_MAKE)
+#undef KC_MAKE
+  return nullptr;
+}
+
+}  // namespace kc
+
+using namespace kc;
+
+struct kc_engine {
+  std::unique_ptr<EngineBase> impl;
+};
+
+extern "C" {
+
+void kc_model_config_default(kc_model_config* c) {
+  if (!c) return;
+  memset(c, 0, sizeof *c);
+  c->nc = c->np = c->ns = 1;
+  c->can_fail = c->can_timeout = 1;
+  c->check_deadlock = 1;
+  c->keep_trace = 1;
+}
+
+int kc_engine_create(const kc_model_config* cfg, kc_engine** out) {
+  if (!cfg || !out) { set_error("kc_engine_create: NULL argument"); return -EINVAL; }
+  *out = nullptr;
+  auto impl = make_engine(*cfg);
+  if (!impl) {
+    set_error("kc_engine_create: unsupported model nc=%d np=%d ns=%d", cfg->nc, cfg->np, cfg->ns);
+    return -EINVAL;
+  }
+  KC_TRY(impl->setup());
+  *out = new kc_engine{std::move(impl)};
+  return 0;
+}
+
+void kc_engine_destroy(kc_engine* e) { delete e; }
+
+int kc_engine_run(kc_engine* e, kc_result* res) {
+  if (!e || !res) { set_error("kc_engine_run: NULL argument"); return -EINVAL; }
+  return e->impl->run(res);
+}
+
+size_t kc_engine_trace_text(kc_engine* e, char* buf, size_t cap) {
+  return e ? e->impl->trace_text(buf, cap) : 0;
+}
+
+int kc_engine_trace_tuple(kc_engine* e, int i, uint64_t* out) {
+  if (!e || !out) { set_error("kc_engine_trace_tuple: NULL"); return -EINVAL; }
+  return e->impl->trace_tuple(i, out);
+}
+
+int64_t kc_engine_level_tuples(kc_engine* e, int level, uint64_t* out, uint64_t cap) {
+  if (!e) { set_error("kc_engine_level_tuples: NULL"); return -EINVAL; }
+  return e->impl->level_tuples(level, out, cap);
+}
+
+int kc_engine_capture_level(kc_engine* e, int level) {
+  if (!e) { set_error("kc_engine_capture_level: NULL"); return -EINVAL; }
+  e->impl->set_capture(level);
+  return 0;
+}
+
+int kc_engine_kernel_times(kc_engine* e, double* ms4, uint64_t* launches4) {
+  if (!e) { set_error("kc_engine_kernel_times: NULL"); return -EINVAL; }
+  e->impl->kernel_times(ms4, launches4);
+  return 0;
+}
+
+}  // extern "C"

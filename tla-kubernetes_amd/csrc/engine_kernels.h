@@ -1,0 +1,223 @@
+// engine_kernels.h — the four per-level BFS kernels (gfx950).
+//
+// One lane = one parent state.  Each kernel re-derives the parent's
+// successor plan from its packed words (cheap integer work) instead of
+// materialising candidate states in HBM; the only random HBM traffic is the
+// FPSet probe of each level-unique successor.
+//
+//   k_expand  : plan + every successor's fingerprint -> batch table
+//               (min order key per fp); per-action "generated" counters;
+//               Assert-failure / deadlock error keys.
+//   k_resolve : the batch representative of each fp probes/inserts the
+//               FPSet; per-parent bitmask + count of NEW successors.
+//   (scan)    : exclusive prefix sum of the counts (hipcub).
+//   k_emit    : NEW successors written in (parent, successor) order to the
+//               next frontier, with parent pointers (TLC's trace file),
+//               invariant checks (TypeOK, OnlyOneVersion), per-action
+//               "distinct" counters and the next level's candidate count.
+//
+// Order key of a successor: (parent index within the level) << 8 | t, where
+// t is its position in TLC's enumeration order.  Error keys put the parent
+// index in bits 16+, the successor position in bits 8-15 and the ErrKind in
+// bits 0-7, so the minimum key is the error a sequential 1-worker TLC BFS
+// would have hit first.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fpset_dev.h"
+#include "kubeapi_spec.h"
+
+namespace kc {
+
+struct Counters {
+  unsigned long long act_gen[A_COUNT];
+  unsigned long long act_dist[A_COUNT];
+  unsigned long long err_key;     // min error key of the level (~0 = none)
+  unsigned long long next_cand;   // successors of the new states (next level's work)
+  unsigned long long chunk_base;  // next-frontier offset of the current chunk
+  unsigned long long overflow;    // states with > MAXSUCC successors, full tables
+  unsigned long long batch_used;  // entries claimed in the batch table
+  unsigned long long pad[3];
+};
+
+template <class M>
+__device__ __forceinline__ typename M::State load_state(const typename M::State* __restrict__ p,
+                                                        uint64_t i) {
+  typename M::State s;
+  const ulonglong2* v = reinterpret_cast<const ulonglong2*>(p + i);
+#pragma unroll
+  for (int k = 0; k < M::W / 2; ++k) {
+    const ulonglong2 q = v[k];
+    s.w[2 * k] = q.x;
+    s.w[2 * k + 1] = q.y;
+  }
+  return s;
+}
+template <class M>
+__device__ __forceinline__ void store_state(typename M::State* __restrict__ p, uint64_t i,
+                                            const typename M::State& s) {
+  ulonglong2* v = reinterpret_cast<ulonglong2*>(p + i);
+#pragma unroll
+  for (int k = 0; k < M::W / 2; ++k) v[k] = make_ulonglong2(s.w[2 * k], s.w[2 * k + 1]);
+}
+
+// batch_insert with a bounded probe: returns false if the table is full.
+__device__ __forceinline__ bool batch_insert_bounded(BatchEntry* __restrict__ t, uint64_t mask,
+                                                     uint64_t fp, uint64_t key,
+                                                     unsigned long long* used) {
+  uint64_t i = batch_slot(fp, mask);
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    unsigned long long e = t[i].fp;
+    if (e == 0ull) {
+      e = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (e == 0ull) {
+        atomicAdd(used, 1ull);
+        e = fp;
+      }
+    }
+    if (e == fp) {
+      atomicMax(&t[i].nkey, ~(unsigned long long)key);
+      return true;
+    }
+    i = (i + 1) & mask;
+  }
+  return false;
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_expand(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+         int check_deadlock, BatchEntry* __restrict__ bt, uint64_t bmask, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const typename M::State s = load_state<M>(cur, i);
+    const typename M::Plan pl = M::plan(s, f);
+    const uint64_t pidx = base + i;
+    if (pl.fail_pos >= 0)
+      atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
+    else if (pl.total == 0 && check_deadlock)
+      atomicMin(&C->err_key, (pidx << 16) | E_DEADLOCK);
+    int tot = pl.total;
+    if (tot > M::MAXSUCC) {
+      atomicAdd(&C->overflow, 1ull);
+      tot = M::MAXSUCC;
+    }
+#pragma unroll
+    for (int slot = 0; slot < M::NSLOT; ++slot) {
+      const int c = (int)((pl.counts >> (6 * slot)) & 63);
+      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
+    }
+    for (int t = 0; t < tot; ++t) {
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      M::apply(s, slot, j, f, x);
+      if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t,
+                                &C->batch_used))
+        atomicAdd(&C->overflow, 1ull);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+          const BatchEntry* __restrict__ bt, uint64_t bmask, unsigned long long* __restrict__ slots,
+          uint64_t nbuckets, uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
+          Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const typename M::State s = load_state<M>(cur, i);
+  const typename M::Plan pl = M::plan(s, f);
+  const uint64_t pidx = base + i;
+  const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
+  uint32_t mask = 0;
+  for (int t = 0; t < tot; ++t) {
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    typename M::State x;
+    M::apply(s, slot, j, f, x);
+    const uint64_t fp = M::fingerprint(x);
+    if (batch_is_rep(bt, bmask, fp, (pidx << 8) | (uint64_t)t)) {
+      const int r = fpset_insert(slots, nbuckets, fp);
+      if (r == 1) mask |= 1u << t;
+      else if (r < 0) atomicAdd(&C->overflow, 1ull);
+    }
+  }
+  newmask[i] = mask;
+  newcnt[i] = (uint32_t)__popc(mask);
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+       const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
+       typename M::State* __restrict__ next, uint64_t level_gidx, uint64_t next_gidx,
+       unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
+       Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned long long sh_cand;
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sh_cand = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cand = 0;
+  if (i < n) {
+    uint32_t mask = newmask[i];
+    if (mask) {
+      const typename M::State s = load_state<M>(cur, i);
+      const typename M::Plan pl = M::plan(s, f);
+      const uint64_t pidx = base + i;
+      uint64_t o = C->chunk_base + offsets[i];
+      for (; mask; mask &= mask - 1) {
+        const int t = __ffs(mask) - 1;
+        int slot, j;
+        M::locate(pl, t, slot, j);
+        typename M::State x;
+        M::apply(s, slot, j, f, x);
+        store_state<M>(next, o, x);
+        if (keep_trace) {
+          parent[next_gidx + o] = level_gidx + pidx;
+          ord[next_gidx + o] = (uint8_t)t;
+        }
+        if (M::check(x) >= 0)
+          atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
+        atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
+        const typename M::Plan px = M::plan(x, f);
+        cand += (unsigned long long)px.total;
+        ++o;
+      }
+    }
+  }
+  // wave reduction of the candidate count, then one LDS atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x == 0 && sh_cand) atomicAdd(&C->next_cand, sh_cand);
+}
+
+// Successor totals per chunk of `chunk` parents (chunk % 256 == 0, so each
+// block lies in one chunk): sizes the batch tables of multi-chunk levels.
+template <class M>
+__global__ void __launch_bounds__(256)
+k_count_chunks(const typename M::State* __restrict__ cur, uint64_t n, uint64_t chunk, Flags f,
+               unsigned long long* __restrict__ chunk_cand) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long c = 0;
+  if (i < n) c = (unsigned long long)M::plan(load_state<M>(cur, i), f).total;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&chunk_cand[((uint64_t)blockIdx.x * blockDim.x) / chunk], c);
+}
+
+}  // namespace kc

@@ -1,0 +1,414 @@
+// fpset.hip — HBM FPSet: host owner, batch kernels and the kc_fpset_* C-ABI
+// (drop-in for TLC's tlc2.tool.fp.FPSet put/contains/size/checkFPs; see
+// include/kubecheck.h and INTEGRATION.md).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/kubecheck.h"
+#include "engine_kernels.h"
+#include "fpset_host.h"
+#include "kc_common.h"
+
+namespace kc {
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Rehash every stored fingerprint of `old` into `nw`.
+__global__ void k_fpset_rehash(const unsigned long long* __restrict__ old, uint64_t old_slots,
+                               unsigned long long* __restrict__ nw, uint64_t new_buckets,
+                               unsigned long long* __restrict__ fail) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < old_slots) {
+    const unsigned long long fp = old[i];
+    if (fp && fpset_insert(nw, new_buckets, fp) < 0) atomicAdd(fail, 1ull);
+  }
+}
+
+int DevFpset::init(uint64_t min_slots, hipStream_t st) {
+  release();
+  nbuckets = (min_slots + 7) / 8;
+  if (nbuckets < 8) nbuckets = 8;
+  KC_HIP_TRY(hipMalloc(&slots, nbuckets * 64));
+  KC_HIP_TRY(hipMemsetAsync(slots, 0, nbuckets * 64, st));
+  KC_HIP_TRY(hipMalloc(&d_fail, sizeof(unsigned long long)));
+  count = 0;
+  return 0;
+}
+
+void DevFpset::release() {
+  if (slots) (void)hipFree(slots);
+  if (d_fail) (void)hipFree(d_fail);
+  slots = nullptr;
+  d_fail = nullptr;
+  nbuckets = 0;
+  count = 0;
+}
+
+int DevFpset::reserve(uint64_t extra, hipStream_t st) {
+  if ((count + extra) * 4 <= capacity() * 3) return 0;
+  uint64_t nb = nbuckets;
+  while ((count + extra) * 4 > nb * 8 * 2) nb *= 2;  // land at <= 50% load
+  unsigned long long* ns = nullptr;
+  KC_HIP_TRY(hipMalloc(&ns, nb * 64));
+  KC_HIP_TRY(hipMemsetAsync(ns, 0, nb * 64, st));
+  KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
+  const uint64_t old_slots = capacity();
+  const unsigned grid = (unsigned)((old_slots + 255) / 256);
+  hipLaunchKernelGGL(k_fpset_rehash, dim3(grid), dim3(256), 0, st, slots, old_slots, ns, nb, d_fail);
+  KC_HIP_TRY(hipGetLastError());
+  unsigned long long fail = 0;
+  KC_HIP_TRY(hipMemcpyAsync(&fail, d_fail, sizeof fail, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  if (fail) {
+    (void)hipFree(ns);
+    set_error("fpset rehash failed (%llu)", fail);
+    return -ENOMEM;
+  }
+  KC_HIP_TRY(hipFree(slots));
+  slots = ns;
+  nbuckets = nb;
+  return 0;
+}
+
+int DevBatchTable::ensure(uint64_t entries, hipStream_t st) {
+  (void)st;
+  if (entries <= cap) return 0;
+  release();
+  KC_HIP_TRY(hipMalloc(&t, entries * sizeof(BatchEntry)));
+  cap = entries;
+  return 0;
+}
+
+void DevBatchTable::release() {
+  if (t) (void)hipFree(t);
+  t = nullptr;
+  cap = 0;
+}
+
+// --------------------------------------------------------------- kernels
+__global__ void k_normalize(uint64_t* __restrict__ fps, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fps[i] = normalize_fp(fps[i]);
+}
+__global__ void k_batch_claim(const uint64_t* __restrict__ fps, uint64_t n,
+                              BatchEntry* __restrict__ bt, uint64_t mask) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) batch_insert(bt, mask, fps[i], i);
+}
+__global__ void k_batch_put(const uint64_t* __restrict__ fps, uint64_t n,
+                            const BatchEntry* __restrict__ bt, uint64_t mask,
+                            unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                            uint8_t* __restrict__ seen, unsigned long long* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nw = 0, full = 0;
+  if (i < n) {
+    const uint64_t fp = fps[i];
+    uint8_t s = 1;
+    if (batch_is_rep(bt, mask, fp, i)) {
+      const int r = fpset_insert(slots, nbuckets, fp);
+      if (r == 1) { s = 0; nw = 1; }
+      else if (r < 0) full = 1;
+    }
+    seen[i] = s;
+  }
+  // one atomic per wave
+  const unsigned long long bw = __ballot(nw != 0), bf = __ballot(full != 0);
+  if ((threadIdx.x & 63) == 0) {
+    if (bw) atomicAdd(&stats[0], (unsigned long long)__popcll(bw));
+    if (bf) atomicAdd(&stats[1], (unsigned long long)__popcll(bf));
+  }
+}
+__global__ void k_contains(const uint64_t* __restrict__ fps, uint64_t n,
+                           const unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                           uint8_t* __restrict__ seen) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) seen[i] = (uint8_t)fpset_contains(slots, nbuckets, fps[i]);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// Stress insert: fingerprints generated in registers (no input traffic).
+__global__ void __launch_bounds__(256)
+k_stress_insert(uint64_t seed, uint64_t start, uint64_t n, unsigned long long* __restrict__ slots,
+                uint64_t nbuckets, unsigned long long* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nw = 0;
+  if (i < n) nw = fpset_insert(slots, nbuckets, normalize_fp(splitmix64(seed + start + i))) == 1;
+  const unsigned long long b = __ballot(nw != 0);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stats[0], (unsigned long long)__popcll(b));
+}
+// Stress lookup: even i -> an inserted fp, odd i -> one from a second stream.
+__global__ void __launch_bounds__(256)
+k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t n, const unsigned long long* __restrict__ slots,
+                uint64_t nbuckets, unsigned long long* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long f = 0;
+  if (i < n) {
+    const uint64_t z = (i & 1) ? splitmix64(seed ^ 0x5bd1e9955bd1e995ull) + i
+                               : seed + (splitmix64(i) % n_ins);
+    const uint64_t fp = normalize_fp((i & 1) ? splitmix64(z) : splitmix64(z));
+    f = fpset_contains(slots, nbuckets, fp);
+  }
+  const unsigned long long b = __ballot(f != 0);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stats[2], (unsigned long long)__popcll(b));
+}
+__global__ void k_compact_fps(const unsigned long long* __restrict__ slots, uint64_t nslots,
+                              unsigned long long* __restrict__ out, unsigned long long* __restrict__ n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots && slots[i]) out[atomicAdd(n, 1ull)] = slots[i];
+}
+__global__ void k_min_gap(const unsigned long long* __restrict__ s, uint64_t n,
+                          unsigned long long* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 < n) atomicMin(out, s[i + 1] - s[i]);
+}
+
+}  // namespace kc
+
+using namespace kc;
+
+struct kc_fpset {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevFpset fs;
+  DevBatchTable bt;
+  uint64_t* d_fps = nullptr;
+  uint8_t* d_seen = nullptr;
+  uint64_t stage_cap = 0;
+  unsigned long long* d_stats = nullptr;  // [new, full, found, spare]
+  std::mutex mu;
+};
+
+static int stage(kc_fpset* s, uint64_t n) {
+  if (n <= s->stage_cap) return 0;
+  if (s->d_fps) (void)hipFree(s->d_fps);
+  if (s->d_seen) (void)hipFree(s->d_seen);
+  s->d_fps = nullptr;
+  s->d_seen = nullptr;
+  s->stage_cap = 0;
+  const uint64_t cap = next_pow2(n);
+  KC_HIP_TRY(hipMalloc(&s->d_fps, cap * 8));
+  KC_HIP_TRY(hipMalloc(&s->d_seen, cap));
+  s->stage_cap = cap;
+  return 0;
+}
+
+static int put_dev(kc_fpset* s, uint64_t* fps, size_t n, uint8_t* seen, hipStream_t st,
+                   uint64_t* n_new) {
+  if (n == 0) return 0;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_normalize, dim3(grid), dim3(256), 0, st, fps, (uint64_t)n);
+  const uint64_t cap = next_pow2(2 * (uint64_t)n + 64);
+  KC_TRY(s->bt.ensure(cap, st));
+  KC_HIP_TRY(hipMemsetAsync(s->bt.t, 0, cap * sizeof(BatchEntry), st));
+  hipLaunchKernelGGL(k_batch_claim, dim3(grid), dim3(256), 0, st, fps, (uint64_t)n, s->bt.t, cap - 1);
+  KC_TRY(s->fs.reserve(n, st));
+  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_batch_put, dim3(grid), dim3(256), 0, st, fps, (uint64_t)n, s->bt.t, cap - 1,
+                     s->fs.slots, s->fs.nbuckets, seen, s->d_stats);
+  KC_HIP_TRY(hipGetLastError());
+  unsigned long long stats[4];
+  KC_HIP_TRY(hipMemcpyAsync(stats, s->d_stats, sizeof stats, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  if (stats[1]) {
+    set_error("fpset full");
+    return -ENOMEM;
+  }
+  s->fs.count += stats[0];
+  if (n_new) *n_new = stats[0];
+  return 0;
+}
+
+extern "C" {
+
+int kc_fpset_create(uint64_t capacity_fps, int device, kc_fpset** out) {
+  if (!out) { set_error("kc_fpset_create: out is NULL"); return -EINVAL; }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("kc_fpset_create: no HIP device");
+    return -ENODEV;
+  }
+  if (device < 0 || device >= ndev) { set_error("kc_fpset_create: bad device %d", device); return -EINVAL; }
+  KC_HIP_TRY(hipSetDevice(device));
+  auto* s = new kc_fpset();
+  s->device = device;
+  int rc = 0;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = -EIO;
+  if (!rc) rc = s->fs.init(capacity_fps * 4 / 3 + 8, s->stream);
+  if (!rc && hipMalloc(&s->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess) rc = -ENOMEM;
+  if (!rc && hipStreamSynchronize(s->stream) != hipSuccess) rc = -EIO;
+  if (rc) { kc_fpset_destroy(s); if (rc == -EIO) set_error("kc_fpset_create: HIP failure"); return rc; }
+  *out = s;
+  return 0;
+}
+
+void kc_fpset_destroy(kc_fpset* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  s->fs.release();
+  s->bt.release();
+  if (s->d_fps) (void)hipFree(s->d_fps);
+  if (s->d_seen) (void)hipFree(s->d_seen);
+  if (s->d_stats) (void)hipFree(s->d_stats);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int kc_fpset_put_batch(kc_fpset* s, const uint64_t* fps, size_t n, uint8_t* seen_out) {
+  if (!s || (n && (!fps || !seen_out))) { set_error("kc_fpset_put_batch: bad argument"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  KC_TRY(stage(s, n));
+  if (n == 0) return 0;
+  KC_HIP_TRY(hipMemcpyAsync(s->d_fps, fps, n * 8, hipMemcpyHostToDevice, s->stream));
+  KC_TRY(put_dev(s, s->d_fps, n, s->d_seen, s->stream, nullptr));
+  KC_HIP_TRY(hipMemcpyAsync(seen_out, s->d_seen, n, hipMemcpyDeviceToHost, s->stream));
+  KC_HIP_TRY(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int kc_fpset_contains_batch(kc_fpset* s, const uint64_t* fps, size_t n, uint8_t* seen_out) {
+  if (!s || (n && (!fps || !seen_out))) { set_error("kc_fpset_contains_batch: bad argument"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  KC_TRY(stage(s, n));
+  if (n == 0) return 0;
+  KC_HIP_TRY(hipMemcpyAsync(s->d_fps, fps, n * 8, hipMemcpyHostToDevice, s->stream));
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_normalize, dim3(grid), dim3(256), 0, s->stream, s->d_fps, (uint64_t)n);
+  hipLaunchKernelGGL(k_contains, dim3(grid), dim3(256), 0, s->stream, s->d_fps, (uint64_t)n,
+                     s->fs.slots, s->fs.nbuckets, s->d_seen);
+  KC_HIP_TRY(hipGetLastError());
+  KC_HIP_TRY(hipMemcpyAsync(seen_out, s->d_seen, n, hipMemcpyDeviceToHost, s->stream));
+  KC_HIP_TRY(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int kc_fpset_put_batch_dev(kc_fpset* s, uint64_t* fps_dev, size_t n, uint8_t* seen_dev, void* hs) {
+  if (!s || (n && (!fps_dev || !seen_dev))) { set_error("kc_fpset_put_batch_dev: bad argument"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = hs ? (hipStream_t)hs : s->stream;
+  return put_dev(s, fps_dev, n, seen_dev, st, nullptr);
+}
+
+int kc_fpset_contains_batch_dev(kc_fpset* s, uint64_t* fps_dev, size_t n, uint8_t* seen_dev, void* hs) {
+  if (!s || (n && (!fps_dev || !seen_dev))) { set_error("kc_fpset_contains_batch_dev: bad argument"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = hs ? (hipStream_t)hs : s->stream;
+  if (n == 0) return 0;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_normalize, dim3(grid), dim3(256), 0, st, fps_dev, (uint64_t)n);
+  hipLaunchKernelGGL(k_contains, dim3(grid), dim3(256), 0, st, fps_dev, (uint64_t)n, s->fs.slots,
+                     s->fs.nbuckets, seen_dev);
+  KC_HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+uint64_t kc_fpset_size(const kc_fpset* s) { return s ? s->fs.count : 0; }
+uint64_t kc_fpset_capacity(const kc_fpset* s) { return s ? s->fs.capacity() : 0; }
+
+int kc_fpset_check_fps(kc_fpset* s, uint64_t* min_gap_out, double* prob_out) {
+  if (!s) { set_error("kc_fpset_check_fps: NULL"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = s->stream;
+  const uint64_t nslots = s->fs.capacity();
+  unsigned long long *d_a = nullptr, *d_b = nullptr, *d_n = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int rc = 0;
+  unsigned long long n = 0, gap = ~0ull;
+  const uint64_t cnt = s->fs.count ? s->fs.count : 1;
+  if (hipMalloc(&d_a, cnt * 8) != hipSuccess || hipMalloc(&d_b, cnt * 8) != hipSuccess ||
+      hipMalloc(&d_n, 16) != hipSuccess) {
+    rc = -ENOMEM; set_error("kc_fpset_check_fps: out of device memory");
+  }
+  if (!rc) {
+    (void)hipMemsetAsync(d_n, 0, 8, st);
+    (void)hipMemcpyAsync(d_n + 1, &gap, 8, hipMemcpyHostToDevice, st);
+    hipLaunchKernelGGL(k_compact_fps, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, st,
+                       s->fs.slots, nslots, d_a, d_n);
+    (void)hipMemcpyAsync(&n, d_n, 8, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    if (n > cnt) { rc = -EIO; set_error("kc_fpset_check_fps: count mismatch"); }
+  }
+  if (!rc && n > 1) {
+    if (hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, d_a, d_b, (int)n, 0, 64, st) != hipSuccess) {
+      rc = -EIO; set_error("kc_fpset_check_fps: sort");
+    }
+    if (!rc && hipMalloc(&tmp, tmp_bytes) != hipSuccess) { rc = -ENOMEM; set_error("kc_fpset_check_fps: temp"); }
+    if (!rc) {
+      (void)hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, d_a, d_b, (int)n, 0, 64, st);
+      hipLaunchKernelGGL(k_min_gap, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_b, n, d_n + 1);
+      (void)hipMemcpyAsync(&gap, d_n + 1, 8, hipMemcpyDeviceToHost, st);
+      if (hipStreamSynchronize(st) != hipSuccess) { rc = -EIO; set_error("kc_fpset_check_fps: HIP"); }
+    }
+  }
+  if (tmp) (void)hipFree(tmp);
+  if (d_a) (void)hipFree(d_a);
+  if (d_b) (void)hipFree(d_b);
+  if (d_n) (void)hipFree(d_n);
+  if (rc) return rc;
+  if (min_gap_out) *min_gap_out = gap;
+  if (prob_out) *prob_out = (n > 1 && gap) ? 1.0 / (double)gap : 0.0;
+  return 0;
+}
+
+int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint64_t n_lookup,
+                    double* insert_seconds, double* lookup_seconds, uint64_t* found_out) {
+  if (!s || batch == 0) { set_error("kc_fpset_stress: bad argument"); return -EINVAL; }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = s->stream;
+  KC_TRY(s->fs.reserve(n, st));
+  hipEvent_t e0, e1, e2;
+  KC_HIP_TRY(hipEventCreate(&e0));
+  KC_HIP_TRY(hipEventCreate(&e1));
+  KC_HIP_TRY(hipEventCreate(&e2));
+  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  KC_HIP_TRY(hipEventRecord(e0, st));
+  for (uint64_t off = 0; off < n; off += batch) {
+    const uint64_t m = std::min(batch, n - off);
+    hipLaunchKernelGGL(k_stress_insert, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, seed,
+                       off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+  }
+  KC_HIP_TRY(hipEventRecord(e1, st));
+  for (uint64_t off = 0; off < n_lookup; off += batch) {
+    const uint64_t m = std::min(batch, n_lookup - off);
+    hipLaunchKernelGGL(k_stress_lookup, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
+                       seed + 0, n, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+  }
+  KC_HIP_TRY(hipEventRecord(e2, st));
+  KC_HIP_TRY(hipGetLastError());
+  unsigned long long stats[4];
+  KC_HIP_TRY(hipMemcpyAsync(stats, s->d_stats, sizeof stats, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  float ms1 = 0, ms2 = 0;
+  KC_HIP_TRY(hipEventElapsedTime(&ms1, e0, e1));
+  KC_HIP_TRY(hipEventElapsedTime(&ms2, e1, e2));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(e2);
+  s->fs.count += stats[0];
+  if (insert_seconds) *insert_seconds = ms1 * 1e-3;
+  if (lookup_seconds) *lookup_seconds = ms2 * 1e-3;
+  if (found_out) *found_out = stats[2];
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// fpset_dev.h — device-side fingerprint set primitives (HBM, gfx950).
+//
+// Two tables:
+//
+//  * FPSet (the drop-in for TLC's tlc2.tool.fp.FPSet, MC.out:5
+//    "OffHeapDiskFPSet"): open addressing over 64-B buckets of 8 u64 slots,
+//    linear probing by bucket.  A probe is one 64-B line read (four 16-B
+//    vector loads by one lane) plus, for a new fingerprint, one 64-bit
+//    atomicCAS into the same line.  Slot value 0 = empty; stored
+//    fingerprints have the MSB clear (TLC's disk FPSets reserve it) and are
+//    never 0 (see normalize()).  Slots are never cleared, so a fingerprint
+//    sits in the first slot that was empty along its probe sequence when it
+//    was inserted — which makes `contains` stop at the first empty slot.
+//
+//  * Batch table (per BFS level chunk / per put_batch call): 16-B entries
+//    {fp, ~key}.  Every candidate CAS-inserts its fp and then atomicMax'es
+//    the complement of its order key, so after the pass each entry holds
+//    the SMALLEST key that produced the fp: the deterministic "first
+//    occurrence" a 1-worker TLC would have seen.  Only that representative
+//    touches the FPSet.  Sized ~2x the batch so it stays in L2/MALL.
+//
+// Visibility: stale L1 copies can only show a slot as empty (0) that was
+// filled in this launch; every such slot is re-checked by the CAS, whose
+// returned value is authoritative (device-scope atomics execute at the
+// memory side on gfx950).  A fingerprint is inserted by at most one lane per
+// launch (the batch representative), so no duplicate can be created.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kc {
+
+struct BatchEntry {
+  unsigned long long fp;
+  unsigned long long nkey;  // ~key; 0 = unclaimed (memset 0 initialises)
+};
+
+__host__ __device__ __forceinline__ uint64_t normalize_fp(uint64_t fp) {
+  fp &= 0x7fffffffffffffffull;
+  return fp ? fp : 1ull;
+}
+
+__device__ __forceinline__ uint64_t bucket_of(uint64_t fp, uint64_t nbuckets) {
+  // multiply-shift on a remixed fp: owner sharding uses the fp's top bits,
+  // so the bucket index must not be a function of those bits alone.
+  return __umul64hi(fp * 0x9e3779b97f4a7c15ull, nbuckets);
+}
+__device__ __forceinline__ uint64_t batch_slot(uint64_t fp, uint64_t mask) {
+  uint64_t h = fp ^ (fp >> 29);
+  h *= 0xbf58476d1ce4e5b9ull;
+  return (h >> 21) & mask;
+}
+
+// Insert: 1 = newly inserted, 0 = already present, -1 = table full.
+__device__ __forceinline__ int fpset_insert(unsigned long long* __restrict__ slots,
+                                            uint64_t nbuckets, uint64_t fp) {
+  uint64_t b = bucket_of(fp, nbuckets);
+  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
+    unsigned long long* bk = slots + b * 8;
+    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(bk);
+    ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
+    unsigned long long e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (e[k] == fp) return 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (e[k] == 0) {
+        const unsigned long long old = atomicCAS(bk + k, 0ull, (unsigned long long)fp);
+        if (old == 0ull) return 1;
+        if (old == fp) return 0;
+      }
+    }
+    b = (b + 1 == nbuckets) ? 0 : b + 1;
+  }
+  return -1;
+}
+
+// Lookup: 1 = present, 0 = absent.
+__device__ __forceinline__ int fpset_contains(const unsigned long long* __restrict__ slots,
+                                              uint64_t nbuckets, uint64_t fp) {
+  uint64_t b = bucket_of(fp, nbuckets);
+  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
+    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(slots + b * 8);
+    ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
+    unsigned long long e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+    bool empty = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (e[k] == fp) return 1;
+      empty |= (e[k] == 0);
+    }
+    if (empty) return 0;
+    b = (b + 1 == nbuckets) ? 0 : b + 1;
+  }
+  return 0;
+}
+
+// Batch table: record (fp, key); keeps the minimum key per fp.
+__device__ __forceinline__ void batch_insert(BatchEntry* __restrict__ t, uint64_t mask,
+                                             uint64_t fp, uint64_t key) {
+  uint64_t i = batch_slot(fp, mask);
+  for (;;) {
+    unsigned long long e = t[i].fp;
+    if (e == 0ull) {
+      e = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (e == 0ull) e = fp;
+    }
+    if (e == fp) {
+      atomicMax(&t[i].nkey, ~(unsigned long long)key);
+      return;
+    }
+    i = (i + 1) & mask;
+  }
+}
+// After the insert pass: is `key` the smallest key recorded for fp?
+__device__ __forceinline__ bool batch_is_rep(const BatchEntry* __restrict__ t, uint64_t mask,
+                                             uint64_t fp, uint64_t key) {
+  uint64_t i = batch_slot(fp, mask);
+  for (;;) {
+    const unsigned long long e = t[i].fp;
+    if (e == fp) return t[i].nkey == ~(unsigned long long)key;
+    if (e == 0ull) return false;  // unreachable: every fp was inserted
+    i = (i + 1) & mask;
+  }
+}
+
+}  // namespace kc

@@ -1,0 +1,35 @@
+// fpset_host.h — host-side owner of an HBM FPSet (used by the engine and by
+// the kc_fpset_* C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fpset_dev.h"
+
+namespace kc {
+
+struct DevFpset {
+  unsigned long long* slots = nullptr;  // nbuckets * 8 u64
+  uint64_t nbuckets = 0;
+  uint64_t count = 0;                   // host-tracked number of stored fps
+  unsigned long long* d_fail = nullptr; // rehash failure counter
+
+  uint64_t capacity() const { return nbuckets * 8; }
+  // allocate for >= min_slots slots (whole buckets), zeroed
+  int init(uint64_t min_slots, hipStream_t st);
+  void release();
+  // grow (rehash into 2x..) so that count + extra <= 75% of capacity
+  int reserve(uint64_t extra, hipStream_t st);
+};
+
+// Batch table used to dedup a batch by minimum order key.
+struct DevBatchTable {
+  BatchEntry* t = nullptr;
+  uint64_t cap = 0;  // allocated entries (power of two)
+  int ensure(uint64_t entries, hipStream_t st);  // grow allocation if needed
+  void release();
+};
+
+uint64_t next_pow2(uint64_t x);
+
+}  // namespace kc

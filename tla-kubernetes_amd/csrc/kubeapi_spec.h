@@ -1,0 +1,578 @@
+// kubeapi_spec.h — KubeAPI.tla lowered to fixed-width packed state vectors.
+//
+// This is the "spec compiler" output for the KubeAPI subset of TLA+: every
+// variable of KubeAPI.tla (VARIABLES apiState, requests, listRequests, pc,
+// stack, op, obj, kind, shouldReconcile; :375,448) is given a finite domain
+// and a fixed bit field, chosen so that equal TLA+ values have equal bits
+// (canonical), and the 22 actions of Next (:471-756) plus TypeOK and
+// OnlyOneVersion (:776-789) become branch-light integer code usable on the
+// GPU (__device__) and on the host (__host__, for trace replay).
+//
+// Parameterisation: the hard-coded process sets {"Client"}, {"PVCController"},
+// {"Server"} (KubeAPI.tla:161,225,268) become NC clients, NP PVC controllers
+// and NS API servers (Model_1 = 1,1,1).  Clients and controllers are the
+// "actors": they call API/ListAPI and appear in version vectors.  Servers
+// have no mutable per-process state (APIStart never writes its own pc,
+// stack, op, obj or kind, :755-756), so they take no bits.
+//
+// Layout, W 64-bit words, W even so a state is whole 16-B
+// vectors:
+//   word 0            apiState: a set over the object universe U (|U| bits)
+//   word 1+a          scalar fields of actor a (see ActorField offsets)
+//   word 1+A+...      listRequests[a].objs, |U| bits per actor, packed
+// Object universe U (values that can be elements of apiState): identity
+// (Secret/foo or PVC/mypvc) x "spec" present x version vector (a subset of
+// the A actors); u = id<<(A+1) | spec<<A | vv.  Scalar object values
+// (obj, stack frame obj, request obj) use objcode: 0 = defaultInitValue,
+// 1+id = the bare record [k |-> .., n |-> ..], 3+u = a record with vv.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define KC_HD __host__ __device__ __forceinline__
+#else
+#define KC_HD inline
+#endif
+
+namespace kc {
+
+// ---------------------------------------------------------------- labels
+// pc values (the PlusCal labels; KubeAPI.tla:467-469 and each action's pc').
+enum Label : int {
+  L_NONE = 0,
+  L_CStart, L_C1, L_C10, L_C11, L_c12, L_C13, L_C2, L_C3, L_C8, L_C6, L_C7, L_C4, L_C5,
+  L_PVCStart, L_PVCListedPVCs, L_PVCHavePVCs, L_PVCDone,
+  L_APIStart,
+  L_DoRequest, L_DoReply, L_DoListRequest, L_DoListReply,
+  L_COUNT
+};
+// action ids, in the order TLC lists them (MC.out:78-621)
+enum Action : int {
+  A_DoRequest = 0, A_DoReply, A_DoListRequest, A_DoListReply, A_CStart, A_C1, A_C10,
+  A_C11, A_c12, A_C13, A_C2, A_C3, A_C8, A_C6, A_C7, A_C4, A_C5, A_PVCStart,
+  A_PVCListedPVCs, A_PVCHavePVCs, A_PVCDone, A_APIStart, A_COUNT
+};
+enum Verb : int { OP_DIV = 0, OP_Create, OP_Get, OP_Update, OP_Delete, OP_Force };
+enum Resp : int { ST_NONE = 0, ST_Pending, ST_Ok, ST_Error };
+enum KindV : int { K_DIV = 0, K_Secret, K_PVC };
+enum Proc : int { PR_NONE = 0, PR_API, PR_ListAPI };
+enum Ident : int { ID_Secret = 0, ID_PVC = 1 };
+
+// error kinds carried in the low byte of an error key
+enum ErrKind : int { E_NONE = 0, E_ASSERT = 1, E_INVARIANT = 2, E_DEADLOCK = 3 };
+
+// run-time switches (MC.tla constants and build-authored variants)
+struct Flags {
+  int can_fail;      // REQUESTS_CAN_FAIL
+  int can_timeout;   // REQUESTS_CAN_TIMEOUT
+  int variant;       // 0 = as written; 1 = Update without HasRead (lost-update bug)
+};
+
+KC_HD constexpr int ceil_log2(int x) { return x <= 1 ? 0 : 1 + ceil_log2((x + 1) / 2); }
+
+KC_HD int popc(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popcll(x);
+#else
+  return __builtin_popcountll(x);
+#endif
+}
+KC_HD int ctz(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ffsll((unsigned long long)x) - 1;
+#else
+  return __builtin_ctzll(x);
+#endif
+}
+// index of the j-th set bit of x (j < popc(x))
+KC_HD int nth_bit(uint64_t x, int j) {
+  for (int k = 0; k < j; ++k) x &= x - 1;
+  return ctz(x);
+}
+KC_HD uint64_t getf(uint64_t w, int off, int n) { return (w >> off) & ((1ull << n) - 1); }
+KC_HD uint64_t setf(uint64_t w, int off, int n, uint64_t v) {
+  const uint64_t m = ((1ull << n) - 1) << off;
+  return (w & ~m) | ((v << off) & m);
+}
+
+template <int NC_, int NP_, int NS_>
+struct Model {
+  static constexpr int NC = NC_, NP = NP_, NS = NS_;
+  static constexpr int A = NC + NP;             // actors (= readers in vv)
+  static constexpr int P = A + NS;              // |ProcSet|
+  static constexpr int UB = A + 2;              // log2 |U|
+  static constexpr int U = 1 << UB;             // object universe size
+  static constexpr int NOBJ = 3 + U;            // objcode values
+  static constexpr int OBJB = ceil_log2(NOBJ);  // objcode bits
+  static_assert(A >= 1 && A <= 4 && NS >= 1, "KubeAPI model: 1..4 actors, >=1 server");
+  static constexpr int OBJ_PER_WORD = 64 / U;   // listRequests objs masks per word
+  static constexpr int OBJ_WORDS = (A + OBJ_PER_WORD - 1) / OBJ_PER_WORD;
+  static constexpr int W_RAW = 1 + A + OBJ_WORDS;
+  static constexpr int W = (W_RAW + 1) & ~1;    // state words (even)
+  static constexpr int MAXSUCC = 32;            // successor slots per state
+
+  // actor word field offsets (LSB first)
+  static constexpr int F_PC = 0, B_PC = 5;
+  static constexpr int F_RQP = F_PC + B_PC, F_RQST = F_RQP + 1, F_RQOP = F_RQST + 2,
+                       F_RQOBJ = F_RQOP + 3;
+  static constexpr int F_LRP = F_RQOBJ + OBJB, F_LRST = F_LRP + 1, F_LRK = F_LRST + 2;
+  static constexpr int F_SD = F_LRK + 2, F_SPROC = F_SD + 1, F_SRET = F_SPROC + 2,
+                       F_SOP = F_SRET + 5, F_SOBJ = F_SOP + 3, F_SKIND = F_SOBJ + OBJB;
+  static constexpr int F_OP = F_SKIND + 2, F_OBJ = F_OP + 3, F_KIND = F_OBJ + OBJB,
+                       F_SR = F_KIND + 2;
+  static constexpr int ACTOR_BITS = F_SR + 1;
+  static_assert(ACTOR_BITS <= 64, "actor word overflow");
+
+  static constexpr uint64_t UMASK = (U == 64) ? ~0ull : ((1ull << U) - 1);
+  // U bits whose identity is `id`: the upper / lower half of U
+  KC_HD static uint64_t id_mask(int id) {
+    const uint64_t half = (1ull << (U / 2)) - 1;
+    return id ? (half << (U / 2)) : half;
+  }
+  KC_HD static uint64_t kind_mask(int kind) {
+    return kind == K_Secret ? id_mask(ID_Secret) : kind == K_PVC ? id_mask(ID_PVC) : 0ull;
+  }
+  KC_HD static int u_id(int u) { return (u >> (A + 1)) & 1; }
+  KC_HD static int u_spec(int u) { return (u >> A) & 1; }
+  KC_HD static int u_vv(int u) { return u & ((1 << A) - 1); }
+  KC_HD static int u_make(int id, int spec, int vv) { return (id << (A + 1)) | (spec << A) | vv; }
+
+  // objcode helpers
+  KC_HD static int oc_bare(int id) { return 1 + id; }
+  KC_HD static int oc_full(int u) { return 3 + u; }
+  KC_HD static bool oc_is_full(int oc) { return oc >= 3; }
+  KC_HD static int oc_u(int oc) { return oc - 3; }
+  KC_HD static int oc_id(int oc) { return oc >= 3 ? u_id(oc - 3) : oc - 1; }
+  // Write(o) == "vv" :> {} @@ o   (KubeAPI.tla:395) — as an element of U
+  KC_HD static int write_u(int oc) {
+    return oc >= 3 ? u_make(u_id(oc - 3), u_spec(oc - 3), 0) : u_make(oc - 1, 0, 0);
+  }
+  // Read(o, c) == [o EXCEPT !.vv = @ \cup {c}]   (:399)
+  KC_HD static int read_u(int u, int c) { return u | (1 << c); }
+
+  struct State { uint64_t w[W]; };
+
+  // ------------------------------------------------------------ accessors
+  // Actor words are selected with unrolled compares rather than s.w[1 + a]:
+  // a runtime index into a register array would spill the state to scratch.
+  KC_HD static uint64_t aw(const State& s, int a) {
+    uint64_t r = s.w[1];
+#pragma unroll
+    for (int k = 1; k < A; ++k) if (a == k) r = s.w[1 + k];
+    return r;
+  }
+  KC_HD static int pc(const State& s, int a) { return (int)getf(aw(s, a), F_PC, B_PC); }
+  KC_HD static int fld(const State& s, int a, int off, int n) { return (int)getf(aw(s, a), off, n); }
+  KC_HD static void put(State& s, int a, int off, int n, int v) {
+#pragma unroll
+    for (int k = 0; k < A; ++k) if (a == k) s.w[1 + k] = setf(s.w[1 + k], off, n, (uint64_t)v);
+  }
+  KC_HD static uint64_t objs(const State& s, int a) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < A; ++k)
+      if (a == k) r = (s.w[1 + A + k / OBJ_PER_WORD] >> ((k % OBJ_PER_WORD) * U)) & UMASK;
+    return r;
+  }
+  KC_HD static void set_objs(State& s, int a, uint64_t v) {
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      if (a == k) {
+        const int wi = 1 + A + k / OBJ_PER_WORD, sh = (k % OBJ_PER_WORD) * U;
+        s.w[wi] = (s.w[wi] & ~(UMASK << sh)) | ((v & UMASK) << sh);
+      }
+    }
+  }
+  KC_HD static bool is_client(int a) { return a < NC; }
+
+  // IsUnboundPVC over a set of U elements (:444-446): PVC identity, no spec
+  KC_HD static uint64_t unbound(uint64_t set) {
+    uint64_t r = 0;
+    for (uint64_t x = set; x; x &= x - 1) {
+      const int u = ctz(x);
+      if (u_id(u) == ID_PVC && !u_spec(u)) r |= 1ull << u;
+    }
+    return r;
+  }
+  // apiState' = {IF IsVersionOf(o, X) THEN Read(o, c) ELSE o : o \in apiState}
+  // restricted to the U bits in `sel`
+  KC_HD static uint64_t read_map(uint64_t api, uint64_t sel, int c) {
+    uint64_t nw = api & ~sel;
+    for (uint64_t x = api & sel; x; x &= x - 1) nw |= 1ull << read_u(ctz(x), c);
+    return nw;
+  }
+
+  // --------------------------------------------------------------- Init
+  // Init (KubeAPI.tla:455-469): 2^NC states, shouldReconcile enumerated as a
+  // binary counter (client 0 least significant, FALSE first).
+  KC_HD static int num_init() { return 1 << NC; }
+  KC_HD static void init_state(int k, State& s) {
+    for (int i = 0; i < W; ++i) s.w[i] = 0;
+    for (int a = 0; a < A; ++a) {
+      put(s, a, F_PC, B_PC, is_client(a) ? L_CStart : L_PVCStart);
+      if (is_client(a)) put(s, a, F_SR, 1, (k >> a) & 1);
+    }
+  }
+
+  // ------------------------------------------------- successor enumeration
+  // Successors are listed in TLC's action order:
+  //   slot a in [0,A)      : DoRequest/DoReply/DoListRequest/DoListReply of actor a
+  //   slot A+a             : the own-label action of actor a (clients, then
+  //                          PVC controllers)
+  //   slot 2A+k, k < NS    : APIStart of server k
+  // At most one action per slot is enabled (pc selects it).  slot_count
+  // returns the slot's successor count, or -1 when evaluating the enabled
+  // action raises an Assert failure (C2 :598, C4 :639, APIStart :740).
+  static constexpr int NSLOT = 2 * A + NS;
+
+  KC_HD static int slot_count(const State& s, int slot, const Flags& f) {
+    if (slot < A) {
+      const int a = slot, p = pc(s, a);
+      const int nb = 1 + (f.can_fail ? 1 : 0) + (f.can_timeout ? 1 : 0);
+      if (p == L_DoRequest || p == L_DoListRequest) return nb;        // :472-480, :500-508
+      if (p == L_DoReply)                                              // :486-490
+        return fld(s, a, F_RQST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
+      if (p == L_DoListReply)                                          // :514-519
+        return fld(s, a, F_LRST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
+      return 0;
+    }
+    if (slot < 2 * A) {
+      const int a = slot - A, p = pc(s, a);
+      if (is_client(a)) {
+        switch (p) {
+          case L_CStart: return 2;                                     // :529-531
+          case L_C1: case L_C10: case L_C11: case L_c12: case L_C13:
+          case L_C3: case L_C8: case L_C7: case L_C5: return 1;
+          case L_C2: return (s.w[0] & id_mask(ID_Secret)) ? 1 : -1;     // :598
+          case L_C4: return (s.w[0] & id_mask(ID_Secret)) ? -1 : 1;     // :639
+          case L_C6: return popc(objs(s, a));                          // :619
+          default: return 0;
+        }
+      }
+      switch (p) {
+        case L_PVCStart: case L_PVCListedPVCs: case L_PVCDone: return 1;
+        case L_PVCHavePVCs: return popc(unbound(objs(s, a)));          // :674
+        default: return 0;
+      }
+    }
+    // APIStart (:698-756): one successor per pending request, then one per
+    // pending list request.  A pending request whose op is not a verb would
+    // hit Assert(FALSE) (:740).
+    int n = 0;
+    for (int c = 0; c < A; ++c) {
+      if (fld(s, c, F_RQP, 1) && fld(s, c, F_RQST, 2) == ST_Pending) {
+        const int op = fld(s, c, F_RQOP, 3);
+        if (op < OP_Create || op > OP_Force) return -1;
+        ++n;
+      }
+    }
+    for (int c = 0; c < A; ++c)
+      if (fld(s, c, F_LRP, 1) && fld(s, c, F_LRST, 2) == ST_Pending) ++n;
+    return n;
+  }
+
+  // Action id of a slot's enabled action.
+  KC_HD static int slot_action(const State& s, int slot) {
+    if (slot >= 2 * A) return A_APIStart;
+    const int a = slot < A ? slot : slot - A, p = pc(s, a);
+    switch (p) {
+      case L_DoRequest: return A_DoRequest;   case L_DoReply: return A_DoReply;
+      case L_DoListRequest: return A_DoListRequest; case L_DoListReply: return A_DoListReply;
+      case L_CStart: return A_CStart; case L_C1: return A_C1; case L_C10: return A_C10;
+      case L_C11: return A_C11; case L_c12: return A_c12; case L_C13: return A_C13;
+      case L_C2: return A_C2; case L_C3: return A_C3; case L_C8: return A_C8;
+      case L_C6: return A_C6; case L_C7: return A_C7; case L_C4: return A_C4;
+      case L_C5: return A_C5; case L_PVCStart: return A_PVCStart;
+      case L_PVCListedPVCs: return A_PVCListedPVCs; case L_PVCHavePVCs: return A_PVCHavePVCs;
+      case L_PVCDone: return A_PVCDone;
+      default: return A_APIStart;
+    }
+  }
+
+  // Successor plan of a state: per-slot counts packed 6 bits each, the total
+  // number of successors and the position of an Assert failure (or -1).
+  struct Plan {
+    uint64_t counts;   // 6 bits per slot
+    int total;
+    int fail_pos;      // successors generated before the failing action, or -1
+    int fail_slot;
+  };
+  static_assert(NSLOT * 6 <= 64, "too many slots");
+  KC_HD static Plan plan(const State& s, const Flags& f) {
+    Plan pl{0, 0, -1, -1};
+#pragma unroll
+    for (int slot = 0; slot < NSLOT; ++slot) {
+      const int c = slot_count(s, slot, f);
+      if (c < 0) { pl.fail_pos = pl.total; pl.fail_slot = slot; break; }
+      pl.counts |= (uint64_t)(c > 63 ? 63 : c) << (6 * slot);
+      pl.total += c;
+    }
+    return pl;
+  }
+  // successor t of a plan -> (slot, index within slot)
+  KC_HD static void locate(const Plan& pl, int t, int& slot, int& j) {
+    int s = 0;
+    for (;;) {
+      const int c = (int)((pl.counts >> (6 * s)) & 63);
+      if (t < c) break;
+      t -= c; ++s;
+    }
+    slot = s; j = t;
+  }
+
+  KC_HD static void push_api(State& t, int a, int ret) {
+    put(t, a, F_SD, 1, 1); put(t, a, F_SPROC, 2, PR_API); put(t, a, F_SRET, 5, ret);
+    put(t, a, F_SOP, 3, fld(t, a, F_OP, 3)); put(t, a, F_SOBJ, OBJB, fld(t, a, F_OBJ, OBJB));
+    put(t, a, F_SKIND, 2, 0);
+  }
+  KC_HD static void push_list(State& t, int a, int ret) {
+    put(t, a, F_SD, 1, 1); put(t, a, F_SPROC, 2, PR_ListAPI); put(t, a, F_SRET, 5, ret);
+    put(t, a, F_SOP, 3, 0); put(t, a, F_SOBJ, OBJB, 0); put(t, a, F_SKIND, 2, fld(t, a, F_KIND, 2));
+  }
+  KC_HD static void pop(State& t, int a) {
+    put(t, a, F_SD, 1, 0); put(t, a, F_SPROC, 2, 0); put(t, a, F_SRET, 5, 0);
+    put(t, a, F_SOP, 3, 0); put(t, a, F_SOBJ, OBJB, 0); put(t, a, F_SKIND, 2, 0);
+  }
+  KC_HD static void call(State& t, int a, int ret, int op, int oc) {
+    push_api(t, a, ret);
+    put(t, a, F_OBJ, OBJB, oc); put(t, a, F_OP, 3, op); put(t, a, F_PC, B_PC, L_DoRequest);
+  }
+
+  // Build successor j of `slot` (KubeAPI.tla:471-756).
+  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t) {
+    for (int i = 0; i < W; ++i) t.w[i] = s.w[i];
+    if (slot < A) {
+      const int a = slot, p = pc(s, a);
+      if (p == L_DoRequest) {                                   // DoRequest :471-483
+        put(t, a, F_RQP, 1, 1); put(t, a, F_RQOP, 3, fld(s, a, F_OP, 3));
+        put(t, a, F_RQOBJ, OBJB, fld(s, a, F_OBJ, OBJB));
+        put(t, a, F_RQST, 2, j == 0 ? ST_Pending : ST_Error);
+        put(t, a, F_PC, B_PC, L_DoReply);
+      } else if (p == L_DoListRequest) {                        // DoListRequest :499-511
+        put(t, a, F_LRP, 1, 1); put(t, a, F_LRK, 2, fld(s, a, F_KIND, 2)); set_objs(t, a, 0);
+        put(t, a, F_LRST, 2, j == 0 ? ST_Pending : ST_Error);
+        put(t, a, F_PC, B_PC, L_DoListReply);
+      } else if (p == L_DoReply) {                              // DoReply :485-495
+        if (j == 1) put(t, a, F_RQST, 2, ST_Error);
+        put(t, a, F_PC, B_PC, fld(s, a, F_SRET, 5)); put(t, a, F_OP, 3, fld(s, a, F_SOP, 3));
+        put(t, a, F_OBJ, OBJB, fld(s, a, F_SOBJ, OBJB));
+        pop(t, a);
+      } else {                                                  // DoListReply :513-524
+        if (j == 1) { set_objs(t, a, 0); put(t, a, F_LRST, 2, ST_Error); }
+        put(t, a, F_PC, B_PC, fld(s, a, F_SRET, 5)); put(t, a, F_KIND, 2, fld(s, a, F_SKIND, 2));
+        pop(t, a);
+      }
+      return;
+    }
+    if (slot < 2 * A) {
+      const int a = slot - A, p = pc(s, a);
+      switch (p) {
+        case L_CStart: {                                        // :528-549
+          const int sr = j == 0 ? 1 : fld(s, a, F_SR, 1);
+          put(t, a, F_SR, 1, sr);
+          if (sr) call(t, a, L_C1, OP_Force, oc_bare(ID_Secret));
+          else {
+            push_list(t, a, L_C3);
+            put(t, a, F_KIND, 2, K_Secret); put(t, a, F_PC, B_PC, L_DoListRequest);
+          }
+          return;
+        }
+        case L_C1:                                              // :551-556
+          put(t, a, F_PC, B_PC, fld(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); return;
+        case L_C10: call(t, a, L_C11, OP_Force, oc_bare(ID_PVC)); return;   // :558-568
+        case L_C11:                                             // :570-575
+          put(t, a, F_PC, B_PC, fld(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); return;
+        case L_c12: call(t, a, L_C13, OP_Get, oc_bare(ID_PVC)); return;     // :577-587
+        case L_C13: {                                           // :589-594
+          bool go = fld(s, a, F_RQST, 2) != ST_Ok;
+          if (!go) {
+            const int oc = fld(s, a, F_RQOBJ, OBJB);
+            go = oc_id(oc) == ID_PVC && !(oc_is_full(oc) && u_spec(oc_u(oc)));
+          }
+          put(t, a, F_PC, B_PC, go ? L_CStart : L_C2); return;
+        }
+        case L_C2: put(t, a, F_SR, 1, 0); put(t, a, F_PC, B_PC, L_C5); return;  // :596-602
+        case L_C3:                                              // :604-609
+          put(t, a, F_PC, B_PC, fld(s, a, F_LRST, 2) != ST_Ok ? L_CStart : L_C8); return;
+        case L_C8: put(t, a, F_PC, B_PC, objs(s, a) == 0 ? L_C4 : L_C6); return; // :611-616
+        case L_C6: {                                            // :618-629
+          const int u = nth_bit(objs(s, a), j);
+          call(t, a, L_C7, OP_Delete, oc_bare(u_id(u)));
+          return;
+        }
+        case L_C7: {                                            // :631-636
+          const bool go = fld(s, a, F_RQST, 2) != ST_Ok || popc(objs(s, a)) > 1;
+          put(t, a, F_PC, B_PC, go ? L_CStart : L_C4); return;
+        }
+        case L_C4: case L_C5: put(t, a, F_PC, B_PC, p == L_C4 ? L_C5 : L_CStart); return;
+        case L_PVCStart:                                        // :655-663
+          push_list(t, a, L_PVCListedPVCs);
+          put(t, a, F_KIND, 2, K_PVC); put(t, a, F_PC, B_PC, L_DoListRequest); return;
+        case L_PVCListedPVCs: {                                 // :665-671
+          const bool go = fld(s, a, F_LRST, 2) != ST_Ok || unbound(objs(s, a)) == 0;
+          put(t, a, F_PC, B_PC, go ? L_PVCStart : L_PVCHavePVCs); return;
+        }
+        case L_PVCHavePVCs: {                                   // :673-688
+          const int u = nth_bit(unbound(objs(s, a)), j);
+          // bound == "spec" :> ("pvname" :> unb.n) @@ unb
+          call(t, a, L_PVCDone, OP_Update, oc_full(u_make(u_id(u), 1, u_vv(u))));
+          return;
+        }
+        default: /* L_PVCDone */ put(t, a, F_PC, B_PC, L_PVCStart); return;  // :690-693
+      }
+    }
+    // APIStart (:698-756)
+    int k = j;
+    for (int c = 0; c < A; ++c) {
+      if (!(fld(s, c, F_RQP, 1) && fld(s, c, F_RQST, 2) == ST_Pending)) continue;
+      if (k-- != 0) continue;
+      const int oc = fld(s, c, F_RQOBJ, OBJB);
+      const int id = oc_id(oc);
+      const uint64_t api = s.w[0], same = api & id_mask(id);
+      int st = ST_Ok;
+      uint64_t nw = api;
+      switch (fld(s, c, F_RQOP, 3)) {
+        case OP_Create:                                         // :700-705
+          if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
+          break;
+        case OP_Force:                                          // :706-715
+          nw = (api & ~same) | (1ull << write_u(oc));
+          break;
+        case OP_Get:                                            // :716-728
+          if (same) {
+            put(t, c, F_RQOBJ, OBJB, oc_full(ctz(same)));       // CHOOSE o \in apiState
+            nw = read_map(api, same, c);
+          } else st = ST_Error;
+          break;
+        case OP_Delete: nw = api & ~same; break;                // :729-731
+        default: {                                              // Update :732-739
+          bool ok = false;
+          for (uint64_t x = same; x; x &= x - 1)
+            if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
+          if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
+        }
+      }
+      t.w[0] = nw;
+      put(t, c, F_RQST, 2, st);
+      return;
+    }
+    for (int c = 0; c < A; ++c) {                               // :745-753
+      if (!(fld(s, c, F_LRP, 1) && fld(s, c, F_LRST, 2) == ST_Pending)) continue;
+      if (k-- != 0) continue;
+      const uint64_t km = kind_mask(fld(s, c, F_LRK, 2)), api = s.w[0];
+      set_objs(t, c, api & km);
+      put(t, c, F_LRST, 2, ST_Ok);
+      t.w[0] = read_map(api, km, c);
+      return;
+    }
+  }
+
+  // ------------------------------------------------------------ invariants
+  // Returns -1 if TypeOK (:776-781) and OnlyOneVersion (:787-789) hold, else
+  // the index of the first violated one in MC.cfg order (0 TypeOK, 1 OOV).
+  KC_HD static int check(const State& s) {
+    for (int c = 0; c < A; ++c) {
+      if (fld(s, c, F_RQP, 1)) {                                // IsValidRequest :426-430
+        const int op = fld(s, c, F_RQOP, 3), st = fld(s, c, F_RQST, 2);
+        if (op < OP_Create || op > OP_Force || fld(s, c, F_RQOBJ, OBJB) == 0 ||
+            st < ST_Pending || st > ST_Error) return 0;
+      }
+      if (fld(s, c, F_LRP, 1)) {                                // IsValidListRequest :432-436
+        const int st = fld(s, c, F_LRST, 2);
+        if ((objs(s, c) & ~kind_mask(fld(s, c, F_LRK, 2))) || st < ST_Pending || st > ST_Error)
+          return 0;
+      }
+    }
+    if (popc(s.w[0] & id_mask(0)) > 1 || popc(s.w[0] & id_mask(1)) > 1) return 1;
+    return -1;
+  }
+
+  // --------------------------------------------------------- fingerprint
+  // 64-bit fingerprint of the canonical packed words, normalised the way the
+  // FPSet stores it: MSB clear (TLC's disk FPSets reserve it), never 0.
+  KC_HD static uint64_t fingerprint(const State& s) {
+    uint64_t h = 0x6a09e667f3bcc909ull ^ (uint64_t)(W * 0x9e3779b97f4a7c15ull);
+    for (int i = 0; i < W_RAW; ++i) {
+      uint64_t k = s.w[i] * 0x87c37b91114253d5ull;
+      k = (k << 31) | (k >> 33);
+      k *= 0x4cf5ad432745937full;
+      h ^= k;
+      h = ((h << 27) | (h >> 37)) * 5 + 0x52dce729ull;
+    }
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    h &= 0x7fffffffffffffffull;
+    return h ? h : 1;
+  }
+
+  // ------------------------------------------------ canonical tuple (ABI)
+  // Interchange form shared with tests (include/kubecheck.h): word 0 =
+  // apiState as a U mask; then 19 words per process: pc, op, obj, kind, sr,
+  // sdepth, sproc, spc, sop, sobj, skind, rq_present, rq_op, rq_status,
+  // rq_obj, lr_present, lr_kind, lr_status, lr_objs.  Object values use the
+  // "oval" byte: def | id<<1 | has_vv<<2 | spec<<3 | vv<<4.
+  static constexpr int TUPLE_PER_PROC = 19;
+  static constexpr int TUPLE_WORDS = 1 + TUPLE_PER_PROC * P;
+  KC_HD static uint64_t oc_to_oval(int oc) {
+    if (oc == 0) return 0;
+    if (oc < 3) return 1u | ((oc - 1) << 1);
+    const int u = oc - 3;
+    return 1u | (u_id(u) << 1) | (1u << 2) | (u_spec(u) << 3) | (u_vv(u) << 4);
+  }
+  KC_HD static int oval_to_oc(uint64_t ov) {
+    if (!(ov & 1)) return 0;
+    const int id = (ov >> 1) & 1, hv = (ov >> 2) & 1, sp = (ov >> 3) & 1, vv = (ov >> 4) & 15;
+    if (!hv) return (sp || vv) ? -1 : 1 + id;
+    return 3 + u_make(id, sp, vv);
+  }
+  KC_HD static void to_tuple(const State& s, uint64_t* o) {
+    o[0] = s.w[0];
+    for (int p = 0; p < P; ++p) {
+      uint64_t* q = o + 1 + TUPLE_PER_PROC * p;
+      for (int k = 0; k < TUPLE_PER_PROC; ++k) q[k] = 0;
+      if (p >= A) { q[0] = L_APIStart; continue; }
+      q[0] = pc(s, p); q[1] = fld(s, p, F_OP, 3); q[2] = oc_to_oval(fld(s, p, F_OBJ, OBJB));
+      q[3] = fld(s, p, F_KIND, 2); q[4] = fld(s, p, F_SR, 1); q[5] = fld(s, p, F_SD, 1);
+      q[6] = fld(s, p, F_SPROC, 2); q[7] = fld(s, p, F_SRET, 5); q[8] = fld(s, p, F_SOP, 3);
+      q[9] = oc_to_oval(fld(s, p, F_SOBJ, OBJB)); q[10] = fld(s, p, F_SKIND, 2);
+      q[11] = fld(s, p, F_RQP, 1); q[12] = fld(s, p, F_RQOP, 3); q[13] = fld(s, p, F_RQST, 2);
+      q[14] = oc_to_oval(fld(s, p, F_RQOBJ, OBJB));
+      q[15] = fld(s, p, F_LRP, 1); q[16] = fld(s, p, F_LRK, 2); q[17] = fld(s, p, F_LRST, 2);
+      q[18] = objs(s, p);
+    }
+  }
+  // returns false if the tuple is outside the lowered domain
+  KC_HD static bool from_tuple(const uint64_t* o, State& s) {
+    for (int i = 0; i < W; ++i) s.w[i] = 0;
+    if (o[0] & ~UMASK) return false;
+    s.w[0] = o[0];
+    for (int p = 0; p < P; ++p) {
+      const uint64_t* q = o + 1 + TUPLE_PER_PROC * p;
+      if (p >= A) {
+        if (q[0] != L_APIStart) return false;
+        for (int k = 1; k < TUPLE_PER_PROC; ++k) if (q[k]) return false;
+        continue;
+      }
+      const int ob = oval_to_oc(q[2]), sob = oval_to_oc(q[9]), rob = oval_to_oc(q[14]);
+      if (ob < 0 || sob < 0 || rob < 0 || (q[18] & ~UMASK)) return false;
+      if (!is_client(p) && q[4]) return false;
+      put(s, p, F_PC, B_PC, (int)q[0]); put(s, p, F_OP, 3, (int)q[1]); put(s, p, F_OBJ, OBJB, ob);
+      put(s, p, F_KIND, 2, (int)q[3]); put(s, p, F_SR, 1, (int)q[4]); put(s, p, F_SD, 1, (int)q[5]);
+      put(s, p, F_SPROC, 2, (int)q[6]); put(s, p, F_SRET, 5, (int)q[7]); put(s, p, F_SOP, 3, (int)q[8]);
+      put(s, p, F_SOBJ, OBJB, sob); put(s, p, F_SKIND, 2, (int)q[10]);
+      put(s, p, F_RQP, 1, (int)q[11]); put(s, p, F_RQOP, 3, (int)q[12]); put(s, p, F_RQST, 2, (int)q[13]);
+      put(s, p, F_RQOBJ, OBJB, rob);
+      put(s, p, F_LRP, 1, (int)q[15]); put(s, p, F_LRK, 2, (int)q[16]); put(s, p, F_LRST, 2, (int)q[17]);
+      set_objs(s, p, q[18]);
+    }
+    return true;
+  }
+};
+
+// Supported instantiations (NC, NP, NS); the engine dispatches on these.
+#define KC_FOR_EACH_MODEL(X) \
+  X(1, 1, 1) X(2, 1, 1) X(1, 2, 1) X(2, 0, 1) X(1, 1, 2) X(1, 3, 1) X(2, 2, 1) X(1, 0, 1) X(0, 1, 1)
+
+}  // namespace kc

@@ -1,0 +1,134 @@
+"""ctypes binding of libkubecheck.so (include/kubecheck.h).
+
+The library is built in-tree (tla-kubernetes_amd/csrc/Makefile ->
+tla-kubernetes_amd/kubecheck/lib/libkubecheck.so).  There is no Python or CPU
+fallback for the model checker: if the library is missing, importing the
+product raises, and engine calls on a machine without a GPU fail with ENODEV.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libkubecheck.so")
+
+KC_NACTIONS = 22
+KC_MAX_LEVELS = 4096
+
+ACTIONS = [
+    "DoRequest", "DoReply", "DoListRequest", "DoListReply", "CStart", "C1", "C10", "C11",
+    "c12", "C13", "C2", "C3", "C8", "C6", "C7", "C4", "C5", "PVCStart", "PVCListedPVCs",
+    "PVCHavePVCs", "PVCDone", "APIStart",
+]
+
+ERR_KINDS = {0: None, 1: "assertion", 2: "invariant", 3: "deadlock"}
+INVARIANTS = {0: "TypeOK", 1: "OnlyOneVersion"}
+
+
+class KcModelConfig(C.Structure):
+    _fields_ = [
+        ("nc", C.c_int), ("np", C.c_int), ("ns", C.c_int),
+        ("can_fail", C.c_int), ("can_timeout", C.c_int), ("check_deadlock", C.c_int),
+        ("variant", C.c_int), ("device", C.c_int), ("keep_trace", C.c_int),
+        ("max_levels", C.c_int), ("fpset_slots", C.c_uint64), ("chunk_states", C.c_uint64),
+        ("verbose", C.c_int),
+    ]
+
+
+class KcResult(C.Structure):
+    _fields_ = [
+        ("init", C.c_uint64), ("generated", C.c_uint64), ("distinct", C.c_uint64),
+        ("queue_left", C.c_uint64), ("depth", C.c_int), ("complete", C.c_int),
+        ("act_gen", C.c_uint64 * KC_NACTIONS), ("act_dist", C.c_uint64 * KC_NACTIONS),
+        ("nlevels", C.c_int), ("level_width", C.c_uint64 * KC_MAX_LEVELS),
+        ("err_kind", C.c_int), ("err_action", C.c_int), ("err_self", C.c_int),
+        ("err_invariant", C.c_int), ("err_level", C.c_int), ("trace_len", C.c_int),
+        ("seconds", C.c_double), ("collision_optimistic", C.c_double),
+        ("fpset_slots", C.c_uint64), ("peak_frontier", C.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) for every symbol of include/kubecheck.h
+_P = C.c_void_p
+_U64P = C.POINTER(C.c_uint64)
+_U8P = C.POINTER(C.c_uint8)
+_IP = C.POINTER(C.c_int)
+SIGNATURES = [
+    ("kc_last_error", C.c_char_p, []),
+    ("kc_abi_version", C.c_int, []),
+    ("kc_build_info", C.c_char_p, []),
+    ("kc_device_count", C.c_int, []),
+    ("kc_fpset_create", C.c_int, [C.c_uint64, C.c_int, C.POINTER(_P)]),
+    ("kc_fpset_destroy", None, [_P]),
+    ("kc_fpset_put_batch", C.c_int, [_P, _U64P, C.c_size_t, _U8P]),
+    ("kc_fpset_contains_batch", C.c_int, [_P, _U64P, C.c_size_t, _U8P]),
+    ("kc_fpset_put_batch_dev", C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    ("kc_fpset_contains_batch_dev", C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    ("kc_fpset_size", C.c_uint64, [_P]),
+    ("kc_fpset_capacity", C.c_uint64, [_P]),
+    ("kc_fpset_check_fps", C.c_int, [_P, _U64P, C.POINTER(C.c_double)]),
+    ("kc_fpset_stress", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                  C.POINTER(C.c_double), C.POINTER(C.c_double), _U64P]),
+    ("kc_squeue_create", C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(_P)]),
+    ("kc_squeue_destroy", None, [_P]),
+    ("kc_squeue_enqueue", C.c_int, [_P, _U64P, C.c_size_t]),
+    ("kc_squeue_dequeue", C.c_int, [_P, _U64P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("kc_squeue_size", C.c_uint64, [_P]),
+    ("kc_model_config_default", None, [C.POINTER(KcModelConfig)]),
+    ("kc_engine_create", C.c_int, [C.POINTER(KcModelConfig), C.POINTER(_P)]),
+    ("kc_engine_destroy", None, [_P]),
+    ("kc_engine_run", C.c_int, [_P, C.POINTER(KcResult)]),
+    ("kc_engine_trace_text", C.c_size_t, [_P, C.c_char_p, C.c_size_t]),
+    ("kc_engine_trace_tuple", C.c_int, [_P, C.c_int, _U64P]),
+    ("kc_engine_level_tuples", C.c_int64, [_P, C.c_int, _U64P, C.c_uint64]),
+    ("kc_engine_capture_level", C.c_int, [_P, C.c_int]),
+    ("kc_engine_kernel_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
+    ("kc_shard_create", C.c_int, [C.POINTER(KcModelConfig), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("kc_shard_init", C.c_int, [_P, _U64P]),
+    ("kc_shard_expand", C.c_int, [_P, _U64P]),
+    ("kc_shard_send_buffer", C.c_int, [_P, C.POINTER(_P), _U64P]),
+    ("kc_shard_recv_buffer", C.c_int, [_P, C.c_uint64, C.POINTER(_P)]),
+    ("kc_shard_insert", C.c_int, [_P, C.c_uint64, _U64P, _U64P]),
+    ("kc_shard_result", C.c_int, [_P, C.POINTER(KcResult)]),
+    ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("kc_spec_init", C.c_int, [C.POINTER(KcModelConfig), _U64P, C.c_int]),
+    ("kc_spec_successors", C.c_int, [C.POINTER(KcModelConfig), _U64P, _IP, _U64P, C.c_int, _IP]),
+    ("kc_spec_check", C.c_int, [C.POINTER(KcModelConfig), _U64P]),
+    ("kc_spec_fingerprint", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
+    ("kc_spec_pack", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
+    ("kc_spec_unpack", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
+]
+
+_lib = None
+
+
+class KubecheckError(RuntimeError):
+    def __init__(self, func: str, code: int, msg: str):
+        super().__init__(f"{func} failed ({code}): {msg}")
+        self.code = code
+
+
+def load() -> C.CDLL:
+    """Load libkubecheck.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libkubecheck.so not found at {LIB_PATH}; build it with "
+            "`make -C tla-kubernetes_amd/csrc` (or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(func: str, rc: int) -> int:
+    if rc < 0:
+        msg = load().kc_last_error()
+        raise KubecheckError(func, rc, msg.decode() if msg else "")
+    return rc
