@@ -110,7 +110,7 @@ typedef struct {
   int can_fail;            /* REQUESTS_CAN_FAIL  (MC.tla:5-7) */
   int can_timeout;         /* REQUESTS_CAN_TIMEOUT (MC.tla:10-12) */
   int check_deadlock;      /* launch:16 */
-  int variant;             /* 0 = KubeAPI.tla as written; 1 = Update w/o HasRead */
+  int variant;             /* 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace */
   int device;              /* HIP device ordinal */
   int keep_trace;          /* parent pointers (TLC's trace file); default 1 */
   int max_levels;          /* 0 = to completion */

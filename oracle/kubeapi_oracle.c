@@ -419,7 +419,10 @@ static void a_APIStart(const model *m, const kstate *s, int self, emitter *e) {
       break;
     case OP_Force:                                                /* :706-715 */
       br(e, KO_B_API_FORCE);
-      if (same) { br(e, KO_B_API_FORCE_REPLACE); t.api = (s->api & ~same) | (1ull << u_of(m, tla_Write(o))); }
+      /* variant 2 (seeded bug): Force adds the new version without removing
+       * the old one, which violates OnlyOneVersion (:787-789) */
+      if (same) { br(e, KO_B_API_FORCE_REPLACE);
+        t.api = (m->cfg.variant == 2 ? s->api : (s->api & ~same)) | (1ull << u_of(m, tla_Write(o))); }
       else { br(e, KO_B_API_FORCE_CREATE); t.api |= 1ull << u_of(m, tla_Write(o)); }
       t.rq_status[c] = ST_Ok;
       break;

@@ -65,7 +65,7 @@ typedef struct {
   int keep_trace;          /* record parent pointers for counterexamples */
   int max_levels;          /* 0 = run to completion */
   uint64_t max_distinct;   /* 0 = unlimited; stop after the level that passes it */
-  int variant;             /* 0 = spec as written; 1 = lost-update bug (no HasRead) */
+  int variant;             /* 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace */
   int fp_bits;             /* 128 (default, 0 means 128) or 64 */
   int fpset_log2;          /* >0: presize the seen-set to 2^k entries (no growth) */
   int progress;            /* print per-level progress to stderr */

@@ -1,0 +1,68 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/kubecheck.h declares, and fails loudly (negative errno + a
+message, no abort) when no GPU is present."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import kubecheck
+from kubecheck import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kubecheck.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_exported():
+    syms = declared_symbols()
+    assert len(syms) >= 40
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (kc_\w+)", out))
+    assert not (set(syms) - exported), set(syms) - exported
+    # and the ctypes table covers them all
+    assert {s for s, _, _ in _lib.SIGNATURES} == set(syms)
+
+
+def test_abi_version_and_info():
+    lib = kubecheck.load()
+    assert lib.kc_abi_version() == 1
+    assert b"gfx950" in lib.kc_build_info()
+
+
+def test_bad_arguments_return_einval():
+    lib = kubecheck.load()
+    assert lib.kc_engine_create(None, None) == -22
+    assert b"NULL" in lib.kc_last_error()
+    cfg = _lib.KcModelConfig()
+    lib.kc_model_config_default(C.byref(cfg))
+    assert (cfg.nc, cfg.np, cfg.ns, cfg.can_fail, cfg.can_timeout, cfg.check_deadlock) == (1, 1, 1, 1, 1, 1)
+    cfg.nc = 7
+    h = C.c_void_p()
+    assert lib.kc_engine_create(C.byref(cfg), C.byref(h)) == -22
+    assert b"unsupported model" in lib.kc_last_error()
+
+
+@pytest.mark.skipif(kubecheck.device_count() > 0, reason="checks the no-GPU failure mode")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(kubecheck.KubecheckError) as e:
+        kubecheck.ModelChecker()
+    assert e.value.code == -19 and "no CPU fallback" in str(e.value)
+    with pytest.raises(kubecheck.KubecheckError):
+        kubecheck.FPSet(1024)
+    with pytest.raises(kubecheck.KubecheckError):
+        kubecheck.StateQueue(4, 16)
+
+
+def test_spec_words():
+    assert kubecheck.Spec(kubecheck.ModelConfig()).state_words == 4        # 32 B per Model_1 state
+    assert kubecheck.Spec(kubecheck.ModelConfig(np=2)).state_words == 6    # 48 B for NP=2
+    assert kubecheck.Spec(kubecheck.ModelConfig()).tuple_words == 1 + 19 * 3

@@ -1,0 +1,123 @@
+"""GPU engine parity: the HIP BFS (through the C-ABI) against the reference's
+recorded run (MC.out) and the CPU oracle, on the same models.  Integer
+counts, level widths, per-action counts, state sets and traces must be
+bit-identical."""
+import numpy as np
+import pytest
+
+import kubecheck
+from kubecheck import ModelChecker, ModelConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def run(**kw):
+    with ModelChecker(ModelConfig(**kw)) as mc:
+        return mc.run()
+
+
+@pytest.fixture(scope="module")
+def model1():
+    return run()
+
+
+def test_model1_matches_mcout(model1, mcout):
+    r = model1
+    assert (r.init, r.generated, r.distinct, r.queue_left, r.depth) == (
+        mcout["init"], mcout["generated"], mcout["distinct"], mcout["queue_left"], mcout["depth"])
+    assert r.complete and r.error is None
+    assert r.act_gen == mcout["act_gen"]                       # MC.out:78-621
+    assert f"{r.collision_optimistic:.1E}" == f"{mcout['collision_optimistic']:.1E}"
+
+
+def test_model1_matches_oracle_order(model1, fixtures):
+    fx = fixtures["model1"]
+    assert model1.level_width == fx["level_width"]
+    # per-action distinct counts follow the sequential (1-worker) BFS order
+    assert model1.act_dist == fx["act_dist"]
+
+
+@pytest.mark.parametrize("level", [2, 37, 51, 124])
+def test_level_state_sets_identical(oracle, level):
+    with ModelChecker(ModelConfig()) as mc:
+        mc.capture_level(level)
+        mc.run()
+        got = mc.level_tuples(level)
+    want = oracle.level_tuples(oracle.config(), level)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)          # same states, same FIFO order
+
+
+@pytest.mark.parametrize("f,t", [(0, 0), (0, 1), (1, 0)])
+def test_constant_variants(fixtures, f, t):
+    r = run(can_fail=f, can_timeout=t)
+    fx = fixtures[f"model1_fail{f}_timeout{t}"]
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+
+
+def test_multi_chunk_and_rehash_paths(model1):
+    # tiny chunks (many k_count_chunks/expand/resolve/emit rounds per level) and
+    # a tiny initial FPSet (repeated rehash) must not change anything
+    r = run(chunk_states=256, fpset_slots=64)
+    assert (r.distinct, r.generated, r.depth) == (model1.distinct, model1.generated, model1.depth)
+    assert r.level_width == model1.level_width
+    assert r.act_gen == model1.act_gen and r.act_dist == model1.act_dist
+    assert r.fpset_slots > 64
+
+
+def test_seeded_assertion_bug_trace(fixtures):
+    # NC=2 clients sharing Secret/foo: C4 Assert (KubeAPI.tla:639-640) fails at depth 10
+    fx = fixtures["nc2"]
+    with ModelChecker(ModelConfig(nc=2)) as mc:
+        r = mc.run()
+    assert r.error == "assertion" and r.error_action == "C4" and r.error_level == 10
+    assert r.trace_len == fx["trace_len"] == 10
+    assert r.level_width == fx["level_width"]
+    assert [list(map(int, t)) for t in r.trace] == fx["trace"]   # the same shortest trace
+    assert "State 10:" in r.trace_text and "Client2" in r.trace_text
+
+
+def test_seeded_invariant_bug_trace(fixtures):
+    # variant 2: Force adds without replacing -> OnlyOneVersion (KubeAPI.tla:787) fails
+    fx = fixtures["variant2"]
+    with ModelChecker(ModelConfig(variant=2)) as mc:
+        r = mc.run()
+    assert r.error == "invariant" and r.error_invariant == "OnlyOneVersion"
+    assert r.trace_len == fx["trace_len"] and r.error_level == fx["err_level"]
+    assert [list(map(int, t)) for t in r.trace] == fx["trace"]
+
+
+@pytest.mark.parametrize("key,kw", [("nc2_np0", dict(nc=2, np=0)), ("ns2", dict(ns=2)),
+                                    ("nc1_np0", dict(np=0)), ("variant1", dict(variant=1))])
+def test_other_models(fixtures, key, kw):
+    fx = fixtures[key]
+    r = run(**kw)
+    assert (r.depth, r.level_width) == (fx["depth"], fx["level_width"])
+    assert (r.error or None) == {0: None, 1: "assertion"}[fx["err_kind"]]
+    if r.error is None:
+        assert (r.distinct, r.generated) == (fx["distinct"], fx["generated"])
+        assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    else:
+        # a level-synchronous BFS finishes the failing level before it stops, so
+        # the partial totals at an error are not comparable (TLC's are not
+        # deterministic either); the error, its level and the trace are.
+        assert (r.error_action, r.error_level, r.trace_len) == (
+            fx["err_action"], fx["err_level"], fx["trace_len"])
+
+
+def test_enlarged_prefix(fixtures):
+    fx = fixtures["np2_40levels"]
+    r = run(np=2, max_levels=40)
+    assert r.level_width == fx["level_width"]
+    assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    assert not r.complete
+
+
+def test_enlarged_full(fixtures):
+    if "np2_full" not in fixtures:
+        pytest.skip("np2_full fixture not generated")
+    fx = fixtures["np2_full"]
+    r = run(np=2, keep_trace=False)
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r.level_width == fx["level_width"]

@@ -66,7 +66,7 @@ enum ErrKind : int { E_NONE = 0, E_ASSERT = 1, E_INVARIANT = 2, E_DEADLOCK = 3 }
 struct Flags {
   int can_fail;      // REQUESTS_CAN_FAIL
   int can_timeout;   // REQUESTS_CAN_TIMEOUT
-  int variant;       // 0 = as written; 1 = Update without HasRead (lost-update bug)
+  int variant;       // 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace
 };
 
 KC_HD constexpr int ceil_log2(int x) { return x <= 1 ? 0 : 1 + ceil_log2((x + 1) / 2); }
@@ -437,7 +437,8 @@ struct Model {
           if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
           break;
         case OP_Force:                                          // :706-715
-          nw = (api & ~same) | (1ull << write_u(oc));
+          // variant 2 (seeded bug): add without replacing -> OnlyOneVersion fails
+          nw = (f.variant == 2 ? api : (api & ~same)) | (1ull << write_u(oc));
           break;
         case OP_Get:                                            // :716-728
           if (same) {
