@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py — distinct states/sec of the KubeAPI BFS model check on MI355X.
+
+One "step" = one complete BFS safety check (TLC's hot path: expand, fingerprint,
+FPSet dedup, invariant checks, parent pointers, next frontier) of the
+BASELINE.json configs[1] model: KubeAPI with enlarged constants — 1 client,
+2 PVC controllers, 1 API server, both REQUESTS_CAN_* TRUE (build-authored
+parameterisation of KubeAPI.tla:161,225,268).  The
+inputs are the model's Init states, so the timed region starts from an empty
+FPSet with nothing precomputed.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload np2|model1|fpset]
+
+N>1 runs one process per GPU (torch.distributed.run) with the state space
+sharded by fingerprint owner and one RCCL all-to-all per BFS level
+(kubecheck.distributed); rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tla-kubernetes_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+WORKLOADS = {
+    # name: (ModelConfig kwargs, description)
+    "np2": (dict(nc=1, np=2, ns=1), "KubeAPI enlarged: NC=1 clients, NP=2 PVC controllers, NS=1 server"),
+    "model1": (dict(nc=1, np=1, ns=1), "KubeAPI toolbox Model_1 (MC.cfg)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="np2", choices=list(WORKLOADS) + ["fpset"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU baseline sample (oracle)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    return ap.parse_args()
+
+
+def state_bytes(kw) -> int:
+    import kubecheck
+
+    return 8 * kubecheck.Spec(kubecheck.ModelConfig(**kw)).state_words
+
+
+def roofline_bfs(times, res, S):
+    """Roofline of the dominant kernel from HIP-event times over the timed steps.
+
+    Algorithmic bytes per unit:
+      resolve: per parent S (state read) + 8 (new-mask/count write); per FPSet
+               probe 64 (one bucket line; the CAS lands in the same line)
+      expand : per parent S; per successor 16 (one batch-table entry)
+      emit   : per parent 8 (mask + offset); per new state S + 9 (frontier
+               write + parent pointer + ordinal)
+    """
+    parents = res["parents"]
+    per_kernel = {
+        "resolve": parents * (S + 8) + res["probes"] * 64,
+        "expand": parents * S + res["succ"] * 16,
+        "emit": parents * 8 + res["new"] * (S + 9),
+        "scan": parents * 8,
+    }
+    name = max(times, key=lambda k: times[k][0])
+    ms, launches = times[name]
+    byts = per_kernel[name]
+    achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return name, {
+        "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+        "kernel": f"k_{name}", "launches": launches,
+        "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2),
+        "bytes_per_launch": int(byts / max(launches, 1)),
+    }
+
+
+def cpu_baseline(kw, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    cfg = pyoracle.config(kw["nc"], kw["np"], kw["ns"], keep_trace=False)
+    rate, done = pyoracle.bench_sample(cfg, seconds)
+    return {"value": round(rate, 1), "unit": "distinct states/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/kubeapi_oracle.c single-threaded BFS of the same model from Init, "
+                      f"stopped after {seconds:.0f} s ({done} distinct states)"}
+
+
+def bench_single(args, kw, desc):
+    import torch
+    import kubecheck
+
+    cfg = kubecheck.ModelConfig(**kw, keep_trace=True, timing=not args.no_timing,
+                                fpset_slots=1 << 20)
+    mc = kubecheck.ModelChecker(cfg)
+    for _ in range(args.warmup):
+        mc.run()
+    torch.cuda.synchronize()
+    times = {"expand": [0.0, 0], "resolve": [0.0, 0], "scan": [0.0, 0], "emit": [0.0, 0]}
+    acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0}
+    t0 = time.perf_counter()
+    results = []
+    for _ in range(args.steps):
+        r = mc.run()
+        results.append(r)
+        kt = mc.kernel_times()
+        for k in times:
+            times[k][0] += kt[k][0]
+            times[k][1] += kt[k][1]
+        acc["parents"] += r.distinct - r.queue_left
+        acc["probes"] += r.fpset_probes
+        acc["succ"] += r.generated - r.init
+        acc["new"] += r.distinct - r.init
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    r = results[-1]
+    assert all((x.distinct, x.generated) == (r.distinct, r.generated) for x in results)
+    assert r.complete and r.error is None
+    out = {
+        "metric": "distinct states/sec (KubeAPI TLC BFS)",
+        "value": round(r.distinct * args.steps / dt, 1),
+        "unit": "distinct states/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt * 1e3 / args.steps, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic (the model's Init states; no external input)",
+        "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
+                   "constants": "REQUESTS_CAN_FAIL=TRUE,REQUESTS_CAN_TIMEOUT=TRUE",
+                   "invariants": "TypeOK,OnlyOneVersion", "distinct": r.distinct,
+                   "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU"},
+    }
+    if not args.no_timing:
+        name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, state_bytes(kw))
+        out["roofline"] = roof
+        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items()}
+    mc.close()
+    return out
+
+
+def bench_fpset(args):
+    import torch
+    import kubecheck
+
+    n = 1 << 30                      # fingerprints inserted per step
+    batch = 1 << 24
+    s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))   # lands at 50% load
+    for _ in range(args.warmup):
+        s.close()
+        s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))
+        s.stress(0x5EED0000, n, batch, n)
+    torch.cuda.synchronize()
+    tin = tlk = 0.0
+    for k in range(args.steps):
+        s.close()
+        s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))
+        ti, tl, found = s.stress(0x5EED0000 + k, n, batch, n)
+        tin += ti
+        tlk += tl
+    gbs = n * args.steps * 64 / tin / 1e9
+    return {
+        "metric": "FPSet probe HBM GB/s (insert)", "value": round(gbs, 1), "unit": "GB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(tin * 1e3 / args.steps, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic splitmix64 fingerprints generated on device",
+        "config": {"workload": f"FPSet stress: {n} inserts + {n} lookups at 50% load, batch {batch}",
+                   "inserts_per_s": round(n * args.steps / tin, 1),
+                   "lookups_per_s": round(n * args.steps / tlk, 1)},
+        "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_stress_insert"},
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and world != 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.workload == "fpset":
+        out = bench_fpset(args)
+    else:
+        kw, desc = WORKLOADS[args.workload]
+        if args.gpus > 1:
+            from kubecheck import distributed
+
+            out = distributed.bench_sharded(args, kw, desc)
+            if out is None:          # not rank 0
+                return
+        else:
+            out = bench_single(args, kw, desc)
+        if args.gpus == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -117,6 +117,7 @@ typedef struct {
   uint64_t fpset_slots;    /* initial FPSet slots; 0 = default */
   uint64_t chunk_states;   /* parents per expansion chunk; 0 = default */
   int verbose;             /* progress lines to stderr */
+  int timing;              /* 1 = time every kernel launch with HIP events */
 } kc_model_config;
 
 typedef struct {
@@ -137,6 +138,9 @@ typedef struct {
   double collision_optimistic; /* TLC's calculated estimate d*(g-d)/2^64 */
   uint64_t fpset_slots;
   uint64_t peak_frontier;
+  uint64_t fpset_probes;   /* FPSet insert probes (level-unique successors) */
+  uint64_t batch_inserts;  /* batch-table inserts (= generated successors) */
+  uint64_t levels_chunks;  /* expansion chunks over the whole run */
 } kc_result;
 
 typedef struct kc_engine kc_engine;
@@ -156,8 +160,8 @@ int kc_engine_trace_tuple(kc_engine *e, int i, uint64_t *out);
 int64_t kc_engine_level_tuples(kc_engine *e, int level, uint64_t *out, uint64_t cap_states);
 /* Ask run() to keep a host copy of level `level`'s packed states. */
 int kc_engine_capture_level(kc_engine *e, int level);
-/* Per-kernel device timings of the last run (ms): expand, resolve, scan,
- * emit; and the number of launches of each. */
+/* Per-kernel device timings of the last run (ms; needs cfg.timing=1):
+ * expand, resolve, scan, emit; and the number of launches of each. */
 int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
 
 /* --------------------------------------------------- Sharded (multi-GPU) */

@@ -80,6 +80,7 @@ class EngineT final : public EngineBase {
  public:
   explicit EngineT(const kc_model_config& cfg) : EngineBase(cfg) {
     flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
+    timing_ = cfg.timing != 0;
   }
   ~EngineT() override { release(); }
 
@@ -124,8 +125,15 @@ class EngineT final : public EngineBase {
       fps[k] = M::fingerprint(init[k]);
       cand += (uint64_t)M::plan(init[k], flags_).total;
     }
+    // the FPSet allocation is kept across runs (cleared each run), like a
+    // TLC FPSet pre-sized with -fpmem; it grows by rehash when needed
     const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
-    KC_TRY(fps_.init(fp_slots, st_));
+    if (fps_.slots && fps_.capacity() >= fp_slots) {
+      KC_HIP_TRY(hipMemsetAsync(fps_.slots, 0, fps_.nbuckets * 64, st_));
+      fps_.count = 0;
+    } else {
+      KC_TRY(fps_.init(fp_slots, st_));
+    }
     KC_TRY(grow_buffer(cur_, cur_cap_, (uint64_t)ni, false, st_));
     KC_TRY(grow_buffer(parent_, par_cap_, (uint64_t)ni + cand, false, st_));
     KC_TRY(grow_buffer(ord_, ord_cap_, (uint64_t)ni + cand, false, st_));
@@ -213,6 +221,8 @@ class EngineT final : public EngineBase {
         // batch table: >= 2x the chunk's candidates, a power of two
         const uint64_t ccand = nchunks > 1 ? chunk_cand_[start / chunk] : cand;
         const uint64_t bcap = next_pow2(2 * ccand + 256);
+        res->batch_inserts += ccand;
+        ++res->levels_chunks;
         KC_TRY(bt_.ensure(bcap, st_));
         KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
         timed(KK_EXPAND, [&] {
@@ -432,6 +442,7 @@ class EngineT final : public EngineBase {
     const double d = (double)res->distinct, gg = (double)res->generated;
     res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
     res->fpset_slots = fps_.capacity();
+    res->fpset_probes = h_ctr_->probes;
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 

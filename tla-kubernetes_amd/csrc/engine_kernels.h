@@ -38,7 +38,8 @@ struct Counters {
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
   unsigned long long batch_used;  // entries claimed in the batch table
-  unsigned long long pad[3];
+  unsigned long long probes;      // FPSet probes (cumulative over the run)
+  unsigned long long pad[2];
 };
 
 template <class M>
@@ -133,12 +134,15 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
           uint64_t nbuckets, uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
           Counters* __restrict__ C) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const typename M::State s = load_state<M>(cur, i);
+  const bool live = i < n;
+  typename M::State s;
+  if (live) s = load_state<M>(cur, i);
+  else for (int k = 0; k < M::W; ++k) s.w[k] = 0;
   const typename M::Plan pl = M::plan(s, f);
   const uint64_t pidx = base + i;
-  const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
+  const int tot = !live ? 0 : pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
   uint32_t mask = 0;
+  unsigned probes = 0;
   for (int t = 0; t < tot; ++t) {
     int slot, j;
     M::locate(pl, t, slot, j);
@@ -146,13 +150,21 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
     M::apply(s, slot, j, f, x);
     const uint64_t fp = M::fingerprint(x);
     if (batch_is_rep(bt, bmask, fp, (pidx << 8) | (uint64_t)t)) {
+      ++probes;
       const int r = fpset_insert(slots, nbuckets, fp);
       if (r == 1) mask |= 1u << t;
       else if (r < 0) atomicAdd(&C->overflow, 1ull);
     }
   }
-  newmask[i] = mask;
-  newcnt[i] = (uint32_t)__popc(mask);
+  if (live) {
+    newmask[i] = mask;
+    newcnt[i] = (uint32_t)__popc(mask);
+  }
+  // probe count: one atomic per wave
+  unsigned long long pw = probes;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
+  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&C->probes, pw);
 }
 
 template <class M>

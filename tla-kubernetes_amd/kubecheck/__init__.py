@@ -50,6 +50,7 @@ class ModelConfig:
     fpset_slots: int = 0
     chunk_states: int = 0
     verbose: int = 0
+    timing: bool = False        # per-kernel HIP-event timing (kernel_times())
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()
@@ -83,6 +84,9 @@ class CheckResult:
     collision_optimistic: float
     fpset_slots: int
     peak_frontier: int
+    fpset_probes: int = 0
+    batch_inserts: int = 0
+    levels_chunks: int = 0
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -104,7 +108,8 @@ def _result(r: KcResult) -> CheckResult:
         error_invariant=INVARIANTS.get(r.err_invariant),
         error_level=r.err_level, trace_len=r.trace_len, seconds=r.seconds,
         collision_optimistic=r.collision_optimistic, fpset_slots=r.fpset_slots,
-        peak_frontier=r.peak_frontier)
+        peak_frontier=r.peak_frontier, fpset_probes=r.fpset_probes,
+        batch_inserts=r.batch_inserts, levels_chunks=r.levels_chunks)
 
 
 class ModelChecker:

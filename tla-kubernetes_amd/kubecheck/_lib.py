@@ -31,7 +31,7 @@ class KcModelConfig(C.Structure):
         ("can_fail", C.c_int), ("can_timeout", C.c_int), ("check_deadlock", C.c_int),
         ("variant", C.c_int), ("device", C.c_int), ("keep_trace", C.c_int),
         ("max_levels", C.c_int), ("fpset_slots", C.c_uint64), ("chunk_states", C.c_uint64),
-        ("verbose", C.c_int),
+        ("verbose", C.c_int), ("timing", C.c_int),
     ]
 
 
@@ -45,6 +45,8 @@ class KcResult(C.Structure):
         ("err_invariant", C.c_int), ("err_level", C.c_int), ("trace_len", C.c_int),
         ("seconds", C.c_double), ("collision_optimistic", C.c_double),
         ("fpset_slots", C.c_uint64), ("peak_frontier", C.c_uint64),
+        ("fpset_probes", C.c_uint64), ("batch_inserts", C.c_uint64),
+        ("levels_chunks", C.c_uint64),
     ]
 
 
