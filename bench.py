@@ -45,6 +45,7 @@ def parse():
                     help="budget of the CPU baseline sample (oracle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
     return ap.parse_args()
 
 
@@ -100,7 +101,7 @@ def bench_single(args, kw, desc):
     import kubecheck
 
     cfg = kubecheck.ModelConfig(**kw, keep_trace=True, timing=not args.no_timing,
-                                fpset_slots=1 << 20)
+                                fpset_slots=1 << 20, chunk_states=args.chunk)
     mc = kubecheck.ModelChecker(cfg)
     for _ in range(args.warmup):
         mc.run()
@@ -136,7 +137,8 @@ def bench_single(args, kw, desc):
         "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
                    "constants": "REQUESTS_CAN_FAIL=TRUE,REQUESTS_CAN_TIMEOUT=TRUE",
                    "invariants": "TypeOK,OnlyOneVersion", "distinct": r.distinct,
-                   "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU"},
+                   "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU",
+                   "fpset_probes": r.fpset_probes, "chunks": r.levels_chunks},
     }
     if not args.no_timing:
         name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, state_bytes(kw))

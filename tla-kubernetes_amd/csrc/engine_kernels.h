@@ -37,7 +37,7 @@ struct Counters {
   unsigned long long next_cand;   // successors of the new states (next level's work)
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
-  unsigned long long batch_used;  // entries claimed in the batch table
+  unsigned long long batch_used;  // (unused)
   unsigned long long probes;      // FPSet probes (cumulative over the run)
   unsigned long long pad[2];
 };
@@ -64,21 +64,25 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 }
 
 // batch_insert with a bounded probe: returns false if the table is full.
+// One 16-B load reads {fp, ~key}; the atomicMax is skipped when the stored
+// ~key already dominates (nkey only grows, so a stale read is a lower bound).
 __device__ __forceinline__ bool batch_insert_bounded(BatchEntry* __restrict__ t, uint64_t mask,
-                                                     uint64_t fp, uint64_t key,
-                                                     unsigned long long* used) {
+                                                     uint64_t fp, uint64_t key) {
+  const unsigned long long nk = ~(unsigned long long)key;
   uint64_t i = batch_slot(fp, mask);
   for (uint64_t probe = 0; probe <= mask; ++probe) {
-    unsigned long long e = t[i].fp;
-    if (e == 0ull) {
-      e = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
-      if (e == 0ull) {
-        atomicAdd(used, 1ull);
-        e = fp;
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&t[i]);
+    unsigned long long efp = e.x, ekey = e.y;
+    if (efp == 0ull) {
+      efp = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (efp == 0ull) {
+        atomicMax(&t[i].nkey, nk);
+        return true;
       }
+      ekey = 0;
     }
-    if (e == fp) {
-      atomicMax(&t[i].nkey, ~(unsigned long long)key);
+    if (efp == fp) {
+      if (ekey < nk) atomicMax(&t[i].nkey, nk);
       return true;
     }
     i = (i + 1) & mask;
@@ -117,8 +121,7 @@ k_expand(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, F
       M::locate(pl, t, slot, j);
       typename M::State x;
       M::apply(s, slot, j, f, x);
-      if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t,
-                                &C->batch_used))
+      if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t))
         atomicAdd(&C->overflow, 1ull);
     }
   }

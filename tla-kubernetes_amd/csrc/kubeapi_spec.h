@@ -28,6 +28,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define KC_HD __host__ __device__ __forceinline__
@@ -96,6 +98,15 @@ KC_HD uint64_t setf(uint64_t w, int off, int n, uint64_t v) {
   return (w & ~m) | ((v << off) & m);
 }
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [0, N).
+template <int N, int I = 0, class F>
+KC_HD void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 template <int NC_, int NP_, int NS_>
 struct Model {
   static constexpr int NC = NC_, NP = NP_, NS = NS_;
@@ -154,37 +165,95 @@ struct Model {
   struct State { uint64_t w[W]; };
 
   // ------------------------------------------------------------ accessors
-  // Actor words are selected with unrolled compares rather than s.w[1 + a]:
-  // a runtime index into a register array would spill the state to scratch.
-  KC_HD static uint64_t aw(const State& s, int a) {
+  // Every actor index used on the device is a compile-time constant (actor
+  // templates + static_for): a runtime index into State::w — including the
+  // select-of-offsets InstCombine makes out of a compare chain — would pin
+  // the state in scratch memory.
+  template <int a> KC_HD static uint64_t aw(const State& s) { return s.w[1 + a]; }
+  template <int a> KC_HD static int pc(const State& s) { return (int)getf(s.w[1 + a], F_PC, B_PC); }
+  template <int a> KC_HD static int fld(const State& s, int off, int n) {
+    return (int)getf(s.w[1 + a], off, n);
+  }
+  template <int a> KC_HD static void put(State& s, int off, int n, int v) {
+    s.w[1 + a] = setf(s.w[1 + a], off, n, (uint64_t)v);
+  }
+  template <int a> KC_HD static uint64_t objs(const State& s) {
+    constexpr int wi = 1 + A + a / OBJ_PER_WORD, sh = (a % OBJ_PER_WORD) * U;
+    return (s.w[wi] >> sh) & UMASK;
+  }
+  template <int a> KC_HD static void set_objs(State& s, uint64_t v) {
+    constexpr int wi = 1 + A + a / OBJ_PER_WORD, sh = (a % OBJ_PER_WORD) * U;
+    s.w[wi] = (s.w[wi] & ~(UMASK << sh)) | ((v & UMASK) << sh);
+  }
+  KC_HD static constexpr bool is_client(int a) { return a < NC; }
+
+  // Runtime-actor accessors for the (single-copy) action bodies of apply():
+  // each candidate word passes through an empty asm so it is a VALUE, and
+  // the actor is chosen with selects on values; without the barrier
+  // InstCombine turns the chain into a load from a select'ed offset, which
+  // forces the whole state into scratch.
+  KC_HD static void opaque(uint64_t& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(x));
+#else
+    (void)x;
+#endif
+  }
+  KC_HD static uint64_t aw_d(const State& s, int a) {
     uint64_t r = s.w[1];
 #pragma unroll
-    for (int k = 1; k < A; ++k) if (a == k) r = s.w[1 + k];
+    for (int k = 1; k < A; ++k) {
+      uint64_t v = s.w[1 + k];
+      opaque(v);
+      r = (a == k) ? v : r;
+    }
     return r;
   }
-  KC_HD static int pc(const State& s, int a) { return (int)getf(aw(s, a), F_PC, B_PC); }
-  KC_HD static int fld(const State& s, int a, int off, int n) { return (int)getf(aw(s, a), off, n); }
-  KC_HD static void put(State& s, int a, int off, int n, int v) {
-#pragma unroll
-    for (int k = 0; k < A; ++k) if (a == k) s.w[1 + k] = setf(s.w[1 + k], off, n, (uint64_t)v);
-  }
-  KC_HD static uint64_t objs(const State& s, int a) {
-    uint64_t r = 0;
-#pragma unroll
-    for (int k = 0; k < A; ++k)
-      if (a == k) r = (s.w[1 + A + k / OBJ_PER_WORD] >> ((k % OBJ_PER_WORD) * U)) & UMASK;
-    return r;
-  }
-  KC_HD static void set_objs(State& s, int a, uint64_t v) {
+  KC_HD static int pc_d(const State& s, int a) { return (int)getf(aw_d(s, a), F_PC, B_PC); }
+  KC_HD static int fld_d(const State& s, int a, int off, int n) { return (int)getf(aw_d(s, a), off, n); }
+  KC_HD static void put_d(State& s, int a, int off, int n, int v) {
 #pragma unroll
     for (int k = 0; k < A; ++k) {
-      if (a == k) {
-        const int wi = 1 + A + k / OBJ_PER_WORD, sh = (k % OBJ_PER_WORD) * U;
-        s.w[wi] = (s.w[wi] & ~(UMASK << sh)) | ((v & UMASK) << sh);
-      }
+      const uint64_t w = s.w[1 + k];
+      uint64_t nw = setf(w, off, n, (uint64_t)v);
+      opaque(nw);
+      s.w[1 + k] = (a == k) ? nw : w;
     }
   }
-  KC_HD static bool is_client(int a) { return a < NC; }
+  KC_HD static uint64_t objs_d(const State& s, int a) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      uint64_t v = (s.w[1 + A + k / OBJ_PER_WORD] >> ((k % OBJ_PER_WORD) * U)) & UMASK;
+      opaque(v);
+      r = (a == k) ? v : r;
+    }
+    return r;
+  }
+  KC_HD static void set_objs_d(State& s, int a, uint64_t v) {
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      const int wi = 1 + A + k / OBJ_PER_WORD, sh = (k % OBJ_PER_WORD) * U;
+      const uint64_t w = s.w[wi];
+      uint64_t nw = (w & ~(UMASK << sh)) | ((v & UMASK) << sh);
+      opaque(nw);
+      s.w[wi] = (a == k) ? nw : w;
+    }
+  }
+
+  // Host-only runtime-index views (tuple conversion, printing).
+  static uint64_t aw_rt(const State& s, int a) { return s.w[1 + a]; }
+  static uint64_t objs_rt(const State& s, int a) {
+    return (s.w[1 + A + a / OBJ_PER_WORD] >> ((a % OBJ_PER_WORD) * U)) & UMASK;
+  }
+  static int fld_rt(const State& s, int a, int off, int n) { return (int)getf(s.w[1 + a], off, n); }
+  static void put_rt(State& s, int a, int off, int n, int v) {
+    s.w[1 + a] = setf(s.w[1 + a], off, n, (uint64_t)v);
+  }
+  static void set_objs_rt(State& s, int a, uint64_t v) {
+    const int wi = 1 + A + a / OBJ_PER_WORD, sh = (a % OBJ_PER_WORD) * U;
+    s.w[wi] = (s.w[wi] & ~(UMASK << sh)) | ((v & UMASK) << sh);
+  }
 
   // IsUnboundPVC over a set of U elements (:444-446): PVC identity, no spec
   KC_HD static uint64_t unbound(uint64_t set) {
@@ -208,11 +277,13 @@ struct Model {
   // binary counter (client 0 least significant, FALSE first).
   KC_HD static int num_init() { return 1 << NC; }
   KC_HD static void init_state(int k, State& s) {
+#pragma unroll
     for (int i = 0; i < W; ++i) s.w[i] = 0;
-    for (int a = 0; a < A; ++a) {
-      put(s, a, F_PC, B_PC, is_client(a) ? L_CStart : L_PVCStart);
-      if (is_client(a)) put(s, a, F_SR, 1, (k >> a) & 1);
-    }
+    static_for<A>([&](auto AI) {
+      constexpr int a = AI;
+      put<a>(s, F_PC, B_PC, is_client(a) ? L_CStart : L_PVCStart);
+      if (is_client(a)) put<a>(s, F_SR, 1, (k >> a) & 1);
+    });
   }
 
   // ------------------------------------------------- successor enumeration
@@ -226,68 +297,88 @@ struct Model {
   // action raises an Assert failure (C2 :598, C4 :639, APIStart :740).
   static constexpr int NSLOT = 2 * A + NS;
 
-  KC_HD static int slot_count(const State& s, int slot, const Flags& f) {
-    if (slot < A) {
-      const int a = slot, p = pc(s, a);
+  template <int slot>
+  KC_HD static int slot_count(const State& s, const Flags& f) {
+    if constexpr (slot < A) {
+      constexpr int a = slot;
+      const int p = pc<a>(s);
       const int nb = 1 + (f.can_fail ? 1 : 0) + (f.can_timeout ? 1 : 0);
       if (p == L_DoRequest || p == L_DoListRequest) return nb;        // :472-480, :500-508
       if (p == L_DoReply)                                              // :486-490
-        return fld(s, a, F_RQST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
+        return fld<a>(s, F_RQST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
       if (p == L_DoListReply)                                          // :514-519
-        return fld(s, a, F_LRST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
+        return fld<a>(s, F_LRST, 2) != ST_Pending ? 1 + (f.can_timeout ? 1 : 0) : 0;
       return 0;
-    }
-    if (slot < 2 * A) {
-      const int a = slot - A, p = pc(s, a);
-      if (is_client(a)) {
+    } else if constexpr (slot < 2 * A) {
+      constexpr int a = slot - A;
+      const int p = pc<a>(s);
+      if constexpr (is_client(a)) {
         switch (p) {
           case L_CStart: return 2;                                     // :529-531
           case L_C1: case L_C10: case L_C11: case L_c12: case L_C13:
           case L_C3: case L_C8: case L_C7: case L_C5: return 1;
           case L_C2: return (s.w[0] & id_mask(ID_Secret)) ? 1 : -1;     // :598
           case L_C4: return (s.w[0] & id_mask(ID_Secret)) ? -1 : 1;     // :639
-          case L_C6: return popc(objs(s, a));                          // :619
+          case L_C6: return popc(objs<a>(s));                          // :619
+          default: return 0;
+        }
+      } else {
+        switch (p) {
+          case L_PVCStart: case L_PVCListedPVCs: case L_PVCDone: return 1;
+          case L_PVCHavePVCs: return popc(unbound(objs<a>(s)));        // :674
           default: return 0;
         }
       }
-      switch (p) {
-        case L_PVCStart: case L_PVCListedPVCs: case L_PVCDone: return 1;
-        case L_PVCHavePVCs: return popc(unbound(objs(s, a)));          // :674
-        default: return 0;
-      }
+    } else {
+      // APIStart (:698-756): one successor per pending request, then one per
+      // pending list request.  A pending request whose op is not a verb
+      // would hit Assert(FALSE) (:740).
+      int n = 0;
+      bool bad = false;
+      static_for<A>([&](auto CI) {
+        constexpr int c = CI;
+        if (fld<c>(s, F_RQP, 1) && fld<c>(s, F_RQST, 2) == ST_Pending) {
+          const int op = fld<c>(s, F_RQOP, 3);
+          if (op < OP_Create || op > OP_Force) bad = true;
+          ++n;
+        }
+      });
+      if (bad) return -1;
+      static_for<A>([&](auto CI) {
+        constexpr int c = CI;
+        if (fld<c>(s, F_LRP, 1) && fld<c>(s, F_LRST, 2) == ST_Pending) ++n;
+      });
+      return n;
     }
-    // APIStart (:698-756): one successor per pending request, then one per
-    // pending list request.  A pending request whose op is not a verb would
-    // hit Assert(FALSE) (:740).
-    int n = 0;
-    for (int c = 0; c < A; ++c) {
-      if (fld(s, c, F_RQP, 1) && fld(s, c, F_RQST, 2) == ST_Pending) {
-        const int op = fld(s, c, F_RQOP, 3);
-        if (op < OP_Create || op > OP_Force) return -1;
-        ++n;
-      }
-    }
-    for (int c = 0; c < A; ++c)
-      if (fld(s, c, F_LRP, 1) && fld(s, c, F_LRST, 2) == ST_Pending) ++n;
-    return n;
   }
 
   // Action id of a slot's enabled action.
-  KC_HD static int slot_action(const State& s, int slot) {
-    if (slot >= 2 * A) return A_APIStart;
-    const int a = slot < A ? slot : slot - A, p = pc(s, a);
-    switch (p) {
-      case L_DoRequest: return A_DoRequest;   case L_DoReply: return A_DoReply;
-      case L_DoListRequest: return A_DoListRequest; case L_DoListReply: return A_DoListReply;
-      case L_CStart: return A_CStart; case L_C1: return A_C1; case L_C10: return A_C10;
-      case L_C11: return A_C11; case L_c12: return A_c12; case L_C13: return A_C13;
-      case L_C2: return A_C2; case L_C3: return A_C3; case L_C8: return A_C8;
-      case L_C6: return A_C6; case L_C7: return A_C7; case L_C4: return A_C4;
-      case L_C5: return A_C5; case L_PVCStart: return A_PVCStart;
-      case L_PVCListedPVCs: return A_PVCListedPVCs; case L_PVCHavePVCs: return A_PVCHavePVCs;
-      case L_PVCDone: return A_PVCDone;
-      default: return A_APIStart;
+  template <int slot>
+  KC_HD static int slot_action_t(const State& s) {
+    if constexpr (slot >= 2 * A) {
+      return A_APIStart;
+    } else {
+      constexpr int a = slot < A ? slot : slot - A;
+      switch (pc<a>(s)) {
+        case L_DoRequest: return A_DoRequest;   case L_DoReply: return A_DoReply;
+        case L_DoListRequest: return A_DoListRequest; case L_DoListReply: return A_DoListReply;
+        case L_CStart: return A_CStart; case L_C1: return A_C1; case L_C10: return A_C10;
+        case L_C11: return A_C11; case L_c12: return A_c12; case L_C13: return A_C13;
+        case L_C2: return A_C2; case L_C3: return A_C3; case L_C8: return A_C8;
+        case L_C6: return A_C6; case L_C7: return A_C7; case L_C4: return A_C4;
+        case L_C5: return A_C5; case L_PVCStart: return A_PVCStart;
+        case L_PVCListedPVCs: return A_PVCListedPVCs; case L_PVCHavePVCs: return A_PVCHavePVCs;
+        case L_PVCDone: return A_PVCDone;
+        default: return A_APIStart;
+      }
     }
+  }
+  KC_HD static int slot_action(const State& s, int slot) {
+    int r = A_APIStart;
+    static_for<NSLOT>([&](auto SI) {
+      if (slot == (int)SI) r = slot_action_t<SI>(s);
+    });
+    return r;
   }
 
   // Successor plan of a state: per-slot counts packed 6 bits each, the total
@@ -301,13 +392,18 @@ struct Model {
   static_assert(NSLOT * 6 <= 64, "too many slots");
   KC_HD static Plan plan(const State& s, const Flags& f) {
     Plan pl{0, 0, -1, -1};
-#pragma unroll
-    for (int slot = 0; slot < NSLOT; ++slot) {
-      const int c = slot_count(s, slot, f);
-      if (c < 0) { pl.fail_pos = pl.total; pl.fail_slot = slot; break; }
+    static_for<NSLOT>([&](auto SI) {
+      constexpr int slot = SI;
+      if (pl.fail_pos >= 0) return;
+      const int c = slot_count<slot>(s, f);
+      if (c < 0) {
+        pl.fail_pos = pl.total;
+        pl.fail_slot = slot;
+        return;
+      }
       pl.counts |= (uint64_t)(c > 63 ? 63 : c) << (6 * slot);
       pl.total += c;
-    }
+    });
     return pl;
   }
   // successor t of a plan -> (slot, index within slot)
@@ -316,175 +412,193 @@ struct Model {
     for (;;) {
       const int c = (int)((pl.counts >> (6 * s)) & 63);
       if (t < c) break;
-      t -= c; ++s;
+      t -= c;
+      ++s;
     }
-    slot = s; j = t;
+    slot = s;
+    j = t;
   }
 
   KC_HD static void push_api(State& t, int a, int ret) {
-    put(t, a, F_SD, 1, 1); put(t, a, F_SPROC, 2, PR_API); put(t, a, F_SRET, 5, ret);
-    put(t, a, F_SOP, 3, fld(t, a, F_OP, 3)); put(t, a, F_SOBJ, OBJB, fld(t, a, F_OBJ, OBJB));
-    put(t, a, F_SKIND, 2, 0);
+    put_d(t, a, F_SD, 1, 1); put_d(t, a, F_SPROC, 2, PR_API); put_d(t, a, F_SRET, 5, ret);
+    put_d(t, a, F_SOP, 3, fld_d(t, a, F_OP, 3)); put_d(t, a, F_SOBJ, OBJB, fld_d(t, a, F_OBJ, OBJB));
+    put_d(t, a, F_SKIND, 2, 0);
   }
   KC_HD static void push_list(State& t, int a, int ret) {
-    put(t, a, F_SD, 1, 1); put(t, a, F_SPROC, 2, PR_ListAPI); put(t, a, F_SRET, 5, ret);
-    put(t, a, F_SOP, 3, 0); put(t, a, F_SOBJ, OBJB, 0); put(t, a, F_SKIND, 2, fld(t, a, F_KIND, 2));
+    put_d(t, a, F_SD, 1, 1); put_d(t, a, F_SPROC, 2, PR_ListAPI); put_d(t, a, F_SRET, 5, ret);
+    put_d(t, a, F_SOP, 3, 0); put_d(t, a, F_SOBJ, OBJB, 0); put_d(t, a, F_SKIND, 2, fld_d(t, a, F_KIND, 2));
   }
   KC_HD static void pop(State& t, int a) {
-    put(t, a, F_SD, 1, 0); put(t, a, F_SPROC, 2, 0); put(t, a, F_SRET, 5, 0);
-    put(t, a, F_SOP, 3, 0); put(t, a, F_SOBJ, OBJB, 0); put(t, a, F_SKIND, 2, 0);
+    put_d(t, a, F_SD, 1, 0); put_d(t, a, F_SPROC, 2, 0); put_d(t, a, F_SRET, 5, 0);
+    put_d(t, a, F_SOP, 3, 0); put_d(t, a, F_SOBJ, OBJB, 0); put_d(t, a, F_SKIND, 2, 0);
   }
   KC_HD static void call(State& t, int a, int ret, int op, int oc) {
     push_api(t, a, ret);
-    put(t, a, F_OBJ, OBJB, oc); put(t, a, F_OP, 3, op); put(t, a, F_PC, B_PC, L_DoRequest);
+    put_d(t, a, F_OBJ, OBJB, oc); put_d(t, a, F_OP, 3, op); put_d(t, a, F_PC, B_PC, L_DoRequest);
   }
 
-  // Build successor j of `slot` (KubeAPI.tla:471-756).
-  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t) {
-    for (int i = 0; i < W; ++i) t.w[i] = s.w[i];
+  // Build successor j of slot `slot` into t (t starts as a copy of s).  One
+  // copy of every action body, indexed by the runtime actor (apply is the
+  // part of the kernel that runs once per successor).
+  KC_HD static void apply_rt(const State& s, int slot, int j, const Flags& f, State& t) {
     if (slot < A) {
-      const int a = slot, p = pc(s, a);
+      const int a = slot;
+      const int p = pc_d(s, a);
       if (p == L_DoRequest) {                                   // DoRequest :471-483
-        put(t, a, F_RQP, 1, 1); put(t, a, F_RQOP, 3, fld(s, a, F_OP, 3));
-        put(t, a, F_RQOBJ, OBJB, fld(s, a, F_OBJ, OBJB));
-        put(t, a, F_RQST, 2, j == 0 ? ST_Pending : ST_Error);
-        put(t, a, F_PC, B_PC, L_DoReply);
+        put_d(t, a, F_RQP, 1, 1); put_d(t, a, F_RQOP, 3, fld_d(s, a, F_OP, 3));
+        put_d(t, a, F_RQOBJ, OBJB, fld_d(s, a, F_OBJ, OBJB));
+        put_d(t, a, F_RQST, 2, j == 0 ? ST_Pending : ST_Error);
+        put_d(t, a, F_PC, B_PC, L_DoReply);
       } else if (p == L_DoListRequest) {                        // DoListRequest :499-511
-        put(t, a, F_LRP, 1, 1); put(t, a, F_LRK, 2, fld(s, a, F_KIND, 2)); set_objs(t, a, 0);
-        put(t, a, F_LRST, 2, j == 0 ? ST_Pending : ST_Error);
-        put(t, a, F_PC, B_PC, L_DoListReply);
+        put_d(t, a, F_LRP, 1, 1); put_d(t, a, F_LRK, 2, fld_d(s, a, F_KIND, 2)); set_objs_d(t, a, 0);
+        put_d(t, a, F_LRST, 2, j == 0 ? ST_Pending : ST_Error);
+        put_d(t, a, F_PC, B_PC, L_DoListReply);
       } else if (p == L_DoReply) {                              // DoReply :485-495
-        if (j == 1) put(t, a, F_RQST, 2, ST_Error);
-        put(t, a, F_PC, B_PC, fld(s, a, F_SRET, 5)); put(t, a, F_OP, 3, fld(s, a, F_SOP, 3));
-        put(t, a, F_OBJ, OBJB, fld(s, a, F_SOBJ, OBJB));
+        if (j == 1) put_d(t, a, F_RQST, 2, ST_Error);
+        put_d(t, a, F_PC, B_PC, fld_d(s, a, F_SRET, 5)); put_d(t, a, F_OP, 3, fld_d(s, a, F_SOP, 3));
+        put_d(t, a, F_OBJ, OBJB, fld_d(s, a, F_SOBJ, OBJB));
         pop(t, a);
       } else {                                                  // DoListReply :513-524
-        if (j == 1) { set_objs(t, a, 0); put(t, a, F_LRST, 2, ST_Error); }
-        put(t, a, F_PC, B_PC, fld(s, a, F_SRET, 5)); put(t, a, F_KIND, 2, fld(s, a, F_SKIND, 2));
+        if (j == 1) { set_objs_d(t, a, 0); put_d(t, a, F_LRST, 2, ST_Error); }
+        put_d(t, a, F_PC, B_PC, fld_d(s, a, F_SRET, 5)); put_d(t, a, F_KIND, 2, fld_d(s, a, F_SKIND, 2));
         pop(t, a);
       }
-      return;
-    }
-    if (slot < 2 * A) {
-      const int a = slot - A, p = pc(s, a);
+    } else if (slot < 2 * A) {
+      const int a = slot - A;
+      const int p = pc_d(s, a);
       switch (p) {
         case L_CStart: {                                        // :528-549
-          const int sr = j == 0 ? 1 : fld(s, a, F_SR, 1);
-          put(t, a, F_SR, 1, sr);
+          const int sr = j == 0 ? 1 : fld_d(s, a, F_SR, 1);
+          put_d(t, a, F_SR, 1, sr);
           if (sr) call(t, a, L_C1, OP_Force, oc_bare(ID_Secret));
           else {
             push_list(t, a, L_C3);
-            put(t, a, F_KIND, 2, K_Secret); put(t, a, F_PC, B_PC, L_DoListRequest);
+            put_d(t, a, F_KIND, 2, K_Secret); put_d(t, a, F_PC, B_PC, L_DoListRequest);
           }
           return;
         }
         case L_C1:                                              // :551-556
-          put(t, a, F_PC, B_PC, fld(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); return;
+          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); return;
         case L_C10: call(t, a, L_C11, OP_Force, oc_bare(ID_PVC)); return;   // :558-568
         case L_C11:                                             // :570-575
-          put(t, a, F_PC, B_PC, fld(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); return;
+          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); return;
         case L_c12: call(t, a, L_C13, OP_Get, oc_bare(ID_PVC)); return;     // :577-587
         case L_C13: {                                           // :589-594
-          bool go = fld(s, a, F_RQST, 2) != ST_Ok;
+          bool go = fld_d(s, a, F_RQST, 2) != ST_Ok;
           if (!go) {
-            const int oc = fld(s, a, F_RQOBJ, OBJB);
+            const int oc = fld_d(s, a, F_RQOBJ, OBJB);
             go = oc_id(oc) == ID_PVC && !(oc_is_full(oc) && u_spec(oc_u(oc)));
           }
-          put(t, a, F_PC, B_PC, go ? L_CStart : L_C2); return;
+          put_d(t, a, F_PC, B_PC, go ? L_CStart : L_C2); return;
         }
-        case L_C2: put(t, a, F_SR, 1, 0); put(t, a, F_PC, B_PC, L_C5); return;  // :596-602
+        case L_C2: put_d(t, a, F_SR, 1, 0); put_d(t, a, F_PC, B_PC, L_C5); return;  // :596-602
         case L_C3:                                              // :604-609
-          put(t, a, F_PC, B_PC, fld(s, a, F_LRST, 2) != ST_Ok ? L_CStart : L_C8); return;
-        case L_C8: put(t, a, F_PC, B_PC, objs(s, a) == 0 ? L_C4 : L_C6); return; // :611-616
+          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_LRST, 2) != ST_Ok ? L_CStart : L_C8); return;
+        case L_C8: put_d(t, a, F_PC, B_PC, objs_d(s, a) == 0 ? L_C4 : L_C6); return; // :611-616
         case L_C6: {                                            // :618-629
-          const int u = nth_bit(objs(s, a), j);
+          const int u = nth_bit(objs_d(s, a), j);
           call(t, a, L_C7, OP_Delete, oc_bare(u_id(u)));
           return;
         }
         case L_C7: {                                            // :631-636
-          const bool go = fld(s, a, F_RQST, 2) != ST_Ok || popc(objs(s, a)) > 1;
-          put(t, a, F_PC, B_PC, go ? L_CStart : L_C4); return;
+          const bool go = fld_d(s, a, F_RQST, 2) != ST_Ok || popc(objs_d(s, a)) > 1;
+          put_d(t, a, F_PC, B_PC, go ? L_CStart : L_C4); return;
         }
-        case L_C4: case L_C5: put(t, a, F_PC, B_PC, p == L_C4 ? L_C5 : L_CStart); return;
+        case L_C4: case L_C5: put_d(t, a, F_PC, B_PC, p == L_C4 ? L_C5 : L_CStart); return;
         case L_PVCStart:                                        // :655-663
           push_list(t, a, L_PVCListedPVCs);
-          put(t, a, F_KIND, 2, K_PVC); put(t, a, F_PC, B_PC, L_DoListRequest); return;
+          put_d(t, a, F_KIND, 2, K_PVC); put_d(t, a, F_PC, B_PC, L_DoListRequest); return;
         case L_PVCListedPVCs: {                                 // :665-671
-          const bool go = fld(s, a, F_LRST, 2) != ST_Ok || unbound(objs(s, a)) == 0;
-          put(t, a, F_PC, B_PC, go ? L_PVCStart : L_PVCHavePVCs); return;
+          const bool go = fld_d(s, a, F_LRST, 2) != ST_Ok || unbound(objs_d(s, a)) == 0;
+          put_d(t, a, F_PC, B_PC, go ? L_PVCStart : L_PVCHavePVCs); return;
         }
         case L_PVCHavePVCs: {                                   // :673-688
-          const int u = nth_bit(unbound(objs(s, a)), j);
+          const int u = nth_bit(unbound(objs_d(s, a)), j);
           // bound == "spec" :> ("pvname" :> unb.n) @@ unb
           call(t, a, L_PVCDone, OP_Update, oc_full(u_make(u_id(u), 1, u_vv(u))));
           return;
         }
-        default: /* L_PVCDone */ put(t, a, F_PC, B_PC, L_PVCStart); return;  // :690-693
+        default: /* L_PVCDone */ put_d(t, a, F_PC, B_PC, L_PVCStart); return;  // :690-693
       }
-    }
-    // APIStart (:698-756)
-    int k = j;
-    for (int c = 0; c < A; ++c) {
-      if (!(fld(s, c, F_RQP, 1) && fld(s, c, F_RQST, 2) == ST_Pending)) continue;
-      if (k-- != 0) continue;
-      const int oc = fld(s, c, F_RQOBJ, OBJB);
-      const int id = oc_id(oc);
-      const uint64_t api = s.w[0], same = api & id_mask(id);
-      int st = ST_Ok;
-      uint64_t nw = api;
-      switch (fld(s, c, F_RQOP, 3)) {
-        case OP_Create:                                         // :700-705
-          if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
-          break;
-        case OP_Force:                                          // :706-715
-          // variant 2 (seeded bug): add without replacing -> OnlyOneVersion fails
-          nw = (f.variant == 2 ? api : (api & ~same)) | (1ull << write_u(oc));
-          break;
-        case OP_Get:                                            // :716-728
-          if (same) {
-            put(t, c, F_RQOBJ, OBJB, oc_full(ctz(same)));       // CHOOSE o \in apiState
-            nw = read_map(api, same, c);
-          } else st = ST_Error;
-          break;
-        case OP_Delete: nw = api & ~same; break;                // :729-731
-        default: {                                              // Update :732-739
-          bool ok = false;
-          for (uint64_t x = same; x; x &= x - 1)
-            if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
-          if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
+    } else {
+      // APIStart (:698-756): successor j serves the j-th pending request,
+      // then the pending list requests.
+      int k = j, c = 0;
+      for (; c < A; ++c) {                                      // the k-th pending request
+        if (!(fld_d(s, c, F_RQP, 1) && fld_d(s, c, F_RQST, 2) == ST_Pending)) continue;
+        if (k-- == 0) break;
+      }
+      if (c < A) {
+        const int oc = fld_d(s, c, F_RQOBJ, OBJB);
+        const int id = oc_id(oc);
+        const uint64_t api = s.w[0], same = api & id_mask(id);
+        int st = ST_Ok;
+        uint64_t nw = api;
+        switch (fld_d(s, c, F_RQOP, 3)) {
+          case OP_Create:                                       // :700-705
+            if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
+            break;
+          case OP_Force:                                        // :706-715
+            // variant 2 (seeded bug): add without replacing -> OnlyOneVersion fails
+            nw = (f.variant == 2 ? api : (api & ~same)) | (1ull << write_u(oc));
+            break;
+          case OP_Get:                                          // :716-728
+            if (same) {
+              put_d(t, c, F_RQOBJ, OBJB, oc_full(ctz(same)));     // CHOOSE o \in apiState
+              nw = read_map(api, same, c);
+            } else st = ST_Error;
+            break;
+          case OP_Delete: nw = api & ~same; break;              // :729-731
+          default: {                                            // Update :732-739
+            bool ok = false;
+            for (uint64_t x = same; x; x &= x - 1)
+              if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
+            if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
+          }
         }
+        t.w[0] = nw;
+        put_d(t, c, F_RQST, 2, st);
+        return;
       }
-      t.w[0] = nw;
-      put(t, c, F_RQST, 2, st);
-      return;
+      for (c = 0; c < A; ++c) {                                 // :745-753
+        if (!(fld_d(s, c, F_LRP, 1) && fld_d(s, c, F_LRST, 2) == ST_Pending)) continue;
+        if (k-- == 0) break;
+      }
+      if (c < A) {
+        const uint64_t km = kind_mask(fld_d(s, c, F_LRK, 2)), api = s.w[0];
+        set_objs_d(t, c, api & km);
+        put_d(t, c, F_LRST, 2, ST_Ok);
+        t.w[0] = read_map(api, km, c);
+      }
     }
-    for (int c = 0; c < A; ++c) {                               // :745-753
-      if (!(fld(s, c, F_LRP, 1) && fld(s, c, F_LRST, 2) == ST_Pending)) continue;
-      if (k-- != 0) continue;
-      const uint64_t km = kind_mask(fld(s, c, F_LRK, 2)), api = s.w[0];
-      set_objs(t, c, api & km);
-      put(t, c, F_LRST, 2, ST_Ok);
-      t.w[0] = read_map(api, km, c);
-      return;
-    }
+  }
+
+  // Build successor j of `slot` (KubeAPI.tla:471-756).
+  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) t.w[i] = s.w[i];
+    apply_rt(s, slot, j, f, t);
   }
 
   // ------------------------------------------------------------ invariants
   // Returns -1 if TypeOK (:776-781) and OnlyOneVersion (:787-789) hold, else
   // the index of the first violated one in MC.cfg order (0 TypeOK, 1 OOV).
   KC_HD static int check(const State& s) {
-    for (int c = 0; c < A; ++c) {
-      if (fld(s, c, F_RQP, 1)) {                                // IsValidRequest :426-430
-        const int op = fld(s, c, F_RQOP, 3), st = fld(s, c, F_RQST, 2);
-        if (op < OP_Create || op > OP_Force || fld(s, c, F_RQOBJ, OBJB) == 0 ||
-            st < ST_Pending || st > ST_Error) return 0;
+    bool typeok = true;
+    static_for<A>([&](auto CI) {
+      constexpr int c = CI;
+      if (fld<c>(s, F_RQP, 1)) {                                // IsValidRequest :426-430
+        const int op = fld<c>(s, F_RQOP, 3), st = fld<c>(s, F_RQST, 2);
+        if (op < OP_Create || op > OP_Force || fld<c>(s, F_RQOBJ, OBJB) == 0 ||
+            st < ST_Pending || st > ST_Error) typeok = false;
       }
-      if (fld(s, c, F_LRP, 1)) {                                // IsValidListRequest :432-436
-        const int st = fld(s, c, F_LRST, 2);
-        if ((objs(s, c) & ~kind_mask(fld(s, c, F_LRK, 2))) || st < ST_Pending || st > ST_Error)
-          return 0;
+      if (fld<c>(s, F_LRP, 1)) {                                // IsValidListRequest :432-436
+        const int st = fld<c>(s, F_LRST, 2);
+        if ((objs<c>(s) & ~kind_mask(fld<c>(s, F_LRK, 2))) || st < ST_Pending || st > ST_Error)
+          typeok = false;
       }
-    }
+    });
+    if (!typeok) return 0;
     if (popc(s.w[0] & id_mask(0)) > 1 || popc(s.w[0] & id_mask(1)) > 1) return 1;
     return -1;
   }
@@ -494,6 +608,7 @@ struct Model {
   // FPSet stores it: MSB clear (TLC's disk FPSets reserve it), never 0.
   KC_HD static uint64_t fingerprint(const State& s) {
     uint64_t h = 0x6a09e667f3bcc909ull ^ (uint64_t)(W * 0x9e3779b97f4a7c15ull);
+#pragma unroll
     for (int i = 0; i < W_RAW; ++i) {
       uint64_t k = s.w[i] * 0x87c37b91114253d5ull;
       k = (k << 31) | (k >> 33);
@@ -528,24 +643,24 @@ struct Model {
     if (!hv) return (sp || vv) ? -1 : 1 + id;
     return 3 + u_make(id, sp, vv);
   }
-  KC_HD static void to_tuple(const State& s, uint64_t* o) {
+  static void to_tuple(const State& s, uint64_t* o) {
     o[0] = s.w[0];
     for (int p = 0; p < P; ++p) {
       uint64_t* q = o + 1 + TUPLE_PER_PROC * p;
       for (int k = 0; k < TUPLE_PER_PROC; ++k) q[k] = 0;
       if (p >= A) { q[0] = L_APIStart; continue; }
-      q[0] = pc(s, p); q[1] = fld(s, p, F_OP, 3); q[2] = oc_to_oval(fld(s, p, F_OBJ, OBJB));
-      q[3] = fld(s, p, F_KIND, 2); q[4] = fld(s, p, F_SR, 1); q[5] = fld(s, p, F_SD, 1);
-      q[6] = fld(s, p, F_SPROC, 2); q[7] = fld(s, p, F_SRET, 5); q[8] = fld(s, p, F_SOP, 3);
-      q[9] = oc_to_oval(fld(s, p, F_SOBJ, OBJB)); q[10] = fld(s, p, F_SKIND, 2);
-      q[11] = fld(s, p, F_RQP, 1); q[12] = fld(s, p, F_RQOP, 3); q[13] = fld(s, p, F_RQST, 2);
-      q[14] = oc_to_oval(fld(s, p, F_RQOBJ, OBJB));
-      q[15] = fld(s, p, F_LRP, 1); q[16] = fld(s, p, F_LRK, 2); q[17] = fld(s, p, F_LRST, 2);
-      q[18] = objs(s, p);
+      q[0] = fld_rt(s, p, F_PC, B_PC); q[1] = fld_rt(s, p, F_OP, 3); q[2] = oc_to_oval(fld_rt(s, p, F_OBJ, OBJB));
+      q[3] = fld_rt(s, p, F_KIND, 2); q[4] = fld_rt(s, p, F_SR, 1); q[5] = fld_rt(s, p, F_SD, 1);
+      q[6] = fld_rt(s, p, F_SPROC, 2); q[7] = fld_rt(s, p, F_SRET, 5); q[8] = fld_rt(s, p, F_SOP, 3);
+      q[9] = oc_to_oval(fld_rt(s, p, F_SOBJ, OBJB)); q[10] = fld_rt(s, p, F_SKIND, 2);
+      q[11] = fld_rt(s, p, F_RQP, 1); q[12] = fld_rt(s, p, F_RQOP, 3); q[13] = fld_rt(s, p, F_RQST, 2);
+      q[14] = oc_to_oval(fld_rt(s, p, F_RQOBJ, OBJB));
+      q[15] = fld_rt(s, p, F_LRP, 1); q[16] = fld_rt(s, p, F_LRK, 2); q[17] = fld_rt(s, p, F_LRST, 2);
+      q[18] = objs_rt(s, p);
     }
   }
   // returns false if the tuple is outside the lowered domain
-  KC_HD static bool from_tuple(const uint64_t* o, State& s) {
+  static bool from_tuple(const uint64_t* o, State& s) {
     for (int i = 0; i < W; ++i) s.w[i] = 0;
     if (o[0] & ~UMASK) return false;
     s.w[0] = o[0];
@@ -559,14 +674,14 @@ struct Model {
       const int ob = oval_to_oc(q[2]), sob = oval_to_oc(q[9]), rob = oval_to_oc(q[14]);
       if (ob < 0 || sob < 0 || rob < 0 || (q[18] & ~UMASK)) return false;
       if (!is_client(p) && q[4]) return false;
-      put(s, p, F_PC, B_PC, (int)q[0]); put(s, p, F_OP, 3, (int)q[1]); put(s, p, F_OBJ, OBJB, ob);
-      put(s, p, F_KIND, 2, (int)q[3]); put(s, p, F_SR, 1, (int)q[4]); put(s, p, F_SD, 1, (int)q[5]);
-      put(s, p, F_SPROC, 2, (int)q[6]); put(s, p, F_SRET, 5, (int)q[7]); put(s, p, F_SOP, 3, (int)q[8]);
-      put(s, p, F_SOBJ, OBJB, sob); put(s, p, F_SKIND, 2, (int)q[10]);
-      put(s, p, F_RQP, 1, (int)q[11]); put(s, p, F_RQOP, 3, (int)q[12]); put(s, p, F_RQST, 2, (int)q[13]);
-      put(s, p, F_RQOBJ, OBJB, rob);
-      put(s, p, F_LRP, 1, (int)q[15]); put(s, p, F_LRK, 2, (int)q[16]); put(s, p, F_LRST, 2, (int)q[17]);
-      set_objs(s, p, q[18]);
+      put_rt(s, p, F_PC, B_PC, (int)q[0]); put_rt(s, p, F_OP, 3, (int)q[1]); put_rt(s, p, F_OBJ, OBJB, ob);
+      put_rt(s, p, F_KIND, 2, (int)q[3]); put_rt(s, p, F_SR, 1, (int)q[4]); put_rt(s, p, F_SD, 1, (int)q[5]);
+      put_rt(s, p, F_SPROC, 2, (int)q[6]); put_rt(s, p, F_SRET, 5, (int)q[7]); put_rt(s, p, F_SOP, 3, (int)q[8]);
+      put_rt(s, p, F_SOBJ, OBJB, sob); put_rt(s, p, F_SKIND, 2, (int)q[10]);
+      put_rt(s, p, F_RQP, 1, (int)q[11]); put_rt(s, p, F_RQOP, 3, (int)q[12]); put_rt(s, p, F_RQST, 2, (int)q[13]);
+      put_rt(s, p, F_RQOBJ, OBJB, rob);
+      put_rt(s, p, F_LRP, 1, (int)q[15]); put_rt(s, p, F_LRK, 2, (int)q[16]); put_rt(s, p, F_LRST, 2, (int)q[17]);
+      set_objs_rt(s, p, q[18]);
     }
     return true;
   }
