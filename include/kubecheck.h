@@ -165,26 +165,43 @@ int kc_engine_capture_level(kc_engine *e, int level);
 int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
 
 /* --------------------------------------------------- Sharded (multi-GPU) */
-/* Per-level stage API for the fingerprint-owner-sharded BFS (one process
- * per GPU; the exchange between stages is done by the caller, e.g. RCCL
- * all-to-all via torch.distributed).  See INTEGRATION.md. */
-int kc_shard_create(const kc_model_config *cfg, int rank, int world, kc_engine **out);
-/* Insert and adopt the init states owned by this rank. */
-int kc_shard_init(kc_engine *e, uint64_t *n_frontier);
-/* Expand the frontier; bucket candidate records by owner into the send
- * buffer.  counts_out[r] = records for rank r (world entries). */
-int kc_shard_expand(kc_engine *e, uint64_t *counts_out);
-/* Device pointer + record size (bytes) of the send / receive buffers;
- * the receive buffer is (re)sized to `recv_records`. */
-int kc_shard_send_buffer(kc_engine *e, void **dev_ptr, uint64_t *record_bytes);
-int kc_shard_recv_buffer(kc_engine *e, uint64_t recv_records, void **dev_ptr);
-/* Dedup + insert received records, compact the new ones into the next
- * frontier.  Returns the local new-state count and the next level's
- * candidate estimate; err_key_out = min local error key (or UINT64_MAX). */
-int kc_shard_insert(kc_engine *e, uint64_t recv_records, uint64_t *n_new,
+/* Fingerprint-owner-sharded BFS, one process per GPU (replaces TLC's
+ * single-host worker pool; TLC's own distributed mode is off in Model_1,
+ * KubeAPI___Model_1.launch:4-7).  The caller drives the levels and does the
+ * exchange between pack() and insert() (kubecheck/distributed.py: RCCL
+ * all-to-all through torch.distributed).  owner(fp) = floor(fp*R/2^63).
+ * Per level:  expand -> pack(send) -> [all-to-all] -> insert(recv) ->
+ * [all-reduce of new counts / error keys] -> advance.
+ * Keys (records and errors): rank<<60 | parent index<<16 | successor<<8 |
+ * low byte (action id in records; 1 assertion, 2 invariant, 3 deadlock,
+ * 0x12 invariant violated by an Init state in error keys). */
+typedef struct kc_shard kc_shard;
+int kc_shard_create(const kc_model_config *cfg, int rank, int world, kc_shard **out);
+void kc_shard_destroy(kc_shard *s);
+/* Adopt (insert + enqueue) the Init states this rank owns. */
+int kc_shard_init(kc_shard *s, uint64_t *n_local);
+/* Expand the frontier; counts_out[r] = records destined to rank r (world
+ * entries); *err_key_out = this rank's min Assert/deadlock key or ~0. */
+int kc_shard_expand(kc_shard *s, uint64_t *counts_out, uint64_t *err_key_out);
+/* Bytes per record: 8*state_words + 16 (state, fingerprint, key). */
+uint64_t kc_shard_record_bytes(kc_shard *s);
+/* Write sum(counts) records, grouped by owner rank, into device memory. */
+int kc_shard_pack(kc_shard *s, void *send_dev);
+/* Dedup + insert `n_records` received records (device memory, sorted by
+ * source rank); *n_new = states added to this rank's next frontier. */
+int kc_shard_insert(kc_shard *s, const void *recv_dev, uint64_t n_records, uint64_t *n_new,
                     uint64_t *err_key_out);
-/* Totals of this shard (generated counts per action etc.). */
-int kc_shard_result(kc_engine *e, kc_result *res);
+/* The new states become the frontier (after the caller's agreement step). */
+int kc_shard_advance(kc_shard *s);
+/* Parent key of local state `idx` of BFS level `level` (trace walk-back). */
+int kc_shard_parent_key(kc_shard *s, int level, uint64_t idx, uint64_t *key_out);
+/* Canonical tuple of current-frontier state `idx`. */
+int kc_shard_frontier_tuple(kc_shard *s, uint64_t idx, uint64_t *out);
+/* This rank's counters: act_gen (its parents), act_dist (its new states),
+ * generated, distinct (owned), fpset_slots. */
+int kc_shard_result(kc_shard *s, kc_result *res);
+/* owner rank of a fingerprint */
+int kc_shard_owner(uint64_t fp, int world);
 
 /* ---------------------------------------------------------- Spec (host) */
 /* Words of the canonical tuple for a model: 1 + 19 * (nc + np + ns). */

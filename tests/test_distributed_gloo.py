@@ -1,0 +1,91 @@
+"""The sharded BFS driver (kubecheck.distributed) over the gloo backend with
+world_size 2 and 3 on CPU: per-level widths, totals, per-action generated
+counts and error traces must equal the single-process results (CPU oracle
+fixtures) — totals do not depend on the number of ranks."""
+import json
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kw, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tla-kubernetes_amd"))
+    import torch.distributed as dist
+    from cpu_shard import CpuShard
+    from kubecheck import ModelConfig
+    from kubecheck.distributed import ShardedModelChecker
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = ModelConfig(**kw)
+    res = ShardedModelChecker(cfg, CpuShard(cfg, rank, world)).run()
+    json.dump(res, open(os.path.join(outdir, f"r{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+def run_sharded(tmp_path, world, **kw):
+    mp.spawn(_worker, args=(world, _free_port(), kw, str(tmp_path)), nprocs=world, join=True)
+    outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    for o in outs:
+        o.pop("seconds")
+    for o in outs[1:]:
+        assert o == outs[0]          # every rank agrees on the global result
+    return outs[0]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_counts_match_single(tmp_path, fixtures, world):
+    fx = fixtures["model1_fail0_timeout0"]
+    r = run_sharded(tmp_path, world, can_fail=False, can_timeout=False)
+    assert r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["act_gen"] == fx["act_gen"]
+    assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+    assert r["complete"] and r["error"] is None
+
+
+def test_sharded_assertion_trace(tmp_path, fixtures, oracle):
+    fx = fixtures["nc2"]
+    r = run_sharded(tmp_path, 2, nc=2)
+    assert r["error"] == "assertion" and r["error_action"] == "C4"
+    assert r["error_level"] == 10 and r["trace_len"] == fx["trace_len"] == 10
+    assert r["level_width"] == fx["level_width"]
+    # the trace is a real behaviour: each state is a successor of the previous
+    cfg = oracle.config(nc=2)
+    for a, b in zip(r["trace"], r["trace"][1:]):
+        succ, _ = oracle.successors(cfg, a)
+        assert any(list(map(int, x)) == b for _, x in succ)
+    _, fail = oracle.successors(cfg, r["trace"][-1])
+    assert fail == "C4"
+
+
+def test_sharded_invariant_trace(tmp_path, fixtures):
+    fx = fixtures["variant2"]
+    r = run_sharded(tmp_path, 2, variant=2)
+    assert r["error"] == "invariant" and r["error_invariant"] == "OnlyOneVersion"
+    assert r["trace_len"] == fx["trace_len"] and r["error_level"] == fx["err_level"]
+
+
+def test_owner_function_matches_library():
+    import kubecheck
+    from kubecheck.distributed import owner
+
+    lib = kubecheck.load()
+    rng = __import__("numpy").random.default_rng(1)
+    for fp in rng.integers(1, 2**63, size=2000, dtype="uint64"):
+        for w in (2, 3, 8):
+            assert owner(int(fp), w) == lib.kc_shard_owner(int(fp), w)

@@ -121,3 +121,5 @@ def test_enlarged_full(fixtures):
     r = run(np=2, keep_trace=False)
     assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r.level_width == fx["level_width"]
+    assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    assert r.complete and r.error is None

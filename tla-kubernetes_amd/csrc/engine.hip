@@ -22,29 +22,13 @@
 #include "../../include/kubecheck.h"
 #include "engine.h"
 #include "engine_kernels.h"
+#include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
 
 namespace kc {
 
 namespace {
-
-template <class T>
-int grow_buffer(T*& p, uint64_t& cap, uint64_t need, bool keep, hipStream_t st) {
-  if (need <= cap) return 0;
-  uint64_t nc = cap ? cap : 1024;
-  while (nc < need) nc *= 2;
-  T* np = nullptr;
-  KC_HIP_TRY(hipMalloc(&np, nc * sizeof(T)));
-  if (keep && p && cap) KC_HIP_TRY(hipMemcpyAsync(np, p, cap * sizeof(T), hipMemcpyDeviceToDevice, st));
-  if (p) {
-    KC_HIP_TRY(hipStreamSynchronize(st));
-    KC_HIP_TRY(hipFree(p));
-  }
-  p = np;
-  cap = nc;
-  return 0;
-}
 
 const char* kActionNames[A_COUNT] = {
     "DoRequest", "DoReply", "DoListRequest", "DoListReply", "CStart", "C1", "C10", "C11",
@@ -58,17 +42,6 @@ __global__ void k_advance(const uint32_t* __restrict__ offsets, const uint32_t* 
                           uint64_t n, Counters* __restrict__ C) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && n > 0)
     C->chunk_base += (unsigned long long)offsets[n - 1] + cnt[n - 1];
-}
-
-// Insert a short list of fingerprints (init states, rehash) into the FPSet.
-__global__ void k_fpset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
-                                    unsigned long long* __restrict__ slots, uint64_t nbuckets,
-                                    int* __restrict__ result) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const int r = fpset_insert(slots, nbuckets, fps[i]);
-    if (result) result[i] = r;
-  }
 }
 
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
@@ -143,8 +116,7 @@ class EngineT final : public EngineBase {
     KC_HIP_TRY(hipMalloc(&d_fps, ni * 8));
     KC_HIP_TRY(hipMalloc(&d_res, ni * sizeof(int)));
     KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), ni * 8, hipMemcpyHostToDevice, st_));
-    hipLaunchKernelGGL(k_fpset_insert_list, dim3(1), dim3(256), 0, st_, d_fps, (uint64_t)ni,
-                       fps_.slots, fps_.nbuckets, d_res);
+    launch_fpset_insert_list(d_fps, (uint64_t)ni, fps_, d_res, st_);
     std::vector<int> ires(ni);
     KC_HIP_TRY(hipMemcpyAsync(ires.data(), d_res, ni * sizeof(int), hipMemcpyDeviceToHost, st_));
     std::vector<unsigned long long> ipar(ni, ~0ull);

@@ -1,0 +1,29 @@
+// engine_util.h — small host helpers shared by the single-GPU engine and the
+// sharded (multi-GPU) stages.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kc_common.h"
+
+namespace kc {
+
+// Grow a device buffer to >= need elements (doubling); keep contents if asked.
+template <class T>
+int grow_buffer(T*& p, uint64_t& cap, uint64_t need, bool keep, hipStream_t st) {
+  if (need <= cap) return 0;
+  uint64_t nc = cap ? cap : 1024;
+  while (nc < need) nc *= 2;
+  T* np = nullptr;
+  KC_HIP_TRY(hipMalloc(&np, nc * sizeof(T)));
+  if (keep && p && cap) KC_HIP_TRY(hipMemcpyAsync(np, p, cap * sizeof(T), hipMemcpyDeviceToDevice, st));
+  if (p) {
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    KC_HIP_TRY(hipFree(p));
+  }
+  p = np;
+  cap = nc;
+  return 0;
+}
+
+}  // namespace kc

@@ -32,6 +32,24 @@ __global__ void k_fpset_rehash(const unsigned long long* __restrict__ old, uint6
   }
 }
 
+// Insert a short list of fingerprints (init states) into the FPSet.
+__global__ void k_fpset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
+                                    unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                                    int* __restrict__ result) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int r = fpset_insert(slots, nbuckets, fps[i]);
+    if (result) result[i] = r;
+  }
+}
+
+void launch_fpset_insert_list(const uint64_t* d_fps, uint64_t n, const DevFpset& fs, int* d_res,
+                              hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_fpset_insert_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d_fps, n, fs.slots, fs.nbuckets, d_res);
+}
+
 int DevFpset::init(uint64_t min_slots, hipStream_t st) {
   release();
   nbuckets = (min_slots + 7) / 8;

@@ -31,5 +31,8 @@ struct DevBatchTable {
 };
 
 uint64_t next_pow2(uint64_t x);
+// insert a device list of (normalised) fps; d_res[i] = 1 new / 0 present (may be NULL)
+void launch_fpset_insert_list(const uint64_t* d_fps, uint64_t n, const DevFpset& fs, int* d_res,
+                              hipStream_t st);
 
 }  // namespace kc

@@ -1,24 +1,531 @@
-// shard.hip — fingerprint-owner-sharded BFS stages (multi-GPU).  Filled in
-// below the single-GPU engine; until then every entry point reports ENOSYS.
+// shard.hip — fingerprint-owner-sharded BFS stages for one GPU of R (one
+// process per GPU; kubecheck/distributed.py drives the levels and does the
+// exchange with RCCL all-to-all through torch.distributed).
+//
+// owner(fp) = floor(fp * R / 2^63) (fps are uniform in [1, 2^63)), the top
+// bits of the fingerprint as in TLC's MultiFPSet [ext-TLC].  Per level:
+//   expand : k_expand (local dedup by min order key, generated counters,
+//            Assert/deadlock keys) + k_shard_count (representatives per
+//            owner, per parent) + one exclusive scan per owner
+//   pack   : k_shard_pack writes records {state, fp, key} into the caller's
+//            send buffer, grouped by owner, each group in (parent, t) order
+//   (all-to-all by the caller)
+//   insert : received records -> batch table (min key) -> FPSet shard ->
+//            new states compacted in key order into the next frontier, with
+//            parent keys (TLC trace file), invariant checks, counters
+// Keys: rank << 60 | parent index << 16 | successor position << 8 | low byte
+// (action id in records, ErrKind in error keys), so the same minimum is
+// taken everywhere and the result does not depend on arrival order.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <memory>
+#include <vector>
 
 #include "../../include/kubecheck.h"
+#include "engine_kernels.h"
+#include "engine_util.h"
+#include "fpset_host.h"
 #include "kc_common.h"
+
+namespace kc {
+
+constexpr uint64_t KEY_INIT = 0xFull << 60;   // parent key of an Init state (| init index)
+
+__device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
+  return (uint32_t)__umul64hi(fp << 1, (uint64_t)world);
+}
+
+template <class M>
+struct Record {
+  uint64_t w[M::W];
+  uint64_t fp;
+  uint64_t key;
+};
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f,
+              const BatchEntry* __restrict__ bt, uint64_t bmask, uint32_t world,
+              uint32_t* __restrict__ cnt /* [world][n] */, uint32_t* __restrict__ repmask) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const typename M::State s = load_state<M>(cur, i);
+  const typename M::Plan pl = M::plan(s, f);
+  const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
+  uint32_t c[16] = {};
+  uint32_t mask = 0;
+  for (int t = 0; t < tot; ++t) {
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    typename M::State x;
+    M::apply(s, slot, j, f, x);
+    const uint64_t fp = M::fingerprint(x);
+    if (batch_is_rep(bt, bmask, fp, (i << 8) | (uint64_t)t)) {
+      mask |= 1u << t;
+      const uint32_t o = owner_of(fp, world);
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) c[k] += (k == o);
+    }
+  }
+  repmask[i] = mask;
+  for (uint32_t k = 0; k < world; ++k) cnt[(uint64_t)k * n + i] = c[k];
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uint32_t world,
+             uint64_t rank, const uint32_t* __restrict__ off /* [world][n] exclusive */,
+             const uint64_t* __restrict__ owner_base, const uint32_t* __restrict__ repmask,
+             Record<M>* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t mask = repmask[i];
+  if (!mask) return;
+  const typename M::State s = load_state<M>(cur, i);
+  const typename M::Plan pl = M::plan(s, f);
+  uint32_t c[16] = {};
+  for (; mask; mask &= mask - 1) {
+    const int t = __ffs(mask) - 1;
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    typename M::State x;
+    M::apply(s, slot, j, f, x);
+    const uint64_t fp = M::fingerprint(x);
+    const uint32_t o = owner_of(fp, world);
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+      if (k == o) { r = c[k]; c[k] = r + 1; }
+    const uint64_t pos = owner_base[o] + off[(uint64_t)o * n + i] + r;
+    Record<M>* rec = out + pos;
+#pragma unroll
+    for (int k = 0; k < M::W; ++k) rec->w[k] = x.w[k];
+    rec->fp = fp;
+    rec->key = (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot);
+  }
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_claim(const Record<M>* __restrict__ in, uint64_t n, BatchEntry* __restrict__ bt,
+              uint64_t bmask, Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !batch_insert_bounded(bt, bmask, in[i].fp, in[i].key)) atomicAdd(&C->overflow, 1ull);
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_resolve(const Record<M>* __restrict__ in, uint64_t n, const BatchEntry* __restrict__ bt,
+                uint64_t bmask, unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t nw = 0;
+  const uint64_t fp = in[i].fp;
+  if (batch_is_rep(bt, bmask, fp, in[i].key)) {
+    const int r = fpset_insert(slots, nbuckets, fp);
+    if (r == 1) nw = 1;
+    else if (r < 0) atomicAdd(&C->overflow, 1ull);
+  }
+  isnew[i] = nw;
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_emit(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
+             const uint32_t* __restrict__ offsets, Flags f, typename M::State* __restrict__ next,
+             unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned long long sh_cand;
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sh_cand = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cand = 0;
+  if (i < n && isnew[i]) {
+    typename M::State x;
+#pragma unroll
+    for (int k = 0; k < M::W; ++k) x.w[k] = in[i].w[k];
+    const uint64_t key = in[i].key, o = offsets[i];
+    store_state<M>(next, o, x);
+    pkeys[next_gidx + o] = key;
+    if (M::check(x) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
+    atomicAdd(&sh_act[key & 0xff], 1u);
+    cand = (unsigned long long)M::plan(x, f).total;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x == 0 && sh_cand) atomicAdd(&C->next_cand, sh_cand);
+}
+
+class ShardBase {
+ public:
+  virtual ~ShardBase() = default;
+  virtual int setup() = 0;
+  virtual int init(uint64_t* n_local) = 0;
+  virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
+  virtual uint64_t record_bytes() const = 0;
+  virtual int pack(void* send) = 0;
+  virtual int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) = 0;
+  virtual int advance() = 0;
+  virtual int parent_key(int level, uint64_t idx, uint64_t* key) = 0;
+  virtual int frontier_tuple(uint64_t idx, uint64_t* out) = 0;
+  virtual int result(kc_result* r) = 0;
+};
+
+template <class M>
+class ShardT final : public ShardBase {
+  using State = typename M::State;
+  using Rec = Record<M>;
+
+ public:
+  ShardT(const kc_model_config& cfg, int rank, int world)
+      : cfg_(cfg), rank_(rank), world_(world) {
+    flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
+  }
+  ~ShardT() override { release(); }
+
+  int setup() override {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+      set_error("kc_shard: no HIP device visible (no CPU fallback)");
+      return -ENODEV;
+    }
+    if (world_ < 1 || world_ > 15 || rank_ < 0 || rank_ >= world_) {
+      set_error("kc_shard: bad rank/world %d/%d (1..15 ranks)", rank_, world_);
+      return -EINVAL;
+    }
+    if (cfg_.device < 0 || cfg_.device >= ndev) {
+      set_error("kc_shard: bad device %d", cfg_.device);
+      return -EINVAL;
+    }
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    KC_HIP_TRY(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
+    KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
+    KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
+    return 0;
+  }
+
+  int init(uint64_t* n_local) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
+    if (fps_.slots && fps_.capacity() >= fp_slots) {
+      KC_HIP_TRY(hipMemsetAsync(fps_.slots, 0, fps_.nbuckets * 64, st_));
+      fps_.count = 0;
+    } else {
+      KC_TRY(fps_.init(fp_slots, st_));
+    }
+    KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
+    std::vector<State> mine;
+    std::vector<unsigned long long> keys;
+    std::vector<uint64_t> fps;
+    cand_ = 0;
+    for (int k = 0; k < M::num_init(); ++k) {
+      State s;
+      M::init_state(k, s);
+      const uint64_t fp = M::fingerprint(s);
+      const uint32_t o = (uint32_t)(((unsigned __int128)(fp << 1) * (uint64_t)world_) >> 64);
+      if ((int)o != rank_) continue;
+      mine.push_back(s);
+      keys.push_back(KEY_INIT | (uint64_t)k);
+      fps.push_back(fp);
+      cand_ += (uint64_t)M::plan(s, flags_).total;
+      if (M::check(s) >= 0 && init_err_ == ~0ull)
+        init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
+    }
+    n_ = mine.size();
+    level_ = 1;
+    level_base_.assign(1, 0);
+    gen_init_ = n_;
+    KC_TRY(grow_buffer(cur_, cur_cap_, std::max<uint64_t>(n_, 1), false, st_));
+    KC_TRY(grow_buffer(pkeys_, pk_cap_, std::max<uint64_t>(n_, 1) + cand_, false, st_));
+    if (n_) {
+      KC_HIP_TRY(hipMemcpyAsync(cur_, mine.data(), n_ * sizeof(State), hipMemcpyHostToDevice, st_));
+      KC_HIP_TRY(hipMemcpyAsync(pkeys_, keys.data(), n_ * 8, hipMemcpyHostToDevice, st_));
+      uint64_t* d_fps = nullptr;
+      KC_HIP_TRY(hipMalloc(&d_fps, n_ * 8));
+      KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), n_ * 8, hipMemcpyHostToDevice, st_));
+      launch_fpset_insert_list(d_fps, n_, fps_, nullptr, st_);
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      (void)hipFree(d_fps);
+    }
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    fps_.count = n_;
+    *n_local = n_;
+    return 0;
+  }
+
+  int expand(uint64_t* counts, uint64_t* err_key) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
+    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
+    for (int o = 0; o < world_; ++o) counts[o] = 0;
+    send_total_ = 0;
+    *err_key = init_err_;
+    init_err_ = ~0ull;
+    if (n_ == 0) return 0;
+    const uint64_t bcap = next_pow2(2 * cand_ + 256);
+    KC_TRY(bt_.ensure(bcap, st_));
+    KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
+    const unsigned grid = (unsigned)((n_ + 255) / 256);
+    hipLaunchKernelGGL(k_expand<M>, dim3(grid), dim3(256), 0, st_, cur_, n_, 0ull, flags_,
+                       cfg_.check_deadlock, bt_.t, bcap - 1, d_ctr_);
+    KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
+    KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
+    KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
+    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(256), 0, st_, cur_, n_, flags_, bt_.t,
+                       bcap - 1, (uint32_t)world_, cnt_, repmask_);
+    size_t tmp_bytes = 0;
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)n_, st_));
+    KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+    for (int o = 0; o < world_; ++o)
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_ + (uint64_t)o * n_,
+                                                  off_ + (uint64_t)o * n_, (int)n_, st_));
+    KC_HIP_TRY(hipGetLastError());
+    // per-owner totals = last offset + last count
+    std::vector<uint32_t> lo(world_), lc(world_);
+    for (int o = 0; o < world_; ++o) {
+      KC_HIP_TRY(hipMemcpyAsync(&lo[o], off_ + (uint64_t)o * n_ + n_ - 1, 4, hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(&lc[o], cnt_ + (uint64_t)o * n_ + n_ - 1, 4, hipMemcpyDeviceToHost, st_));
+    }
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (h_ctr_->overflow) {
+      set_error("kc_shard_expand: successor overflow / batch table full");
+      return -ENOMEM;
+    }
+    uint64_t base[16] = {};
+    for (int o = 0; o < world_; ++o) {
+      counts[o] = (uint64_t)lo[o] + lc[o];
+      base[o] = send_total_;
+      send_total_ += counts[o];
+    }
+    KC_HIP_TRY(hipMemcpyAsync(d_owner_base_, base, sizeof base, hipMemcpyHostToDevice, st_));
+    if (h_ctr_->err_key != ~0ull)
+      *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_ctr_->err_key);
+    return 0;
+  }
+
+  uint64_t record_bytes() const override { return sizeof(Rec); }
+
+  int pack(void* send) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    if (n_ && send_total_) {
+      hipLaunchKernelGGL(k_shard_pack<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
+                         cur_, n_, flags_, (uint32_t)world_, (uint64_t)rank_, off_,
+                         d_owner_base_, repmask_, (Rec*)send);
+      KC_HIP_TRY(hipGetLastError());
+    }
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    return 0;
+  }
+
+  int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    const Rec* in = (const Rec*)recv;
+    *n_new = 0;
+    *err_key = ~0ull;
+    next_n_ = 0;
+    if (n) {
+      const uint64_t bcap = next_pow2(2 * n + 256);
+      KC_TRY(bt_.ensure(bcap, st_));
+      KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
+      KC_TRY(fps_.reserve(n, st_));
+      KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
+      KC_TRY(grow_buffer(ioff_, ioff_cap_, n, false, st_));
+      KC_TRY(grow_buffer(next_, next_cap_, n, false, st_));
+      const uint64_t next_gidx = level_base_.back() + n_;
+      KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + n, true, st_));
+      const unsigned grid = (unsigned)((n + 255) / 256);
+      hipLaunchKernelGGL(k_shard_claim<M>, dim3(grid), dim3(256), 0, st_, in, n, bt_.t, bcap - 1, d_ctr_);
+      hipLaunchKernelGGL(k_shard_resolve<M>, dim3(grid), dim3(256), 0, st_, in, n, bt_.t, bcap - 1,
+                         fps_.slots, fps_.nbuckets, isnew_, d_ctr_);
+      size_t tmp_bytes = 0;
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
+      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
+      hipLaunchKernelGGL(k_shard_emit<M>, dim3(grid), dim3(256), 0, st_, in, n, isnew_, ioff_,
+                         flags_, next_, pkeys_, next_gidx, d_ctr_);
+      KC_HIP_TRY(hipGetLastError());
+      uint32_t lo = 0, lc = 0;
+      KC_HIP_TRY(hipMemcpyAsync(&lo, ioff_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(&lc, isnew_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      if (h_ctr_->overflow) {
+        set_error("kc_shard_insert: table full");
+        return -ENOMEM;
+      }
+      next_n_ = (uint64_t)lo + lc;
+      fps_.count += next_n_;
+      next_cand_ = h_ctr_->next_cand;
+      if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
+    } else {
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      next_cand_ = 0;
+    }
+    *n_new = next_n_;
+    return 0;
+  }
+
+  int advance() override {
+    level_base_.push_back(level_base_.back() + n_);
+    std::swap(cur_, next_);
+    std::swap(cur_cap_, next_cap_);
+    n_ = next_n_;
+    cand_ = next_cand_;
+    ++level_;
+    return 0;
+  }
+
+  int parent_key(int level, uint64_t idx, uint64_t* key) override {
+    if (level < 1 || level > (int)level_base_.size()) {
+      set_error("kc_shard_parent_key: bad level %d", level);
+      return -EINVAL;
+    }
+    const uint64_t g = level_base_[level - 1] + idx;
+    KC_HIP_TRY(hipMemcpy(key, pkeys_ + g, 8, hipMemcpyDeviceToHost));
+    return 0;
+  }
+
+  int frontier_tuple(uint64_t idx, uint64_t* out) override {
+    if (idx >= n_) { set_error("kc_shard_frontier_tuple: index"); return -EINVAL; }
+    State s;
+    KC_HIP_TRY(hipMemcpy(&s, cur_ + idx, sizeof(State), hipMemcpyDeviceToHost));
+    M::to_tuple(s, out);
+    return M::TUPLE_WORDS;
+  }
+
+  int result(kc_result* r) override {
+    KC_HIP_TRY(hipMemcpy(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost));
+    memset(r, 0, sizeof *r);
+    uint64_t gen = 0;
+    for (int a = 0; a < A_COUNT; ++a) {
+      r->act_gen[a] = h_ctr_->act_gen[a];
+      r->act_dist[a] = h_ctr_->act_dist[a];
+      gen += h_ctr_->act_gen[a];
+    }
+    r->init = gen_init_;
+    r->generated = gen;                 // successors generated by this rank's parents
+    r->distinct = fps_.count;
+    r->fpset_slots = fps_.capacity();
+    r->fpset_probes = h_ctr_->probes;
+    r->nlevels = level_;
+    return 0;
+  }
+
+ private:
+  void release() {
+    (void)hipSetDevice(cfg_.device);
+    fps_.release();
+    bt_.release();
+    for (void* p : {(void*)cur_, (void*)next_, (void*)pkeys_, (void*)cnt_, (void*)off_,
+                    (void*)repmask_, (void*)isnew_, (void*)ioff_, (void*)scan_tmp_, (void*)d_ctr_,
+                    (void*)d_owner_base_})
+      if (p) (void)hipFree(p);
+    if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  kc_model_config cfg_;
+  int rank_, world_;
+  Flags flags_{};
+  hipStream_t st_ = nullptr;
+  DevFpset fps_;
+  DevBatchTable bt_;
+  State *cur_ = nullptr, *next_ = nullptr;
+  uint64_t cur_cap_ = 0, next_cap_ = 0;
+  unsigned long long* pkeys_ = nullptr;
+  uint64_t pk_cap_ = 0;
+  uint32_t *cnt_ = nullptr, *off_ = nullptr, *repmask_ = nullptr, *isnew_ = nullptr, *ioff_ = nullptr;
+  uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
+  uint8_t* scan_tmp_ = nullptr;
+  uint64_t scan_cap_ = 0;
+  uint64_t* d_owner_base_ = nullptr;
+  Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
+  uint64_t n_ = 0, next_n_ = 0, cand_ = 0, next_cand_ = 0, send_total_ = 0, gen_init_ = 0;
+  uint64_t init_err_ = ~0ull;
+  int level_ = 0;
+  std::vector<uint64_t> level_base_;
+};
+
+std::unique_ptr<ShardBase> make_shard(const kc_model_config& cfg, int rank, int world) {
+#define KC_MAKE(a, b, c)                                                   \
+  if (cfg.nc == a && cfg.np == b && cfg.ns == c)                           \
+    return std::unique_ptr<ShardBase>(new ShardT<Model<a, b, c>>(cfg, rank, world));
+  KC_FOR_EACH_MODEL(KC_MAKE)
+#undef KC_MAKE
+  return nullptr;
+}
+
+}  // namespace kc
 
 using namespace kc;
 
+struct kc_shard {
+  std::unique_ptr<ShardBase> impl;
+};
+
 extern "C" {
 
-int kc_shard_create(const kc_model_config*, int, int, kc_engine** out) {
-  if (out) *out = nullptr;
-  set_error("kc_shard_create: not built yet");
-  return -ENOSYS;
+int kc_shard_create(const kc_model_config* cfg, int rank, int world, kc_shard** out) {
+  if (!cfg || !out) { set_error("kc_shard_create: NULL"); return -EINVAL; }
+  *out = nullptr;
+  auto impl = make_shard(*cfg, rank, world);
+  if (!impl) {
+    set_error("kc_shard_create: unsupported model nc=%d np=%d ns=%d", cfg->nc, cfg->np, cfg->ns);
+    return -EINVAL;
+  }
+  KC_TRY(impl->setup());
+  *out = new kc_shard{std::move(impl)};
+  return 0;
 }
-int kc_shard_init(kc_engine*, uint64_t*) { set_error("not built"); return -ENOSYS; }
-int kc_shard_expand(kc_engine*, uint64_t*) { set_error("not built"); return -ENOSYS; }
-int kc_shard_send_buffer(kc_engine*, void**, uint64_t*) { set_error("not built"); return -ENOSYS; }
-int kc_shard_recv_buffer(kc_engine*, uint64_t, void**) { set_error("not built"); return -ENOSYS; }
-int kc_shard_insert(kc_engine*, uint64_t, uint64_t*, uint64_t*) { set_error("not built"); return -ENOSYS; }
-int kc_shard_result(kc_engine*, kc_result*) { set_error("not built"); return -ENOSYS; }
+void kc_shard_destroy(kc_shard* s) { delete s; }
+int kc_shard_init(kc_shard* s, uint64_t* n_local) {
+  if (!s || !n_local) { set_error("kc_shard_init: NULL"); return -EINVAL; }
+  return s->impl->init(n_local);
+}
+int kc_shard_expand(kc_shard* s, uint64_t* counts, uint64_t* err_key) {
+  if (!s || !counts || !err_key) { set_error("kc_shard_expand: NULL"); return -EINVAL; }
+  return s->impl->expand(counts, err_key);
+}
+uint64_t kc_shard_record_bytes(kc_shard* s) { return s ? s->impl->record_bytes() : 0; }
+int kc_shard_pack(kc_shard* s, void* send_dev) {
+  if (!s) { set_error("kc_shard_pack: NULL"); return -EINVAL; }
+  return s->impl->pack(send_dev);
+}
+int kc_shard_insert(kc_shard* s, const void* recv_dev, uint64_t n_records, uint64_t* n_new,
+                    uint64_t* err_key) {
+  if (!s || !n_new || !err_key) { set_error("kc_shard_insert: NULL"); return -EINVAL; }
+  return s->impl->insert(recv_dev, n_records, n_new, err_key);
+}
+int kc_shard_advance(kc_shard* s) {
+  if (!s) { set_error("kc_shard_advance: NULL"); return -EINVAL; }
+  return s->impl->advance();
+}
+int kc_shard_parent_key(kc_shard* s, int level, uint64_t idx, uint64_t* key) {
+  if (!s || !key) { set_error("kc_shard_parent_key: NULL"); return -EINVAL; }
+  return s->impl->parent_key(level, idx, key);
+}
+int kc_shard_frontier_tuple(kc_shard* s, uint64_t idx, uint64_t* out) {
+  if (!s || !out) { set_error("kc_shard_frontier_tuple: NULL"); return -EINVAL; }
+  return s->impl->frontier_tuple(idx, out);
+}
+int kc_shard_result(kc_shard* s, kc_result* r) {
+  if (!s || !r) { set_error("kc_shard_result: NULL"); return -EINVAL; }
+  return s->impl->result(r);
+}
+int kc_shard_owner(uint64_t fp, int world) {
+  if (world < 1) return -EINVAL;
+  return (int)(((unsigned __int128)((fp & 0x7fffffffffffffffull) << 1) * (uint64_t)world) >> 64);
+}
 
 }  // extern "C"

@@ -86,12 +86,17 @@ SIGNATURES = [
     ("kc_engine_capture_level", C.c_int, [_P, C.c_int]),
     ("kc_engine_kernel_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
     ("kc_shard_create", C.c_int, [C.POINTER(KcModelConfig), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("kc_shard_destroy", None, [_P]),
     ("kc_shard_init", C.c_int, [_P, _U64P]),
-    ("kc_shard_expand", C.c_int, [_P, _U64P]),
-    ("kc_shard_send_buffer", C.c_int, [_P, C.POINTER(_P), _U64P]),
-    ("kc_shard_recv_buffer", C.c_int, [_P, C.c_uint64, C.POINTER(_P)]),
-    ("kc_shard_insert", C.c_int, [_P, C.c_uint64, _U64P, _U64P]),
+    ("kc_shard_expand", C.c_int, [_P, _U64P, _U64P]),
+    ("kc_shard_record_bytes", C.c_uint64, [_P]),
+    ("kc_shard_pack", C.c_int, [_P, _P]),
+    ("kc_shard_insert", C.c_int, [_P, _P, C.c_uint64, _U64P, _U64P]),
+    ("kc_shard_advance", C.c_int, [_P]),
+    ("kc_shard_parent_key", C.c_int, [_P, C.c_int, C.c_uint64, _U64P]),
+    ("kc_shard_frontier_tuple", C.c_int, [_P, C.c_uint64, _U64P]),
     ("kc_shard_result", C.c_int, [_P, C.POINTER(KcResult)]),
+    ("kc_shard_owner", C.c_int, [C.c_uint64, C.c_int]),
     ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_init", C.c_int, [C.POINTER(KcModelConfig), _U64P, C.c_int]),

@@ -1,0 +1,269 @@
+"""Fingerprint-owner-sharded BFS across GPUs (one process per GPU).
+
+Replaces TLC's single-host worker pool for the KubeAPI hot path (TLC's own
+distributed mode, RMI TLCServer/TLCWorker, is off in Model_1:
+KubeAPI___Model_1.launch:4-7).  Each rank owns the fingerprints with
+owner(fp) = floor(fp * R / 2^63), their FPSet shard and the frontier of the
+states it owns.  Per BFS level:
+
+    expand (local dedup)  ->  pack records per owner  ->  all-to-all (counts,
+    then records)  ->  insert (dedup by min key, FPSet shard, compact)  ->
+    all-reduce (new-state count SUM, error key MIN)  ->  advance
+
+All state data moves over RCCL (torch.distributed backend "nccl" on ROCm)
+between HBM buffers; the host only sees counts.  Level-synchronous, so
+traces stay shortest and totals do not depend on R.
+
+The stage implementation ("backend") is libkubecheck.so's kc_shard_* on the
+GPU (:class:`HipShard`).  The driver only needs the stage protocol, which
+is how the CPU tests exercise it under gloo with a host emulation of the
+stages.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import ACTIONS, INVARIANTS, ModelConfig, Spec
+from ._lib import KcResult, check, load
+
+NONE_KEY = (1 << 63) - 1       # "no error" in the int64 all-reduce
+M44 = (1 << 44) - 1
+
+
+def owner(fp: int, world: int) -> int:
+    """owner(fp) = floor(fp * R / 2^63) for a normalised fingerprint."""
+    return ((fp & ((1 << 63) - 1)) * world) >> 63
+
+
+class HipShard:
+    """kc_shard_* stages on this process's GPU (device = cfg.device)."""
+
+    device_type = "cuda"
+
+    def __init__(self, cfg: ModelConfig, rank: int, world: int):
+        self._lib = load()
+        self.cfg, self.rank, self.world = cfg, rank, world
+        self._c = cfg.to_c()
+        self._h = C.c_void_p()
+        check("kc_shard_create", self._lib.kc_shard_create(C.byref(self._c), rank, world, C.byref(self._h)))
+        self.record_bytes = int(self._lib.kc_shard_record_bytes(self._h))
+        self.tuple_words = self._lib.kc_spec_tuple_words(cfg.nc, cfg.np, cfg.ns)
+
+    def init(self) -> int:
+        n = C.c_uint64()
+        check("kc_shard_init", self._lib.kc_shard_init(self._h, C.byref(n)))
+        return n.value
+
+    def expand(self):
+        counts = (C.c_uint64 * self.world)()
+        err = C.c_uint64()
+        check("kc_shard_expand", self._lib.kc_shard_expand(self._h, counts, C.byref(err)))
+        return [int(x) for x in counts], int(err.value)
+
+    def pack(self, send) -> None:
+        check("kc_shard_pack", self._lib.kc_shard_pack(self._h, C.c_void_p(send.data_ptr())))
+
+    def insert(self, recv, n: int):
+        nn, err = C.c_uint64(), C.c_uint64()
+        check("kc_shard_insert", self._lib.kc_shard_insert(
+            self._h, C.c_void_p(recv.data_ptr()), n, C.byref(nn), C.byref(err)))
+        return int(nn.value), int(err.value)
+
+    def advance(self) -> None:
+        check("kc_shard_advance", self._lib.kc_shard_advance(self._h))
+
+    def parent_key(self, level: int, idx: int) -> int:
+        k = C.c_uint64()
+        check("kc_shard_parent_key", self._lib.kc_shard_parent_key(self._h, level, idx, C.byref(k)))
+        return int(k.value)
+
+    def result(self) -> dict:
+        r = KcResult()
+        check("kc_shard_result", self._lib.kc_shard_result(self._h, C.byref(r)))
+        return {"act_gen": [int(r.act_gen[i]) for i in range(len(ACTIONS))],
+                "act_dist": [int(r.act_dist[i]) for i in range(len(ACTIONS))],
+                "init": int(r.init), "generated": int(r.generated), "distinct": int(r.distinct),
+                "fpset_slots": int(r.fpset_slots)}
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.kc_shard_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+class ShardedModelChecker:
+    """Level-synchronous sharded BFS driver (collectives via torch.distributed)."""
+
+    def __init__(self, cfg: ModelConfig, backend, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.cfg, self.be, self.group = cfg, backend, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.dev = torch.device(backend.device_type, torch.cuda.current_device()) \
+            if backend.device_type == "cuda" else torch.device("cpu")
+        self._send = torch.empty(0, dtype=torch.uint8, device=self.dev)
+        self._recv = torch.empty(0, dtype=torch.uint8, device=self.dev)
+        self.spec = Spec(cfg)
+
+    # -- collectives -----------------------------------------------------
+    def _i64(self, vals: Sequence[int]):
+        return self.torch.tensor(list(vals), dtype=self.torch.int64, device=self.dev)
+
+    def _allreduce(self, vals: Sequence[int], op) -> List[int]:
+        t = self._i64(vals)
+        self.dist.all_reduce(t, op=op, group=self.group)
+        return [int(x) for x in t.tolist()]
+
+    def _buffer(self, name: str, nbytes: int):
+        buf = getattr(self, name)
+        if buf.numel() < nbytes:
+            buf = self.torch.empty(max(nbytes, 2 * buf.numel()), dtype=self.torch.uint8, device=self.dev)
+            setattr(self, name, buf)
+        return buf
+
+    def _sync(self):
+        if self.dev.type == "cuda":
+            self.torch.cuda.current_stream().synchronize()
+
+    # -- the BFS ---------------------------------------------------------
+    def run(self) -> dict:
+        dist, be, rb = self.dist, self.be, self.be.record_bytes
+        t0 = time.perf_counter()
+        n_local = be.init()
+        width = self._allreduce([n_local], dist.ReduceOp.SUM)[0]
+        widths = [width]
+        level, err = 1, NONE_KEY
+        while True:
+            if self.cfg.max_levels and level >= self.cfg.max_levels:
+                break
+            counts, e1 = be.expand()
+            send = self._buffer("_send", max(sum(counts), 1) * rb)
+            be.pack(send)
+            # exchange: counts first, then the records (one all-to-all each)
+            cin = self._i64(counts)
+            cout = self.torch.empty_like(cin)
+            dist.all_to_all_single(cout, cin, group=self.group)
+            rcounts = [int(x) for x in cout.tolist()]
+            recv = self._buffer("_recv", max(sum(rcounts), 1) * rb)
+            dist.all_to_all_single(recv[: sum(rcounts) * rb], send[: sum(counts) * rb],
+                                   output_split_sizes=[c * rb for c in rcounts],
+                                   input_split_sizes=[c * rb for c in counts], group=self.group)
+            self._sync()
+            n_new, e2 = be.insert(recv, sum(rcounts))
+            e = min(e1, e2)
+            [err] = self._allreduce([e if e < NONE_KEY else NONE_KEY], dist.ReduceOp.MIN)
+            [total_new] = self._allreduce([n_new], dist.ReduceOp.SUM)
+            if err != NONE_KEY:
+                break
+            if total_new == 0:
+                break
+            be.advance()
+            level += 1
+            widths.append(total_new)
+        seconds = time.perf_counter() - t0
+        res = be.result()
+        agg = self._allreduce(res["act_gen"] + res["act_dist"] +
+                              [res["init"], res["generated"], res["distinct"]], dist.ReduceOp.SUM)
+        na = len(ACTIONS)
+        out = {
+            "init": agg[2 * na], "generated": agg[2 * na] + agg[2 * na + 1],
+            "distinct": agg[2 * na + 2], "depth": len(widths), "level_width": widths,
+            "act_gen": dict(zip(ACTIONS, agg[:na])), "act_dist": dict(zip(ACTIONS, agg[na:2 * na])),
+            "seconds": seconds, "error": None, "complete": err == NONE_KEY and not (
+                self.cfg.max_levels and level >= self.cfg.max_levels),
+        }
+        if err != NONE_KEY:
+            out.update(self._error(err, level))
+        return out
+
+    # -- counterexamples -------------------------------------------------
+    def _query_parent(self, rank: int, level: int, idx: int) -> int:
+        key = self.be.parent_key(level, idx) if self.rank == rank else 0
+        t = self._i64([key - (1 << 64) if key >= (1 << 63) else key])
+        self.dist.broadcast(t, src=rank, group=self.group)
+        v = int(t.item())
+        return v + (1 << 64) if v < 0 else v
+
+    def _error(self, err: int, level: int) -> dict:
+        kind = err & 0xff
+        rank, pidx, pos = err >> 60, (err >> 16) & M44, (err >> 8) & 0xff
+        path = []            # successor ordinals from an Init state
+        r, idx, lvl = rank, pidx, level
+        while lvl > 1:
+            key = self._query_parent(r, lvl, idx)
+            path.append((key >> 8) & 0xff)
+            r, idx, lvl = key >> 60, (key >> 16) & M44, lvl - 1
+        init_key = self._query_parent(r, 1, idx)
+        states = [self.spec.init()[init_key & 0xffff]]
+        for t in reversed(path):
+            succ, _ = self.spec.successors(states[-1])
+            states.append(succ[t][1])
+        out = {"error_level": level}
+        if kind == 2:                           # invariant violated by successor `pos`
+            succ, _ = self.spec.successors(states[-1])
+            states.append(succ[pos][1])
+            out.update(error="invariant", error_invariant=self.spec.check_invariants(states[-1]),
+                       error_level=level + 1)
+        elif kind == 0x12:                      # an Init state violates an invariant
+            out.update(error="invariant", error_invariant=self.spec.check_invariants(states[-1]))
+        elif kind == 1:
+            _, fail = self.spec.successors(states[-1])
+            out.update(error="assertion", error_action=fail)
+        else:
+            out.update(error="deadlock")
+        out["trace"] = [[int(x) for x in s] for s in states]
+        out["trace_len"] = len(states)
+        return out
+
+
+def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
+    """bench.py --gpus N: every rank checks its shard; rank 0 reports."""
+    import torch
+    import torch.distributed as dist
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20)
+    be = HipShard(cfg, rank, world)
+    mc = ShardedModelChecker(cfg, be)
+    for _ in range(args.warmup):
+        mc.run()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = mc.run()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    be.close()
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "distinct states/sec (KubeAPI TLC BFS)",
+            "value": round(res["distinct"] * args.steps / dt, 1),
+            "unit": "distinct states/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (the model's Init states; no external input)",
+            "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
+                       "distinct": res["distinct"], "generated": res["generated"],
+                       "depth": res["depth"],
+                       "parallelism": f"{world} GPUs, fingerprint-owner sharding, "
+                                      "RCCL all-to-all per BFS level"},
+        }
+    dist.destroy_process_group()
+    return out
