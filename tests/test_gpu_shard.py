@@ -1,0 +1,134 @@
+"""HIP shard stages (kc_shard_*) on one GPU: R ranks emulated in one process
+by exchanging the device send buffers directly (the box has one GPU; RCCL
+needs one process per GPU).  Counts, widths, per-action generated counts
+and error traces must equal the single-GPU/oracle results for every R.
+Also runs the real driver (RCCL via torch.distributed) at world_size 1."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from kubecheck import ACTIONS, ModelConfig, Spec
+from kubecheck.distributed import HipShard, NONE_KEY
+
+pytestmark = pytest.mark.gpu
+
+
+def emulate(R, **kw):
+    cfg = ModelConfig(**kw)
+    shards = [HipShard(cfg, r, R) for r in range(R)]
+    rb = shards[0].record_bytes
+    n = sum(s.init() for s in shards)
+    widths, err = [n], NONE_KEY
+    while True:
+        sends, counts = [], []
+        for s in shards:
+            c, e = s.expand()
+            err = min(err, e)
+            buf = torch.empty(max(sum(c), 1) * rb, dtype=torch.uint8, device="cuda")
+            s.pack(buf)
+            sends.append(buf)
+            counts.append(c)
+        total = 0
+        for r, s in enumerate(shards):
+            parts, m = [], 0
+            for src in range(R):
+                off = sum(counts[src][:r]) * rb
+                parts.append(sends[src][off: off + counts[src][r] * rb])
+                m += counts[src][r]
+            recv = torch.cat(parts) if m else torch.empty(rb, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            nn, e = s.insert(recv, m)
+            err = min(err, e)
+            total += nn
+        if err != NONE_KEY or total == 0:
+            break
+        for s in shards:
+            s.advance()
+        widths.append(total)
+    res = [s.result() for s in shards]
+    out = {"level_width": widths, "err": err,
+           "distinct": sum(r["distinct"] for r in res),
+           "generated": sum(r["init"] + r["generated"] for r in res),
+           "act_gen": dict(zip(ACTIONS, np.sum([r["act_gen"] for r in res], axis=0).tolist()))}
+    for s in shards:
+        s.close()
+    return out
+
+
+@pytest.mark.parametrize("R", [1, 2, 4, 8])
+def test_model1_any_shard_count(fixtures, R):
+    fx = fixtures["model1"]
+    r = emulate(R)
+    assert r["err"] == NONE_KEY
+    assert r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+    assert r["act_gen"] == fx["act_gen"]
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_errors_sharded(fixtures, R):
+    r = emulate(R, nc=2)
+    assert r["err"] & 0xFF == 1 and len(r["level_width"]) == 10
+    assert r["level_width"] == fixtures["nc2"]["level_width"]
+    r = emulate(R, variant=2)
+    assert r["err"] & 0xFF == 2
+    assert len(r["level_width"]) + 1 == fixtures["variant2"]["err_level"]
+
+
+def test_enlarged_prefix_sharded(fixtures):
+    fx = fixtures["np2_40levels"]
+    assert emulate_levels(4, 40, np=2) == fx["level_width"]
+
+
+def emulate_levels(R, L, **kw):
+    cfg = ModelConfig(**kw)
+    shards = [HipShard(cfg, r, R) for r in range(R)]
+    rb = shards[0].record_bytes
+    widths = [sum(s.init() for s in shards)]
+    while len(widths) < L:
+        sends, counts = [], []
+        for s in shards:
+            c, _ = s.expand()
+            buf = torch.empty(max(sum(c), 1) * rb, dtype=torch.uint8, device="cuda")
+            s.pack(buf)
+            sends.append(buf)
+            counts.append(c)
+        total = 0
+        for r, s in enumerate(shards):
+            parts = [sends[src][sum(counts[src][:r]) * rb: (sum(counts[src][:r]) + counts[src][r]) * rb]
+                     for src in range(R)]
+            m = sum(counts[src][r] for src in range(R))
+            torch.cuda.synchronize()
+            total += s.insert(torch.cat(parts), m)[0]
+        for s in shards:
+            s.advance()
+        widths.append(total)
+    for s in shards:
+        s.close()
+    return widths
+
+
+def test_driver_world1_rccl(fixtures):
+    import torch.distributed as dist
+    from kubecheck.distributed import ShardedModelChecker
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        cfg = ModelConfig()
+        r = ShardedModelChecker(cfg, HipShard(cfg, 0, 1)).run()
+        fx = fixtures["model1"]
+        assert r["level_width"] == fx["level_width"]
+        assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+        cfg2 = ModelConfig(nc=2)
+        r2 = ShardedModelChecker(cfg2, HipShard(cfg2, 0, 1)).run()
+        assert r2["error"] == "assertion" and r2["trace"] == fixtures["nc2"]["trace"]
+    finally:
+        dist.destroy_process_group()
