@@ -6,6 +6,10 @@ import sys
 
 import pytest
 
+# torch first (its first import on a fresh box is slow, and it must own the
+# process's HIP runtime before libkubecheck.so loads: see kubecheck/_lib.py)
+import torch  # noqa: F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "tla-kubernetes_amd"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:

@@ -121,6 +121,14 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 and
+    # cannot initialise on top of /opt/rocm's if that one is loaded first, so
+    # when torch is installed it is loaded before libkubecheck (whose
+    # libamdhip64.so.7 dependency then resolves to the already-loaded copy).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libkubecheck.so not found at {LIB_PATH}; build it with "
