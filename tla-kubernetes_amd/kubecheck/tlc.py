@@ -162,8 +162,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         else:
             out(2114, "Deadlock reached.", 1)
         out(2121, "The behavior up to this point is:", 1)
-        for i, block in enumerate(r.trace_text.split("State ")[1:], 1):
-            out(2217, f"{i}: " + block.split(":", 1)[1].strip(), 4)
+        blocks = re.split(r"^State (\d+):$", r.trace_text, flags=re.M)[1:]
+        for num, body in zip(blocks[0::2], blocks[1::2]):
+            out(2217, f"{num}: {body.strip()}", 4)
     out(2201, "The coverage statistics:")
     for name in kubecheck.ACTIONS:
         out(2772, f"<{name}>: {r.act_dist[name]}:{r.act_gen[name]}")
