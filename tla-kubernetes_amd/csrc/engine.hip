@@ -158,7 +158,9 @@ class EngineT final : public EngineBase {
       }
     }
 
-    const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 21)) + 255) / 256 * 256;
+    // default: one chunk per level (the batch table is sized exactly from the
+    // previous level's successor count); chunk_states bounds its memory
+    const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 40)) + 255) / 256 * 256;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
       // capacity for this level's output (cand is exact: next_cand of the
@@ -176,32 +178,37 @@ class EngineT final : public EngineBase {
       // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
-      // multi-chunk level: exact candidate count per chunk first
       const uint64_t nchunks = (n + chunk - 1) / chunk;
-      if (nchunks > 1) {
-        KC_TRY(grow_buffer(d_chunk_cand_, chunk_cand_cap_, nchunks, false, st_));
-        KC_HIP_TRY(hipMemsetAsync(d_chunk_cand_, 0, nchunks * 8, st_));
-        hipLaunchKernelGGL(k_count_chunks<M>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st_,
-                           cur_, n, chunk, flags_, d_chunk_cand_);
-        chunk_cand_.resize(nchunks);
-        KC_HIP_TRY(hipMemcpyAsync(chunk_cand_.data(), d_chunk_cand_, nchunks * 8,
-                                  hipMemcpyDeviceToHost, st_));
-        KC_HIP_TRY(hipStreamSynchronize(st_));
-      }
       for (uint64_t start = 0; start < n; start += chunk) {
         const uint64_t cn = std::min(chunk, n - start);
-        // batch table: >= 2x the chunk's candidates, a power of two
-        const uint64_t ccand = nchunks > 1 ? chunk_cand_[start / chunk] : cand;
-        const uint64_t bcap = next_pow2(2 * ccand + 256);
-        res->batch_inserts += ccand;
+        // batch table: 2x the chunk's successors.  Exact for a one-chunk level
+        // (cand = the previous level's emit count); for several chunks the
+        // level average, re-run with 2x slots if a probe run overflows
+        // (k_expand only claims entries, so it can be repeated).
+        const uint64_t est = nchunks > 1 ? (uint64_t)((double)cand * cn / n * 1.25) + 1024 : cand;
+        uint64_t bcap = next_pow2(2 * est + 256);
+        for (int attempt = 0;; ++attempt) {
+          KC_TRY(bt_.ensure(bcap, st_));
+          KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
+          timed(KK_EXPAND, [&] {
+            hipLaunchKernelGGL(k_expand<M>, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, st_,
+                               cur_ + start, cn, start, flags_, cfg_.check_deadlock, bt_.t, bcap - 1,
+                               d_ctr_);
+          });
+          if (nchunks == 1) break;
+          unsigned long long over = 0;
+          KC_HIP_TRY(hipMemcpyAsync(&over, &d_ctr_->batch_used, 8, hipMemcpyDeviceToHost, st_));
+          KC_HIP_TRY(hipStreamSynchronize(st_));
+          if (!over) break;
+          if (attempt > 6) {
+            set_error("kubecheck: batch table overflow");
+            return -ENOMEM;
+          }
+          KC_HIP_TRY(hipMemsetAsync(&d_ctr_->batch_used, 0, 8, st_));
+          bcap *= 2;
+        }
+        res->batch_inserts += est;
         ++res->levels_chunks;
-        KC_TRY(bt_.ensure(bcap, st_));
-        KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
-        timed(KK_EXPAND, [&] {
-          hipLaunchKernelGGL(k_expand<M>, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, st_,
-                             cur_ + start, cn, start, flags_, cfg_.check_deadlock, bt_.t, bcap - 1,
-                             d_ctr_);
-        });
         const unsigned grid = (unsigned)((cn + 255) / 256);
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_resolve<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
@@ -228,7 +235,7 @@ class EngineT final : public EngineBase {
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
-      if (c.overflow) {
+      if (c.overflow || c.batch_used) {
         set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
         return -ENOMEM;
       }
@@ -427,7 +434,6 @@ class EngineT final : public EngineBase {
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     for (auto& e : ev_pool_) (void)hipEventDestroy(e);
-    if (d_chunk_cand_) (void)hipFree(d_chunk_cand_);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
@@ -446,9 +452,6 @@ class EngineT final : public EngineBase {
   uint64_t scan_cap_ = 0;
   Counters* d_ctr_ = nullptr;
   Counters* h_ctr_ = nullptr;
-  unsigned long long* d_chunk_cand_ = nullptr;
-  uint64_t chunk_cand_cap_ = 0;
-  std::vector<unsigned long long> chunk_cand_;
   std::vector<hipEvent_t> ev_pool_;
   std::vector<int> ev_kind_;
   size_t ev_used_ = 0;

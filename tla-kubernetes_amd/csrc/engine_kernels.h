@@ -37,7 +37,7 @@ struct Counters {
   unsigned long long next_cand;   // successors of the new states (next level's work)
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
-  unsigned long long batch_used;  // (unused)
+  unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
   unsigned long long probes;      // FPSet probes (cumulative over the run)
   unsigned long long pad[2];
 };
@@ -70,7 +70,10 @@ __device__ __forceinline__ bool batch_insert_bounded(BatchEntry* __restrict__ t,
                                                      uint64_t fp, uint64_t key) {
   const unsigned long long nk = ~(unsigned long long)key;
   uint64_t i = batch_slot(fp, mask);
-  for (uint64_t probe = 0; probe <= mask; ++probe) {
+  // a probe run this long means the table is overfull (at <= 50% load the
+  // chance is negligible): report it and let the host retry with 2x slots
+  const uint64_t max_probe = mask < 1024 ? mask : 1024;
+  for (uint64_t probe = 0; probe <= max_probe; ++probe) {
     const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&t[i]);
     unsigned long long efp = e.x, ekey = e.y;
     if (efp == 0ull) {
@@ -94,40 +97,30 @@ template <class M>
 __global__ void __launch_bounds__(256)
 k_expand(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
          int check_deadlock, BatchEntry* __restrict__ bt, uint64_t bmask, Counters* __restrict__ C) {
-  __shared__ unsigned int sh_act[A_COUNT];
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
-  __syncthreads();
+  // Idempotent (batch-table claims and min error keys only), so the host can
+  // re-run a chunk with a larger table if a probe run reports overflow.
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const typename M::State s = load_state<M>(cur, i);
-    const typename M::Plan pl = M::plan(s, f);
-    const uint64_t pidx = base + i;
-    if (pl.fail_pos >= 0)
-      atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
-    else if (pl.total == 0 && check_deadlock)
-      atomicMin(&C->err_key, (pidx << 16) | E_DEADLOCK);
-    int tot = pl.total;
-    if (tot > M::MAXSUCC) {
-      atomicAdd(&C->overflow, 1ull);
-      tot = M::MAXSUCC;
-    }
-#pragma unroll
-    for (int slot = 0; slot < M::NSLOT; ++slot) {
-      const int c = (int)((pl.counts >> (6 * slot)) & 63);
-      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
-    }
-    for (int t = 0; t < tot; ++t) {
-      int slot, j;
-      M::locate(pl, t, slot, j);
-      typename M::State x;
-      M::apply(s, slot, j, f, x);
-      if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t))
-        atomicAdd(&C->overflow, 1ull);
-    }
+  if (i >= n) return;
+  const typename M::State s = load_state<M>(cur, i);
+  const typename M::Plan pl = M::plan(s, f);
+  const uint64_t pidx = base + i;
+  if (pl.fail_pos >= 0)
+    atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
+  else if (pl.total == 0 && check_deadlock)
+    atomicMin(&C->err_key, (pidx << 16) | E_DEADLOCK);
+  int tot = pl.total;
+  if (tot > M::MAXSUCC) {
+    atomicAdd(&C->overflow, 1ull);
+    tot = M::MAXSUCC;
   }
-  __syncthreads();
-  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  for (int t = 0; t < tot; ++t) {
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    typename M::State x;
+    M::apply(s, slot, j, f, x);
+    if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t))
+      atomicAdd(&C->batch_used, 1ull);      // batch table overfull: host retries
+  }
 }
 
 template <class M>
@@ -136,6 +129,9 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
           const BatchEntry* __restrict__ bt, uint64_t bmask, unsigned long long* __restrict__ slots,
           uint64_t nbuckets, uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
           Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < n;
   typename M::State s;
@@ -146,6 +142,14 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
   const int tot = !live ? 0 : pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
   uint32_t mask = 0;
   unsigned probes = 0;
+  // per-action "generated" counters (TLC msg 2772, second number)
+  if (live) {
+#pragma unroll
+    for (int slot = 0; slot < M::NSLOT; ++slot) {
+      const int c = (int)((pl.counts >> (6 * slot)) & 63);
+      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
+    }
+  }
   for (int t = 0; t < tot; ++t) {
     int slot, j;
     M::locate(pl, t, slot, j);
@@ -168,6 +172,9 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
   if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&C->probes, pw);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 template <class M>
@@ -219,20 +226,6 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&C->act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&C->next_cand, sh_cand);
-}
-
-// Successor totals per chunk of `chunk` parents (chunk % 256 == 0, so each
-// block lies in one chunk): sizes the batch tables of multi-chunk levels.
-template <class M>
-__global__ void __launch_bounds__(256)
-k_count_chunks(const typename M::State* __restrict__ cur, uint64_t n, uint64_t chunk, Flags f,
-               unsigned long long* __restrict__ chunk_cand) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long c = 0;
-  if (i < n) c = (unsigned long long)M::plan(load_state<M>(cur, i), f).total;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&chunk_cand[((uint64_t)blockIdx.x * blockDim.x) / chunk], c);
 }
 
 }  // namespace kc

@@ -48,29 +48,42 @@ template <class M>
 __global__ void __launch_bounds__(256)
 k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f,
               const BatchEntry* __restrict__ bt, uint64_t bmask, uint32_t world,
-              uint32_t* __restrict__ cnt /* [world][n] */, uint32_t* __restrict__ repmask) {
+              uint32_t* __restrict__ cnt /* [world][n] */, uint32_t* __restrict__ repmask,
+              Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const typename M::State s = load_state<M>(cur, i);
-  const typename M::Plan pl = M::plan(s, f);
-  const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
-  uint32_t c[16] = {};
-  uint32_t mask = 0;
-  for (int t = 0; t < tot; ++t) {
-    int slot, j;
-    M::locate(pl, t, slot, j);
-    typename M::State x;
-    M::apply(s, slot, j, f, x);
-    const uint64_t fp = M::fingerprint(x);
-    if (batch_is_rep(bt, bmask, fp, (i << 8) | (uint64_t)t)) {
-      mask |= 1u << t;
-      const uint32_t o = owner_of(fp, world);
+  if (i < n) {
+    const typename M::State s = load_state<M>(cur, i);
+    const typename M::Plan pl = M::plan(s, f);
+    const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
 #pragma unroll
-      for (uint32_t k = 0; k < 16; ++k) c[k] += (k == o);
+    for (int slot = 0; slot < M::NSLOT; ++slot) {       // per-action "generated"
+      const int c = (int)((pl.counts >> (6 * slot)) & 63);
+      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
     }
+    uint32_t c[16] = {};
+    uint32_t mask = 0;
+    for (int t = 0; t < tot; ++t) {
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      M::apply(s, slot, j, f, x);
+      const uint64_t fp = M::fingerprint(x);
+      if (batch_is_rep(bt, bmask, fp, (i << 8) | (uint64_t)t)) {
+        mask |= 1u << t;
+        const uint32_t o = owner_of(fp, world);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) c[k] += (k == o);
+      }
+    }
+    repmask[i] = mask;
+    for (uint32_t k = 0; k < world; ++k) cnt[(uint64_t)k * n + i] = c[k];
   }
-  repmask[i] = mask;
-  for (uint32_t k = 0; k < world; ++k) cnt[(uint64_t)k * n + i] = c[k];
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 template <class M>
@@ -281,7 +294,7 @@ class ShardT final : public ShardBase {
     KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
     hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(256), 0, st_, cur_, n_, flags_, bt_.t,
-                       bcap - 1, (uint32_t)world_, cnt_, repmask_);
+                       bcap - 1, (uint32_t)world_, cnt_, repmask_, d_ctr_);
     size_t tmp_bytes = 0;
     KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)n_, st_));
     KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
@@ -297,7 +310,7 @@ class ShardT final : public ShardBase {
     }
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
-    if (h_ctr_->overflow) {
+    if (h_ctr_->overflow || h_ctr_->batch_used) {
       set_error("kc_shard_expand: successor overflow / batch table full");
       return -ENOMEM;
     }
@@ -359,7 +372,7 @@ class ShardT final : public ShardBase {
       KC_HIP_TRY(hipMemcpyAsync(&lc, isnew_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipStreamSynchronize(st_));
-      if (h_ctr_->overflow) {
+      if (h_ctr_->overflow || h_ctr_->batch_used) {
         set_error("kc_shard_insert: table full");
         return -ENOMEM;
       }
