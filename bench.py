@@ -85,6 +85,26 @@ def roofline_bfs(times, res, S):
     }
 
 
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    summary for this workload (profiles/<round>_<workload>_rocprof_summary.json,
+    written by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE
+    passes, gfx950-corrected).  bench.py cannot collect PMC counters itself
+    (they need their own rocprofv3 run), so the figure is the profile's."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_rocprof_summary.json")))
+    if not files:
+        return None, None
+    try:
+        with open(files[-1]) as fh:
+            k = json.load(fh)["kernels"].get(kernel, {})
+    except (OSError, ValueError):
+        return None, None
+    b = k.get("hbm_bytes_per_launch")
+    return (int(b) if b else None), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(kw, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
@@ -142,6 +162,10 @@ def bench_single(args, kw, desc):
     }
     if not args.no_timing:
         name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, state_bytes(kw))
+        roof["traffic"], src = pmc_traffic(args.workload, roof["kernel"])
+        if src:
+            roof["traffic_unit"] = "HBM bytes per launch (PMC)"
+            roof["traffic_source"] = src
         out["roofline"] = roof
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items()}
     mc.close()
