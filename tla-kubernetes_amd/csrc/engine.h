@@ -11,6 +11,9 @@ namespace kc {
 
 // Kernel kinds timed by the engine (kc_engine_kernel_times order).
 enum KernelKind { KK_EXPAND = 0, KK_RESOLVE = 1, KK_SCAN = 2, KK_EMIT = 3, KK_COUNT = 4 };
+// diagnostic-only ablation timings (KC_ABLATE=1 in the environment): extra
+// launches of cut-down k_claim variants on scratch buffers, printed to stderr
+enum AblateKind { KA_LDS = KK_COUNT, KA_COMPUTE = KK_COUNT + 1, KA_TOTAL = KK_COUNT + 2 };
 
 class EngineBase {
  public:
@@ -36,8 +39,9 @@ class EngineBase {
   kc_model_config cfg_;
   int capture_level_ = 0;
   bool timing_ = false;
-  double ktime_ms_[KK_COUNT] = {};
-  uint64_t klaunch_[KK_COUNT] = {};
+  double ktime_ms_[KA_TOTAL] = {};
+  uint64_t klaunch_[KA_TOTAL] = {};
+  bool ablate_ = false;
 };
 
 std::unique_ptr<EngineBase> make_engine(const kc_model_config& cfg);

@@ -4,8 +4,8 @@
 //
 // Per level (all on one HIP stream, one host sync per level):
 //   for each chunk of <= chunk_states parents:
-//     memset batch table; k_expand; k_resolve; hipcub exclusive scan;
-//     k_emit; k_advance
+//     k_claim (LDS tile dedup + ClaimSet claims); k_settle (winners);
+//     hipcub exclusive scan; k_emit; k_advance
 //   read {next width, next candidates, error key} back.
 // The frontier buffers are the StateQueue: double-buffered packed states
 // in HBM, FIFO order = (parent order, TLC successor order), identical to a
@@ -54,6 +54,9 @@ class EngineT final : public EngineBase {
   explicit EngineT(const kc_model_config& cfg) : EngineBase(cfg) {
     flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
     timing_ = cfg.timing != 0;
+    const char* ab = getenv("KC_ABLATE");
+    ablate_ = ab && ab[0] == '1';
+    if (ablate_) timing_ = true;
   }
   ~EngineT() override { release(); }
 
@@ -98,14 +101,13 @@ class EngineT final : public EngineBase {
       fps[k] = M::fingerprint(init[k]);
       cand += (uint64_t)M::plan(init[k], flags_).total;
     }
-    // the FPSet allocation is kept across runs (cleared each run), like a
+    // the seen-set allocation is kept across runs (cleared each run), like a
     // TLC FPSet pre-sized with -fpmem; it grows by rehash when needed
     const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
-    if (fps_.slots && fps_.capacity() >= fp_slots) {
-      KC_HIP_TRY(hipMemsetAsync(fps_.slots, 0, fps_.nbuckets * 64, st_));
-      fps_.count = 0;
+    if (cs_.t && cs_.capacity() >= fp_slots) {
+      KC_TRY(cs_.clear(st_));
     } else {
-      KC_TRY(fps_.init(fp_slots, st_));
+      KC_TRY(cs_.init(fp_slots, st_));
     }
     KC_TRY(grow_buffer(cur_, cur_cap_, (uint64_t)ni, false, st_));
     KC_TRY(grow_buffer(parent_, par_cap_, (uint64_t)ni + cand, false, st_));
@@ -116,7 +118,7 @@ class EngineT final : public EngineBase {
     KC_HIP_TRY(hipMalloc(&d_fps, ni * 8));
     KC_HIP_TRY(hipMalloc(&d_res, ni * sizeof(int)));
     KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), ni * 8, hipMemcpyHostToDevice, st_));
-    launch_fpset_insert_list(d_fps, (uint64_t)ni, fps_, d_res, st_);
+    launch_claimset_insert_list(d_fps, (uint64_t)ni, cs_, 1u, d_res, st_);
     std::vector<int> ires(ni);
     KC_HIP_TRY(hipMemcpyAsync(ires.data(), d_res, ni * sizeof(int), hipMemcpyDeviceToHost, st_));
     std::vector<unsigned long long> ipar(ni, ~0ull);
@@ -128,12 +130,12 @@ class EngineT final : public EngineBase {
     (void)hipFree(d_fps);
     (void)hipFree(d_res);
     for (int k = 0; k < ni; ++k) {
-      if (ires[k] != 1) {
+      if (ires[k] != CL_NEW) {
         set_error("kubecheck: init states not distinct");
         return -EIO;
       }
     }
-    fps_.count = ni;
+    cs_.count = ni;
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
     res->init = ni;
     res->generated = ni;
@@ -158,11 +160,16 @@ class EngineT final : public EngineBase {
       }
     }
 
-    // default: one chunk per level (the batch table is sized exactly from the
-    // previous level's successor count); chunk_states bounds its memory
+    // default: one chunk per level; chunk_states bounds the per-chunk
+    // buffers.  Claims are level-global (keys grow with the parent index),
+    // so a chunk's winners are final once its own claim pass is done.
     const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 40)) + 255) / 256 * 256;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
+      if (n >= (1ull << 32)) {
+        set_error("kubecheck: level wider than 2^32 states");
+        return -ENOMEM;
+      }
       // capacity for this level's output (cand is exact: next_cand of the
       // previous level)
       KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
@@ -171,49 +178,51 @@ class EngineT final : public EngineBase {
         KC_TRY(grow_buffer(parent_, par_cap_, next_gidx + cand + 1, true, st_));
         KC_TRY(grow_buffer(ord_, ord_cap_, next_gidx + cand + 1, true, st_));
       }
-      KC_TRY(fps_.reserve(cand, st_));
+      KC_TRY(cs_.reserve(cand, st_));
+      KC_TRY(grow_buffer(curmask_, cur_mcap_, std::min(n, chunk), false, st_));
+      {
+        const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
+        KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
+        KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
+        KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+      }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(newcnt_, cnt_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
       // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
-      const uint64_t nchunks = (n + chunk - 1) / chunk;
+      const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
       for (uint64_t start = 0; start < n; start += chunk) {
         const uint64_t cn = std::min(chunk, n - start);
-        // batch table: 2x the chunk's successors.  Exact for a one-chunk level
-        // (cand = the previous level's emit count); for several chunks the
-        // level average, re-run with 2x slots if a probe run overflows
-        // (k_expand only claims entries, so it can be repeated).
-        const uint64_t est = nchunks > 1 ? (uint64_t)((double)cand * cn / n * 1.25) + 1024 : cand;
-        uint64_t bcap = next_pow2(2 * est + 256);
-        for (int attempt = 0;; ++attempt) {
-          KC_TRY(bt_.ensure(bcap, st_));
-          KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
-          timed(KK_EXPAND, [&] {
-            hipLaunchKernelGGL(k_expand<M>, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, st_,
-                               cur_ + start, cn, start, flags_, cfg_.check_deadlock, bt_.t, bcap - 1,
-                               d_ctr_);
-          });
-          if (nchunks == 1) break;
-          unsigned long long over = 0;
-          KC_HIP_TRY(hipMemcpyAsync(&over, &d_ctr_->batch_used, 8, hipMemcpyDeviceToHost, st_));
-          KC_HIP_TRY(hipStreamSynchronize(st_));
-          if (!over) break;
-          if (attempt > 6) {
-            set_error("kubecheck: batch table overflow");
-            return -ENOMEM;
-          }
-          KC_HIP_TRY(hipMemsetAsync(&d_ctr_->batch_used, 0, 8, st_));
-          bcap *= 2;
-        }
-        res->batch_inserts += est;
         ++res->levels_chunks;
         const unsigned grid = (unsigned)((cn + 255) / 256);
+        const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
+        timed(KK_EXPAND, [&] {
+          hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
+                             start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets, succ_level,
+                             curmask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+        });
+        if (ablate_) {
+          KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
+          timed(KA_LDS, [&] {
+            hipLaunchKernelGGL((k_claim<M, 1>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets,
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+          });
+          timed(KA_COMPUTE, [&] {
+            hipLaunchKernelGGL((k_claim<M, 2>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets,
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+          });
+        }
         timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_resolve<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
-                             flags_, bt_.t, bcap - 1, fps_.slots, fps_.nbuckets, newmask_, newcnt_,
+          hipLaunchKernelGGL(k_settle_rec, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
+                             cs_.nbuckets, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
                              d_ctr_);
+          hipLaunchKernelGGL(k_settle_tile<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
+                             cn, start, flags_, cs_.t, cs_.nbuckets, succ_level, rcount_, curmask_,
+                             newmask_, newcnt_, d_ctr_);
         });
         size_t tmp_bytes = 0;
         KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt_, offsets_, (int)cn, st_));
@@ -243,7 +252,7 @@ class EngineT final : public EngineBase {
       for (int a = 0; a < A_COUNT; ++a) gen += c.act_gen[a];
       res->generated = ni + gen;
       const uint64_t n_new = c.chunk_base;
-      fps_.count += n_new;
+      cs_.count += n_new;
       res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
       if (c.err_key != ~0ull) {
         KC_TRY(report_error(res, c.err_key, level, level_gidx, n));
@@ -278,6 +287,10 @@ class EngineT final : public EngineBase {
     last_level_ = res->nlevels;
     last_n_ = n;
     finish(res, t0, n);
+    if (ablate_)
+      fprintf(stderr, "kubecheck ablate: claim %.2f ms | successors+LDS %.2f ms | successors only %.2f ms | settle %.2f | emit %.2f ms\n",
+              ktime_ms_[KK_EXPAND], ktime_ms_[KA_LDS], ktime_ms_[KA_COMPUTE], ktime_ms_[KK_RESOLVE],
+              ktime_ms_[KK_EMIT]);
     return 0;
   }
 
@@ -420,16 +433,16 @@ class EngineT final : public EngineBase {
     res->complete = (left == 0 && res->err_kind == 0 && !(cfg_.max_levels && res->nlevels >= cfg_.max_levels && left));
     const double d = (double)res->distinct, gg = (double)res->generated;
     res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
-    res->fpset_slots = fps_.capacity();
+    res->fpset_slots = cs_.capacity();
     res->fpset_probes = h_ctr_->probes;
+    res->batch_inserts = h_ctr_->settles;
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
   void release() {
     (void)hipSetDevice(cfg_.device);
-    fps_.release();
-    bt_.release();
-    for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_,
+    cs_.release();
+    for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)curmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
                     (void*)newcnt_, (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
@@ -439,15 +452,20 @@ class EngineT final : public EngineBase {
 
   Flags flags_{};
   hipStream_t st_ = nullptr;
-  DevFpset fps_;
-  DevBatchTable bt_;
+  DevClaimSet cs_;
   State *cur_ = nullptr, *next_ = nullptr;
   uint64_t cur_cap_ = 0, next_cap_ = 0;
   unsigned long long* parent_ = nullptr;
   uint8_t* ord_ = nullptr;
   uint64_t par_cap_ = 0, ord_cap_ = 0;
   uint32_t *newmask_ = nullptr, *newcnt_ = nullptr, *offsets_ = nullptr;
-  uint64_t mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
+  uint32_t* curmask_ = nullptr;
+  uint32_t* abl_mask_ = nullptr;
+  unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
+  unsigned long long* rec_fp_ = nullptr;
+  uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;
+  uint64_t abl_cap_ = 0;
+  uint64_t cur_mcap_ = 0, mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
   Counters* d_ctr_ = nullptr;

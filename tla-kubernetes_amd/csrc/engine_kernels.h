@@ -38,8 +38,9 @@ struct Counters {
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
   unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
-  unsigned long long probes;      // FPSet probes (cumulative over the run)
-  unsigned long long pad[2];
+  unsigned long long probes;      // FPSet / ClaimSet probes (cumulative over the run)
+  unsigned long long settles;     // ClaimSet re-reads in k_settle (cumulative)
+  unsigned long long pad;
 };
 
 template <class M>
@@ -175,6 +176,244 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+}
+
+// ------------------------------------------------------------------------
+// Single-GPU engine, claim path (ClaimSet, fpset_dev.h).
+//
+//   k_claim  : one workgroup = TILE consecutive parents.  Every successor's
+//              fingerprint goes into an LDS hash table keeping the minimum
+//              tile-local key (parent << 5 | position); siblings in BFS order
+//              produce the same state often (diamonds: a-then-b = b-then-a),
+//              so about half of all successors die here without touching HBM.
+//              Then each tile representative claims its fp in the ClaimSet
+//              (one 64-B bucket read; atomics only for current-level fps).
+//              Per parent: bitmask of successors that may have won (curmask);
+//              per tile: the list of those candidates {fp, tile-local key}.
+//   k_settle_rec : re-reads each candidate's claim and keeps those whose
+//              claim is the stored minimum -> newmask / newcnt (scan + emit);
+//              no successor is re-derived.
+//   k_settle_tile: the same for a tile whose candidate list overflowed, by
+//              re-deriving its curmask successors.
+// Tile-local dedup only ever discards a copy whose fp is held by a smaller
+// key of the same tile, which can never be the level minimum; an LDS table
+// overflow just sends the copy to the ClaimSet directly.
+constexpr int CLAIM_TILE = 256;
+constexpr int CLAIM_LDS_BITS = 11;
+constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
+// Candidate records per tile (tile representatives whose claim may have won):
+// fp + tile-local key, for k_settle_rec.  A tile with more candidates than
+// CLAIM_RCAP is settled by k_settle_tile (re-derivation from curmask).
+constexpr int CLAIM_RCAP = 1024;
+
+__device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t tile,
+                                               unsigned long long* __restrict__ rec_fp,
+                                               unsigned int* __restrict__ rec_lk, uint64_t fp,
+                                               unsigned int lk) {
+  const unsigned int k = atomicAdd(sh_rc, 1u);
+  if (k < CLAIM_RCAP) {
+    rec_fp[tile * CLAIM_RCAP + k] = fp;
+    rec_lk[tile * CLAIM_RCAP + k] = lk;
+  }
+}
+
+__device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int* sh_key,
+                                         uint64_t fp, unsigned int lk) {
+  unsigned int h = (unsigned int)((fp * 0xd6e8feb86659fd93ull) >> (64 - CLAIM_LDS_BITS));
+  for (int p = 0; p < CLAIM_LDS; ++p) {
+    unsigned long long e = __hip_atomic_load(&sh_fp[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (e == 0ull) {
+      e = atomicCAS(&sh_fp[h], 0ull, (unsigned long long)fp);
+      if (e == 0ull) e = fp;
+    }
+    if (e == fp) {
+      atomicMin(&sh_key[h], lk);
+      return (int)h;
+    }
+    h = (h + 1) & (CLAIM_LDS - 1);
+  }
+  return -1;
+}
+
+// ABL (diagnostic builds of the same kernel, launched on scratch buffers when
+// KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only.
+template <class M, int ABL = 0>
+__global__ void __launch_bounds__(CLAIM_TILE)
+k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+        int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+        uint32_t* __restrict__ curmask, unsigned int* __restrict__ rcount,
+        unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
+        Counters* __restrict__ C) {
+  __shared__ unsigned long long sh_fp[CLAIM_LDS];
+  __shared__ unsigned int sh_key[CLAIM_LDS];
+  __shared__ unsigned int sh_cur[CLAIM_TILE];
+  __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned int sh_rc;
+  if (threadIdx.x == 0) sh_rc = 0;
+  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+    sh_fp[k] = 0ull;
+    sh_key[k] = ~0u;
+  }
+  sh_cur[threadIdx.x] = 0;
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
+  const uint64_t i = tile0 + threadIdx.x;
+  const bool live = i < n;
+  unsigned probes = 0;
+  if (live) {
+    const typename M::State s = load_state<M>(cur, i);
+    const typename M::Plan pl = M::plan(s, f);
+    const uint64_t pidx = base + i;
+    if (ABL == 0) {
+      if (pl.fail_pos >= 0)
+        atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
+      else if (pl.total == 0 && check_deadlock)
+        atomicMin(&C->err_key, (pidx << 16) | E_DEADLOCK);
+#pragma unroll
+      for (int slot = 0; slot < M::NSLOT; ++slot) {      // per-action "generated" (msg 2772)
+        const int c = (int)((pl.counts >> (6 * slot)) & 63);
+        if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
+      }
+    }
+    int tot = pl.total;
+    if (tot > M::MAXSUCC) {
+      if (ABL == 0) atomicAdd(&C->overflow, 1ull);
+      tot = M::MAXSUCC;
+    }
+    uint64_t acc = 0;
+    for (int t = 0; t < tot; ++t) {
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      M::apply(s, slot, j, f, x);
+      const uint64_t fp = M::fingerprint(x);
+      if (ABL == 2) {
+        acc ^= fp;
+        continue;
+      }
+      if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
+        // LDS table full: claim this copy directly
+        ++probes;
+        const int r = claimset_claim(cs, nbuckets, fp, make_claim(level, (pidx << 8) | (uint64_t)t), level);
+        if (r >= CL_CUR) {
+          if (r == CL_FULL) {
+            atomicAdd(&C->overflow, 1ull);
+          } else {
+            atomicOr(&sh_cur[threadIdx.x], 1u << t);
+            push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
+          }
+        }
+      }
+    }
+    if (ABL == 2) sh_cur[threadIdx.x] = (unsigned)acc;
+  }
+  __syncthreads();
+  if (ABL != 0) {
+    if (live) curmask[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
+    return;
+  }
+  // every tile representative claims its fp in the ClaimSet
+  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+    const unsigned long long fp = sh_fp[k];
+    if (!fp) continue;
+    const unsigned int lk = sh_key[k];
+    const unsigned int lp = lk >> 5, t = lk & 31;
+    const uint64_t pidx = base + tile0 + lp;
+    ++probes;
+    const int r = claimset_claim(cs, nbuckets, fp, make_claim(level, (pidx << 8) | t), level);
+    if (r >= CL_CUR) {
+      if (r == CL_FULL) {
+        atomicAdd(&C->overflow, 1ull);
+      } else {
+        atomicOr(&sh_cur[lp], 1u << t);
+        push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk);
+      }
+    }
+  }
+  __syncthreads();
+  if (live) curmask[i] = sh_cur[threadIdx.x];
+  if (threadIdx.x == 0) rcount[blockIdx.x] = sh_rc;
+  unsigned long long pw = probes;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
+  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&C->probes, pw);
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+}
+
+// k_settle_rec: one workgroup per claim tile; each candidate record re-reads
+// its claim (one bucket line) and wins iff the stored claim is its own.
+static __global__ void __launch_bounds__(CLAIM_TILE)
+k_settle_rec(uint64_t n, uint64_t base, const ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+             uint32_t level, const unsigned int* __restrict__ rcount,
+             const unsigned long long* __restrict__ rec_fp, const unsigned int* __restrict__ rec_lk,
+             uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_new[CLAIM_TILE];
+  const unsigned int cnt = rcount[blockIdx.x];
+  if (cnt > CLAIM_RCAP) return;                   // k_settle_tile's tile
+  sh_new[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
+  unsigned reads = 0;
+  for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
+    const uint64_t r = (uint64_t)blockIdx.x * CLAIM_RCAP + k;
+    const unsigned long long fp = rec_fp[r];
+    const unsigned int lk = rec_lk[r];
+    const uint64_t pidx = base + tile0 + (lk >> 5);
+    ++reads;
+    if (~claimset_get(cs, nbuckets, fp) == make_claim(level, (pidx << 8) | (lk & 31)))
+      atomicOr(&sh_new[lk >> 5], 1u << (lk & 31));
+  }
+  __syncthreads();
+  const uint64_t i = tile0 + threadIdx.x;
+  if (i < n) {
+    newmask[i] = sh_new[threadIdx.x];
+    newcnt[i] = (uint32_t)__popc(sh_new[threadIdx.x]);
+  }
+  unsigned long long rw = reads;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
+  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&C->settles, rw);
+}
+
+// k_settle_tile: the tiles whose candidate list overflowed CLAIM_RCAP
+// re-derive their curmask successors (every other tile returns at once).
+template <class M>
+__global__ void __launch_bounds__(CLAIM_TILE)
+k_settle_tile(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+              const ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+              const unsigned int* __restrict__ rcount, const uint32_t* __restrict__ curmask,
+              uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
+              Counters* __restrict__ C) {
+  if (rcount[blockIdx.x] <= CLAIM_RCAP) return;
+  const uint64_t i = (uint64_t)blockIdx.x * CLAIM_TILE + threadIdx.x;
+  uint32_t nm = 0;
+  unsigned reads = 0;
+  if (i < n) {
+    uint32_t mask = curmask[i];
+    if (mask) {
+      const typename M::State s = load_state<M>(cur, i);
+      const typename M::Plan pl = M::plan(s, f);
+      const uint64_t pidx = base + i;
+      for (; mask; mask &= mask - 1) {
+        const int t = __ffs(mask) - 1;
+        int slot, j;
+        M::locate(pl, t, slot, j);
+        typename M::State x;
+        M::apply(s, slot, j, f, x);
+        ++reads;
+        const unsigned long long nc = claimset_get(cs, nbuckets, M::fingerprint(x));
+        if (~nc == make_claim(level, (pidx << 8) | (uint64_t)t)) nm |= 1u << t;
+      }
+    }
+    newmask[i] = nm;
+    newcnt[i] = (uint32_t)__popc(nm);
+  }
+  unsigned long long rw = reads;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
+  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&C->settles, rw);
 }
 
 template <class M>

@@ -96,6 +96,100 @@ int DevFpset::reserve(uint64_t extra, hipStream_t st) {
   return 0;
 }
 
+// ---------------------------------------------------------------- ClaimSet
+// Move every entry of `old` into `nw` (fps are unique, so the claim word is
+// a plain store next to the CAS'd fp).
+__global__ void k_claimset_rehash(const ClaimEntry* __restrict__ old, uint64_t old_slots,
+                                  ClaimEntry* __restrict__ nw, uint64_t new_buckets,
+                                  unsigned long long* __restrict__ fail) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_slots) return;
+  const ClaimEntry e = old[i];
+  if (!e.fp) return;
+  uint64_t b = bucket_of(e.fp, new_buckets);
+  for (uint64_t probe = 0; probe < new_buckets; ++probe) {
+    ClaimEntry* bk = nw + b * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (bk[k].fp == 0ull && atomicCAS(&bk[k].fp, 0ull, e.fp) == 0ull) {
+        bk[k].nclaim = e.nclaim;
+        return;
+      }
+    }
+    b = (b + 1 == new_buckets) ? 0 : b + 1;
+  }
+  atomicAdd(fail, 1ull);
+}
+
+__global__ void k_claimset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
+                                       ClaimEntry* __restrict__ t, uint64_t nbuckets,
+                                       uint32_t level, int* __restrict__ result) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int r = claimset_claim(t, nbuckets, fps[i], make_claim(level, i), level);
+    if (result) result[i] = r;
+  }
+}
+
+void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevClaimSet& cs,
+                                 uint32_t level, int* d_res, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_claimset_insert_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d_fps, n, cs.t, cs.nbuckets, level, d_res);
+}
+
+int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
+  release();
+  nbuckets = (min_slots + 3) / 4;
+  if (nbuckets < 8) nbuckets = 8;
+  KC_HIP_TRY(hipMalloc(&t, nbuckets * 64));
+  KC_HIP_TRY(hipMemsetAsync(t, 0, nbuckets * 64, st));
+  KC_HIP_TRY(hipMalloc(&d_fail, sizeof(unsigned long long)));
+  count = 0;
+  return 0;
+}
+
+int DevClaimSet::clear(hipStream_t st) {
+  KC_HIP_TRY(hipMemsetAsync(t, 0, nbuckets * 64, st));
+  count = 0;
+  return 0;
+}
+
+void DevClaimSet::release() {
+  if (t) (void)hipFree(t);
+  if (d_fail) (void)hipFree(d_fail);
+  t = nullptr;
+  d_fail = nullptr;
+  nbuckets = 0;
+  count = 0;
+}
+
+int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
+  if ((count + extra) * 2 <= capacity()) return 0;
+  uint64_t nb = nbuckets;
+  while ((count + extra) * 3 > nb * 4) nb *= 2;      // land at <= 1/3 load
+  ClaimEntry* ns = nullptr;
+  KC_HIP_TRY(hipMalloc(&ns, nb * 64));
+  KC_HIP_TRY(hipMemsetAsync(ns, 0, nb * 64, st));
+  KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
+  const uint64_t old_slots = capacity();
+  hipLaunchKernelGGL(k_claimset_rehash, dim3((unsigned)((old_slots + 255) / 256)), dim3(256), 0, st,
+                     t, old_slots, ns, nb, d_fail);
+  KC_HIP_TRY(hipGetLastError());
+  unsigned long long fail = 0;
+  KC_HIP_TRY(hipMemcpyAsync(&fail, d_fail, sizeof fail, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  if (fail) {
+    (void)hipFree(ns);
+    set_error("claimset rehash failed (%llu)", fail);
+    return -ENOMEM;
+  }
+  KC_HIP_TRY(hipFree(t));
+  t = ns;
+  nbuckets = nb;
+  return 0;
+}
+
 int DevBatchTable::ensure(uint64_t entries, hipStream_t st) {
   (void)st;
   if (entries <= cap) return 0;

@@ -22,6 +22,25 @@ struct DevFpset {
   int reserve(uint64_t extra, hipStream_t st);
 };
 
+// Host owner of the engine's ClaimSet (fpset_dev.h): nbuckets * 4 entries.
+struct DevClaimSet {
+  ClaimEntry* t = nullptr;
+  uint64_t nbuckets = 0;
+  uint64_t count = 0;                   // host-tracked number of stored fps
+  unsigned long long* d_fail = nullptr;
+
+  uint64_t capacity() const { return nbuckets * 4; }
+  int init(uint64_t min_slots, hipStream_t st);
+  int clear(hipStream_t st);
+  void release();
+  // grow (rehash) so that count + extra <= 1/2 of capacity
+  int reserve(uint64_t extra, hipStream_t st);
+};
+// claim a device list of (normalised) fps at `level` with keys 0..n-1;
+// d_res[i] = ClaimResult (may be NULL)
+void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevClaimSet& cs,
+                                 uint32_t level, int* d_res, hipStream_t st);
+
 // Batch table used to dedup a batch by minimum order key.
 struct DevBatchTable {
   BatchEntry* t = nullptr;

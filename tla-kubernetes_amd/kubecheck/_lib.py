@@ -10,7 +10,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libkubecheck.so")
+LIB_PATH = os.environ.get("KUBECHECK_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libkubecheck.so")
 
 KC_NACTIONS = 22
 KC_MAX_LEVELS = 4096
