@@ -142,7 +142,7 @@ class EngineT final : public EngineBase {
     res->distinct = ni;
     init_states_ = init;
 
-    uint64_t n = ni, level_gidx = 0;
+    uint64_t n = ni, level_gidx = 0, cand_total = 0;
     int level = 1;
     res->level_width[0] = n;
     res->nlevels = 1;
@@ -191,7 +191,7 @@ class EngineT final : public EngineBase {
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
       // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
-      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
+      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->chunk_base, 0, 3 * 8, st_));
       const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
       for (uint64_t start = 0; start < n; start += chunk) {
         const uint64_t cn = std::min(chunk, n - start);
@@ -200,28 +200,28 @@ class EngineT final : public EngineBase {
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
-                             start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets, succ_level,
+                             start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
                              curmask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
           timed(KA_LDS, [&] {
             hipLaunchKernelGGL((k_claim<M, 1>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
-                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                                succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
           });
           timed(KA_COMPUTE, [&] {
             hipLaunchKernelGGL((k_claim<M, 2>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
-                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nbuckets,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                                succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
           });
         }
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nbuckets, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
                              d_ctr_);
           hipLaunchKernelGGL(k_settle_tile<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
-                             cn, start, flags_, cs_.t, cs_.nbuckets, succ_level, rcount_, curmask_,
+                             cn, start, flags_, cs_.t, cs_.nslots, succ_level, rcount_, curmask_,
                              newmask_, newcnt_, d_ctr_);
         });
         size_t tmp_bytes = 0;
@@ -249,7 +249,7 @@ class EngineT final : public EngineBase {
         return -ENOMEM;
       }
       uint64_t gen = 0;
-      for (int a = 0; a < A_COUNT; ++a) gen += c.act_gen[a];
+      for (int a = 0; a < A_COUNT; ++a) gen += c.act_gen(a);
       res->generated = ni + gen;
       const uint64_t n_new = c.chunk_base;
       cs_.count += n_new;
@@ -273,7 +273,8 @@ class EngineT final : public EngineBase {
       std::swap(cur_, next_);
       std::swap(cur_cap_, next_cap_);
       n = n_new;
-      cand = c.next_cand;
+      cand = c.next_cand() - cand_total;
+      cand_total += cand;
       ++level;
       if (n) {
         if (level > KC_MAX_LEVELS) {
@@ -425,8 +426,8 @@ class EngineT final : public EngineBase {
 
   void finish(kc_result* res, std::chrono::steady_clock::time_point t0, uint64_t left) {
     for (int a = 0; a < A_COUNT; ++a) {
-      res->act_gen[a] = h_ctr_->act_gen[a];
-      res->act_dist[a] = h_ctr_->act_dist[a];
+      res->act_gen[a] = h_ctr_->act_gen(a);
+      res->act_dist[a] = h_ctr_->act_dist(a);
     }
     res->depth = res->nlevels;
     res->queue_left = left;
@@ -434,8 +435,8 @@ class EngineT final : public EngineBase {
     const double d = (double)res->distinct, gg = (double)res->generated;
     res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
     res->fpset_slots = cs_.capacity();
-    res->fpset_probes = h_ctr_->probes;
-    res->batch_inserts = h_ctr_->settles;
+    res->fpset_probes = h_ctr_->probes();
+    res->batch_inserts = h_ctr_->settles();
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 

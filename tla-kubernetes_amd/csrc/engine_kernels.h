@@ -30,18 +30,49 @@
 
 namespace kc {
 
-struct Counters {
+// Counters.  Totals that every workgroup adds to (per-action counts, probe
+// counts, the next level's candidate count) are striped over CTR_STRIPES
+// rows in separate cache lines, row = blockIdx.x % CTR_STRIPES: one hot
+// address taking an atomic from every workgroup serialises at the memory
+// side (it cost k_settle_rec 4/5 of its time).  The host sums the rows.
+constexpr int CTR_STRIPES = 64;
+struct CtrStripe {                  // 512 B
   unsigned long long act_gen[A_COUNT];
   unsigned long long act_dist[A_COUNT];
+  unsigned long long probes;        // FPSet / ClaimSet probes
+  unsigned long long settles;       // ClaimSet re-reads in k_settle_*
+  unsigned long long next_cand;     // successors of the new states (cumulative)
+  unsigned long long pad[64 - 2 * A_COUNT - 3];
+};
+struct Counters {
   unsigned long long err_key;     // min error key of the level (~0 = none)
-  unsigned long long next_cand;   // successors of the new states (next level's work)
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
   unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
-  unsigned long long probes;      // FPSet / ClaimSet probes (cumulative over the run)
-  unsigned long long settles;     // ClaimSet re-reads in k_settle (cumulative)
-  unsigned long long pad;
+  unsigned long long head_pad[12];
+  CtrStripe s[CTR_STRIPES];
+
+  unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
+  unsigned long long act_dist(int a) const { return sum(&CtrStripe::act_dist, a); }
+  unsigned long long probes() const { return sum1(&CtrStripe::probes); }
+  unsigned long long settles() const { return sum1(&CtrStripe::settles); }
+  unsigned long long next_cand() const { return sum1(&CtrStripe::next_cand); }
+
+ private:
+  unsigned long long sum(unsigned long long (CtrStripe::*f)[A_COUNT], int a) const {
+    unsigned long long t = 0;
+    for (int k = 0; k < CTR_STRIPES; ++k) t += (s[k].*f)[a];
+    return t;
+  }
+  unsigned long long sum1(unsigned long long CtrStripe::*f) const {
+    unsigned long long t = 0;
+    for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].*f;
+    return t;
+  }
 };
+__device__ __forceinline__ CtrStripe& stripe(Counters* C) {
+  return C->s[blockIdx.x & (CTR_STRIPES - 1)];
+}
 
 template <class M>
 __device__ __forceinline__ typename M::State load_state(const typename M::State* __restrict__ p,
@@ -172,10 +203,10 @@ k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, 
   unsigned long long pw = probes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
-  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&C->probes, pw);
+  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------
@@ -337,9 +368,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   unsigned long long pw = probes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
-  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&C->probes, pw);
+  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 // k_settle_rec: one workgroup per claim tile; each candidate record re-reads
@@ -374,7 +405,7 @@ k_settle_rec(uint64_t n, uint64_t base, const ClaimEntry* __restrict__ cs, uint6
   unsigned long long rw = reads;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
-  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&C->settles, rw);
+  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
 }
 
 // k_settle_tile: the tiles whose candidate list overflowed CLAIM_RCAP
@@ -413,7 +444,7 @@ k_settle_tile(const typename M::State* __restrict__ cur, uint64_t n, uint64_t ba
   unsigned long long rw = reads;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
-  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&C->settles, rw);
+  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
 }
 
 template <class M>
@@ -463,8 +494,8 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
-  if (threadIdx.x == 0 && sh_cand) atomicAdd(&C->next_cand, sh_cand);
+    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
 
 }  // namespace kc

@@ -100,33 +100,29 @@ int DevFpset::reserve(uint64_t extra, hipStream_t st) {
 // Move every entry of `old` into `nw` (fps are unique, so the claim word is
 // a plain store next to the CAS'd fp).
 __global__ void k_claimset_rehash(const ClaimEntry* __restrict__ old, uint64_t old_slots,
-                                  ClaimEntry* __restrict__ nw, uint64_t new_buckets,
+                                  ClaimEntry* __restrict__ nw, uint64_t new_slots,
                                   unsigned long long* __restrict__ fail) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= old_slots) return;
   const ClaimEntry e = old[i];
   if (!e.fp) return;
-  uint64_t b = bucket_of(e.fp, new_buckets);
-  for (uint64_t probe = 0; probe < new_buckets; ++probe) {
-    ClaimEntry* bk = nw + b * 4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (bk[k].fp == 0ull && atomicCAS(&bk[k].fp, 0ull, e.fp) == 0ull) {
-        bk[k].nclaim = e.nclaim;
-        return;
-      }
+  uint64_t k = bucket_of(e.fp, new_slots);
+  for (uint64_t probe = 0; probe < new_slots; ++probe) {
+    if (nw[k].fp == 0ull && atomicCAS(&nw[k].fp, 0ull, e.fp) == 0ull) {
+      nw[k].nclaim = e.nclaim;
+      return;
     }
-    b = (b + 1 == new_buckets) ? 0 : b + 1;
+    k = (k + 1 == new_slots) ? 0 : k + 1;
   }
   atomicAdd(fail, 1ull);
 }
 
 __global__ void k_claimset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
-                                       ClaimEntry* __restrict__ t, uint64_t nbuckets,
+                                       ClaimEntry* __restrict__ t, uint64_t nslots,
                                        uint32_t level, int* __restrict__ result) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const int r = claimset_claim(t, nbuckets, fps[i], make_claim(level, i), level);
+    const int r = claimset_claim(t, nslots, fps[i], make_claim(level, i), level);
     if (result) result[i] = r;
   }
 }
@@ -135,22 +131,21 @@ void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevCla
                                  uint32_t level, int* d_res, hipStream_t st) {
   if (n)
     hipLaunchKernelGGL(k_claimset_insert_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       d_fps, n, cs.t, cs.nbuckets, level, d_res);
+                       d_fps, n, cs.t, cs.nslots, level, d_res);
 }
 
 int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
   release();
-  nbuckets = (min_slots + 3) / 4;
-  if (nbuckets < 8) nbuckets = 8;
-  KC_HIP_TRY(hipMalloc(&t, nbuckets * 64));
-  KC_HIP_TRY(hipMemsetAsync(t, 0, nbuckets * 64, st));
+  nslots = min_slots < 64 ? 64 : min_slots;
+  KC_HIP_TRY(hipMalloc(&t, nslots * sizeof(ClaimEntry)));
+  KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * sizeof(ClaimEntry), st));
   KC_HIP_TRY(hipMalloc(&d_fail, sizeof(unsigned long long)));
   count = 0;
   return 0;
 }
 
 int DevClaimSet::clear(hipStream_t st) {
-  KC_HIP_TRY(hipMemsetAsync(t, 0, nbuckets * 64, st));
+  KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * sizeof(ClaimEntry), st));
   count = 0;
   return 0;
 }
@@ -160,33 +155,33 @@ void DevClaimSet::release() {
   if (d_fail) (void)hipFree(d_fail);
   t = nullptr;
   d_fail = nullptr;
-  nbuckets = 0;
+  nslots = 0;
   count = 0;
 }
 
+// Linear probing stays short below 1/2 load; grow to land at <= 1/3.
 int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
   if ((count + extra) * 2 <= capacity()) return 0;
-  uint64_t nb = nbuckets;
-  while ((count + extra) * 3 > nb * 4) nb *= 2;      // land at <= 1/3 load
-  ClaimEntry* ns = nullptr;
-  KC_HIP_TRY(hipMalloc(&ns, nb * 64));
-  KC_HIP_TRY(hipMemsetAsync(ns, 0, nb * 64, st));
+  uint64_t ns = nslots;
+  while ((count + extra) * 3 > ns) ns *= 2;
+  ClaimEntry* nt = nullptr;
+  KC_HIP_TRY(hipMalloc(&nt, ns * sizeof(ClaimEntry)));
+  KC_HIP_TRY(hipMemsetAsync(nt, 0, ns * sizeof(ClaimEntry), st));
   KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
-  const uint64_t old_slots = capacity();
-  hipLaunchKernelGGL(k_claimset_rehash, dim3((unsigned)((old_slots + 255) / 256)), dim3(256), 0, st,
-                     t, old_slots, ns, nb, d_fail);
+  hipLaunchKernelGGL(k_claimset_rehash, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, st,
+                     t, nslots, nt, ns, d_fail);
   KC_HIP_TRY(hipGetLastError());
   unsigned long long fail = 0;
   KC_HIP_TRY(hipMemcpyAsync(&fail, d_fail, sizeof fail, hipMemcpyDeviceToHost, st));
   KC_HIP_TRY(hipStreamSynchronize(st));
   if (fail) {
-    (void)hipFree(ns);
+    (void)hipFree(nt);
     set_error("claimset rehash failed (%llu)", fail);
     return -ENOMEM;
   }
   KC_HIP_TRY(hipFree(t));
-  t = ns;
-  nbuckets = nb;
+  t = nt;
+  nslots = ns;
   return 0;
 }
 

@@ -20,8 +20,8 @@
 //    touches the FPSet.  Sized ~2x the batch so it stays in L2/MALL.
 //    (Used by kc_fpset_put_batch and the sharded stages.)
 //
-//  * ClaimSet (the single-GPU engine's seen-set): the two fused — 64-B
-//    buckets of 4 {fp, ~claim} entries, see below.
+//  * ClaimSet (the single-GPU engine's seen-set): the two fused — 16-B
+//    {fp, ~claim} slots with linear probing, see below.
 //
 // Visibility: stale L1 copies can only show a slot as empty (0) that was
 // filled in this launch; every such slot is re-checked by the CAS, whose
@@ -102,14 +102,17 @@ __device__ __forceinline__ int fpset_contains(const unsigned long long* __restri
 
 // ---------------------------------------------------------------- ClaimSet
 // The BFS engine's seen-set: the FPSet fused with the per-level "first
-// occurrence" table.  A 64-B bucket holds 4 entries {fp, ~claim}, where
-// claim = level << 40 | key and key = (parent index in level) << 8 |
-// (successor position).  Within one level every copy of a fingerprint does
-// atomicMax(~claim), so after the level's claim pass the entry holds the
-// SMALLEST key (the state a 1-worker TLC BFS meets first).  Entries of older
-// levels carry smaller levels, so a claim never changes them and a probe
-// that finds one knows the state is old without any write.  ~claim = 0
-// (never written) reads as "claim pending, current level".
+// occurrence" table.  Open addressing with linear probing over 16-B slots
+// {fp, ~claim}, where claim = level << 40 | key and key = (parent index in
+// level) << 8 | (successor position).  A probe is ONE 16-B load (measured on
+// MI355X: one 16-B load per lane reaches ~48 G random probes/s at 16-64 GB
+// tables, a lane reading a whole 64-B bucket with four loads ~20 G/s;
+// tools/microbench/random_probe.hip).  Within one level every copy of a
+// fingerprint does atomicMax(~claim), so after the level's claim pass the
+// slot holds the SMALLEST key (the state a 1-worker TLC BFS meets first).
+// Slots of older levels carry smaller levels, so a claim never changes them
+// and a probe that finds one knows the state is old without any write.
+// ~claim = 0 (never written) reads as "claim pending, current level".
 struct ClaimEntry {
   unsigned long long fp;
   unsigned long long nclaim;  // ~(level << 40 | key); 0 = not yet set
@@ -134,33 +137,24 @@ __device__ __forceinline__ int claim_settle(unsigned long long* nclaim_p, unsign
 // entry already holding a smaller key; CL_OLD: stored by an earlier level;
 // CL_FULL: no empty slot anywhere.  Stale (other-XCD L2) copies can only show
 // slots as empty or claims as larger; both are settled by the atomics, whose
-// returned values are authoritative.  Slots fill in order and are never
+// returned values are authoritative.  Slots fill in probe order and are never
 // cleared, so an fp is always found before the first truly empty slot.
-__device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64_t nbuckets,
+__device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64_t nslots,
                                               uint64_t fp, uint64_t claim, uint32_t level) {
   const unsigned long long nc = ~(unsigned long long)claim;
-  uint64_t b = bucket_of(fp, nbuckets);
-  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
-    ClaimEntry* bk = t + b * 4;
-    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(bk);
-    const ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
-    const unsigned long long f[4] = {q0.x, q1.x, q2.x, q3.x};
-    const unsigned long long c[4] = {q0.y, q1.y, q2.y, q3.y};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (f[k] == fp) return claim_settle(&bk[k].nclaim, c[k], nc, level);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (f[k] == 0) {
-        const unsigned long long old = atomicCAS(&bk[k].fp, 0ull, (unsigned long long)fp);
-        if (old == 0ull) {
-          atomicMax(&bk[k].nclaim, nc);
-          return CL_NEW;
-        }
-        if (old == fp) return claim_settle(&bk[k].nclaim, 0ull, nc, level);
+  uint64_t i = bucket_of(fp, nslots);
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+    if (e.x == fp) return claim_settle(&t[i].nclaim, e.y, nc, level);
+    if (e.x == 0ull) {
+      const unsigned long long old = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (old == 0ull) {
+        atomicMax(&t[i].nclaim, nc);
+        return CL_NEW;
       }
+      if (old == fp) return claim_settle(&t[i].nclaim, 0ull, nc, level);
     }
-    b = (b + 1 == nbuckets) ? 0 : b + 1;
+    i = (i + 1 == nslots) ? 0 : i + 1;
   }
   return CL_FULL;
 }
@@ -168,17 +162,13 @@ __device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64
 // ~claim stored for fp (0 if absent).  Called in a later kernel than the
 // claims, so every claim is visible.
 __device__ __forceinline__ unsigned long long claimset_get(const ClaimEntry* __restrict__ t,
-                                                           uint64_t nbuckets, uint64_t fp) {
-  uint64_t b = bucket_of(fp, nbuckets);
-  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
-    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(t + b * 4);
-    const ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
-    if (q0.x == fp) return q0.y;
-    if (q1.x == fp) return q1.y;
-    if (q2.x == fp) return q2.y;
-    if (q3.x == fp) return q3.y;
-    if ((q0.x == 0) | (q1.x == 0) | (q2.x == 0) | (q3.x == 0)) return 0;
-    b = (b + 1 == nbuckets) ? 0 : b + 1;
+                                                           uint64_t nslots, uint64_t fp) {
+  uint64_t i = bucket_of(fp, nslots);
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+    if (e.x == fp) return e.y;
+    if (e.x == 0ull) return 0;
+    i = (i + 1 == nslots) ? 0 : i + 1;
   }
   return 0;
 }

@@ -22,14 +22,14 @@ struct DevFpset {
   int reserve(uint64_t extra, hipStream_t st);
 };
 
-// Host owner of the engine's ClaimSet (fpset_dev.h): nbuckets * 4 entries.
+// Host owner of the engine's ClaimSet (fpset_dev.h): nslots 16-B entries.
 struct DevClaimSet {
   ClaimEntry* t = nullptr;
-  uint64_t nbuckets = 0;
+  uint64_t nslots = 0;
   uint64_t count = 0;                   // host-tracked number of stored fps
   unsigned long long* d_fail = nullptr;
 
-  uint64_t capacity() const { return nbuckets * 4; }
+  uint64_t capacity() const { return nslots; }
   int init(uint64_t min_slots, hipStream_t st);
   int clear(hipStream_t st);
   void release();

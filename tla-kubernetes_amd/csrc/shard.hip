@@ -83,7 +83,7 @@ k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f,
   }
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 template <class M>
@@ -173,8 +173,8 @@ k_shard_emit(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __res
   if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&C->act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
-  if (threadIdx.x == 0 && sh_cand) atomicAdd(&C->next_cand, sh_cand);
+    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
 
 class ShardBase {
@@ -236,6 +236,7 @@ class ShardT final : public ShardBase {
       KC_TRY(fps_.init(fp_slots, st_));
     }
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
+    cand_total_ = 0;
     std::vector<State> mine;
     std::vector<unsigned long long> keys;
     std::vector<uint64_t> fps;
@@ -278,7 +279,7 @@ class ShardT final : public ShardBase {
   int expand(uint64_t* counts, uint64_t* err_key) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
-    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->next_cand, 0, 4 * 8, st_));
+    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->chunk_base, 0, 3 * 8, st_));
     for (int o = 0; o < world_; ++o) counts[o] = 0;
     send_total_ = 0;
     *err_key = init_err_;
@@ -378,7 +379,8 @@ class ShardT final : public ShardBase {
       }
       next_n_ = (uint64_t)lo + lc;
       fps_.count += next_n_;
-      next_cand_ = h_ctr_->next_cand;
+      next_cand_ = h_ctr_->next_cand() - cand_total_;
+      cand_total_ += next_cand_;
       if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
     } else {
       KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
@@ -422,15 +424,15 @@ class ShardT final : public ShardBase {
     memset(r, 0, sizeof *r);
     uint64_t gen = 0;
     for (int a = 0; a < A_COUNT; ++a) {
-      r->act_gen[a] = h_ctr_->act_gen[a];
-      r->act_dist[a] = h_ctr_->act_dist[a];
-      gen += h_ctr_->act_gen[a];
+      r->act_gen[a] = h_ctr_->act_gen(a);
+      r->act_dist[a] = h_ctr_->act_dist(a);
+      gen += r->act_gen[a];
     }
     r->init = gen_init_;
     r->generated = gen;                 // successors generated by this rank's parents
     r->distinct = fps_.count;
     r->fpset_slots = fps_.capacity();
-    r->fpset_probes = h_ctr_->probes;
+    r->fpset_probes = h_ctr_->probes();
     r->nlevels = level_;
     return 0;
   }
@@ -465,6 +467,7 @@ class ShardT final : public ShardBase {
   uint64_t* d_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
   uint64_t n_ = 0, next_n_ = 0, cand_ = 0, next_cand_ = 0, send_total_ = 0, gen_init_ = 0;
+  uint64_t cand_total_ = 0;   // cumulative next_cand counter already consumed
   uint64_t init_err_ = ~0ull;
   int level_ = 0;
   std::vector<uint64_t> level_base_;

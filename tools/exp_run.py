@@ -20,8 +20,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--nc", type=int, default=1)
 ap.add_argument("--np", type=int, default=2)
 ap.add_argument("--runs", type=int, default=2)
+ap.add_argument("--slots", type=int, default=20, help="log2 initial seen-set slots")
 a = ap.parse_args()
-cfg = kubecheck.ModelConfig(nc=a.nc, np=a.np, keep_trace=True, timing=True, fpset_slots=1 << 20)
+cfg = kubecheck.ModelConfig(nc=a.nc, np=a.np, keep_trace=True, timing=True, fpset_slots=1 << a.slots)
 with kubecheck.ModelChecker(cfg) as mc:
     for k in range(a.runs):
         t0 = time.perf_counter()

@@ -1,0 +1,11 @@
+# rocprofv3 kernel trace of tools/exp_run.py (one NP=2 check) -> summary
+set -o pipefail
+TAG=${1:-t}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+cd /tmp
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/tools/exp_run.py --runs 1 > $O/trace.log 2>&1 || { echo TRACE_FAIL; tail -20 $O/trace.log; exit 1; }
+cd $R
+python3 tools/pmc_summary.py --trace $O/trace --out $O/summary.json
