@@ -209,17 +209,6 @@ struct Model {
     }
     return r;
   }
-  KC_HD static int pc_d(const State& s, int a) { return (int)getf(aw_d(s, a), F_PC, B_PC); }
-  KC_HD static int fld_d(const State& s, int a, int off, int n) { return (int)getf(aw_d(s, a), off, n); }
-  KC_HD static void put_d(State& s, int a, int off, int n, int v) {
-#pragma unroll
-    for (int k = 0; k < A; ++k) {
-      const uint64_t w = s.w[1 + k];
-      uint64_t nw = setf(w, off, n, (uint64_t)v);
-      opaque(nw);
-      s.w[1 + k] = (a == k) ? nw : w;
-    }
-  }
   KC_HD static uint64_t objs_d(const State& s, int a) {
     uint64_t r = 0;
 #pragma unroll
@@ -419,157 +408,183 @@ struct Model {
     j = t;
   }
 
-  KC_HD static void push_api(State& t, int a, int ret) {
-    put_d(t, a, F_SD, 1, 1); put_d(t, a, F_SPROC, 2, PR_API); put_d(t, a, F_SRET, 5, ret);
-    put_d(t, a, F_SOP, 3, fld_d(t, a, F_OP, 3)); put_d(t, a, F_SOBJ, OBJB, fld_d(t, a, F_OBJ, OBJB));
-    put_d(t, a, F_SKIND, 2, 0);
+  // ---- one actor's scalar word, held in a register while an action
+  // rewrites it (each field access is a shift/mask on that word; the word
+  // is selected once and written back once, instead of a select over every
+  // actor word per field).
+  KC_HD static int g(uint64_t w, int off, int n) { return (int)getf(w, off, n); }
+  KC_HD static uint64_t sw(uint64_t w, int off, int n, int v) { return setf(w, off, n, (uint64_t)v); }
+  // the call-stack fields [F_SD, F_OP) are contiguous
+  static constexpr uint64_t FRAME_MASK = ((1ull << (F_OP - F_SD)) - 1) << F_SD;
+  KC_HD static uint64_t push_api_w(uint64_t w, int ret) {       // API(...) call frame
+    const int op = g(w, F_OP, 3), ob = g(w, F_OBJ, OBJB);
+    w &= ~FRAME_MASK;
+    w = sw(w, F_SD, 1, 1); w = sw(w, F_SPROC, 2, PR_API); w = sw(w, F_SRET, 5, ret);
+    w = sw(w, F_SOP, 3, op); w = sw(w, F_SOBJ, OBJB, ob);
+    return w;
   }
-  KC_HD static void push_list(State& t, int a, int ret) {
-    put_d(t, a, F_SD, 1, 1); put_d(t, a, F_SPROC, 2, PR_ListAPI); put_d(t, a, F_SRET, 5, ret);
-    put_d(t, a, F_SOP, 3, 0); put_d(t, a, F_SOBJ, OBJB, 0); put_d(t, a, F_SKIND, 2, fld_d(t, a, F_KIND, 2));
+  KC_HD static uint64_t push_list_w(uint64_t w, int ret) {      // ListAPI(...) call frame
+    const int kd = g(w, F_KIND, 2);
+    w &= ~FRAME_MASK;
+    w = sw(w, F_SD, 1, 1); w = sw(w, F_SPROC, 2, PR_ListAPI); w = sw(w, F_SRET, 5, ret);
+    w = sw(w, F_SKIND, 2, kd);
+    return w;
   }
-  KC_HD static void pop(State& t, int a) {
-    put_d(t, a, F_SD, 1, 0); put_d(t, a, F_SPROC, 2, 0); put_d(t, a, F_SRET, 5, 0);
-    put_d(t, a, F_SOP, 3, 0); put_d(t, a, F_SOBJ, OBJB, 0); put_d(t, a, F_SKIND, 2, 0);
+  KC_HD static uint64_t call_w(uint64_t w, int ret, int op, int oc) {
+    w = push_api_w(w, ret);
+    w = sw(w, F_OBJ, OBJB, oc); w = sw(w, F_OP, 3, op);
+    return sw(w, F_PC, B_PC, L_DoRequest);
   }
-  KC_HD static void call(State& t, int a, int ret, int op, int oc) {
-    push_api(t, a, ret);
-    put_d(t, a, F_OBJ, OBJB, oc); put_d(t, a, F_OP, 3, op); put_d(t, a, F_PC, B_PC, L_DoRequest);
+  // write actor a's word (select over the A words; values behind opaque())
+  KC_HD static void put_word_d(State& t, int a, uint64_t nw) {
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      uint64_t v = nw;
+      opaque(v);
+      t.w[1 + k] = (a == k) ? v : t.w[1 + k];
+    }
   }
 
   // Build successor j of slot `slot` into t (t starts as a copy of s).  One
   // copy of every action body, indexed by the runtime actor (apply is the
   // part of the kernel that runs once per successor).
   KC_HD static void apply_rt(const State& s, int slot, int j, const Flags& f, State& t) {
-    if (slot < A) {
-      const int a = slot;
-      const int p = pc_d(s, a);
-      if (p == L_DoRequest) {                                   // DoRequest :471-483
-        put_d(t, a, F_RQP, 1, 1); put_d(t, a, F_RQOP, 3, fld_d(s, a, F_OP, 3));
-        put_d(t, a, F_RQOBJ, OBJB, fld_d(s, a, F_OBJ, OBJB));
-        put_d(t, a, F_RQST, 2, j == 0 ? ST_Pending : ST_Error);
-        put_d(t, a, F_PC, B_PC, L_DoReply);
-      } else if (p == L_DoListRequest) {                        // DoListRequest :499-511
-        put_d(t, a, F_LRP, 1, 1); put_d(t, a, F_LRK, 2, fld_d(s, a, F_KIND, 2)); set_objs_d(t, a, 0);
-        put_d(t, a, F_LRST, 2, j == 0 ? ST_Pending : ST_Error);
-        put_d(t, a, F_PC, B_PC, L_DoListReply);
-      } else if (p == L_DoReply) {                              // DoReply :485-495
-        if (j == 1) put_d(t, a, F_RQST, 2, ST_Error);
-        put_d(t, a, F_PC, B_PC, fld_d(s, a, F_SRET, 5)); put_d(t, a, F_OP, 3, fld_d(s, a, F_SOP, 3));
-        put_d(t, a, F_OBJ, OBJB, fld_d(s, a, F_SOBJ, OBJB));
-        pop(t, a);
-      } else {                                                  // DoListReply :513-524
-        if (j == 1) { set_objs_d(t, a, 0); put_d(t, a, F_LRST, 2, ST_Error); }
-        put_d(t, a, F_PC, B_PC, fld_d(s, a, F_SRET, 5)); put_d(t, a, F_KIND, 2, fld_d(s, a, F_SKIND, 2));
-        pop(t, a);
-      }
-    } else if (slot < 2 * A) {
-      const int a = slot - A;
-      const int p = pc_d(s, a);
-      switch (p) {
-        case L_CStart: {                                        // :528-549
-          const int sr = j == 0 ? 1 : fld_d(s, a, F_SR, 1);
-          put_d(t, a, F_SR, 1, sr);
-          if (sr) call(t, a, L_C1, OP_Force, oc_bare(ID_Secret));
-          else {
-            push_list(t, a, L_C3);
-            put_d(t, a, F_KIND, 2, K_Secret); put_d(t, a, F_PC, B_PC, L_DoListRequest);
-          }
-          return;
+    if (slot < 2 * A) {
+      const int a = slot < A ? slot : slot - A;
+      uint64_t w = aw_d(s, a);
+      const int p = g(w, F_PC, B_PC);
+      if (slot < A) {
+        if (p == L_DoRequest) {                                 // DoRequest :471-483
+          w = sw(w, F_RQP, 1, 1); w = sw(w, F_RQOP, 3, g(w, F_OP, 3));
+          w = sw(w, F_RQOBJ, OBJB, g(w, F_OBJ, OBJB));
+          w = sw(w, F_RQST, 2, j == 0 ? ST_Pending : ST_Error);
+          w = sw(w, F_PC, B_PC, L_DoReply);
+        } else if (p == L_DoListRequest) {                      // DoListRequest :499-511
+          w = sw(w, F_LRP, 1, 1); w = sw(w, F_LRK, 2, g(w, F_KIND, 2));
+          w = sw(w, F_LRST, 2, j == 0 ? ST_Pending : ST_Error);
+          w = sw(w, F_PC, B_PC, L_DoListReply);
+          set_objs_d(t, a, 0);
+        } else if (p == L_DoReply) {                            // DoReply :485-495
+          if (j == 1) w = sw(w, F_RQST, 2, ST_Error);
+          w = sw(w, F_PC, B_PC, g(w, F_SRET, 5)); w = sw(w, F_OP, 3, g(w, F_SOP, 3));
+          w = sw(w, F_OBJ, OBJB, g(w, F_SOBJ, OBJB));
+          w &= ~FRAME_MASK;
+        } else {                                                // DoListReply :513-524
+          if (j == 1) { w = sw(w, F_LRST, 2, ST_Error); set_objs_d(t, a, 0); }
+          w = sw(w, F_PC, B_PC, g(w, F_SRET, 5)); w = sw(w, F_KIND, 2, g(w, F_SKIND, 2));
+          w &= ~FRAME_MASK;
         }
-        case L_C1:                                              // :551-556
-          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); return;
-        case L_C10: call(t, a, L_C11, OP_Force, oc_bare(ID_PVC)); return;   // :558-568
-        case L_C11:                                             // :570-575
-          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); return;
-        case L_c12: call(t, a, L_C13, OP_Get, oc_bare(ID_PVC)); return;     // :577-587
-        case L_C13: {                                           // :589-594
-          bool go = fld_d(s, a, F_RQST, 2) != ST_Ok;
-          if (!go) {
-            const int oc = fld_d(s, a, F_RQOBJ, OBJB);
-            go = oc_id(oc) == ID_PVC && !(oc_is_full(oc) && u_spec(oc_u(oc)));
-          }
-          put_d(t, a, F_PC, B_PC, go ? L_CStart : L_C2); return;
-        }
-        case L_C2: put_d(t, a, F_SR, 1, 0); put_d(t, a, F_PC, B_PC, L_C5); return;  // :596-602
-        case L_C3:                                              // :604-609
-          put_d(t, a, F_PC, B_PC, fld_d(s, a, F_LRST, 2) != ST_Ok ? L_CStart : L_C8); return;
-        case L_C8: put_d(t, a, F_PC, B_PC, objs_d(s, a) == 0 ? L_C4 : L_C6); return; // :611-616
-        case L_C6: {                                            // :618-629
-          const int u = nth_bit(objs_d(s, a), j);
-          call(t, a, L_C7, OP_Delete, oc_bare(u_id(u)));
-          return;
-        }
-        case L_C7: {                                            // :631-636
-          const bool go = fld_d(s, a, F_RQST, 2) != ST_Ok || popc(objs_d(s, a)) > 1;
-          put_d(t, a, F_PC, B_PC, go ? L_CStart : L_C4); return;
-        }
-        case L_C4: case L_C5: put_d(t, a, F_PC, B_PC, p == L_C4 ? L_C5 : L_CStart); return;
-        case L_PVCStart:                                        // :655-663
-          push_list(t, a, L_PVCListedPVCs);
-          put_d(t, a, F_KIND, 2, K_PVC); put_d(t, a, F_PC, B_PC, L_DoListRequest); return;
-        case L_PVCListedPVCs: {                                 // :665-671
-          const bool go = fld_d(s, a, F_LRST, 2) != ST_Ok || unbound(objs_d(s, a)) == 0;
-          put_d(t, a, F_PC, B_PC, go ? L_PVCStart : L_PVCHavePVCs); return;
-        }
-        case L_PVCHavePVCs: {                                   // :673-688
-          const int u = nth_bit(unbound(objs_d(s, a)), j);
-          // bound == "spec" :> ("pvname" :> unb.n) @@ unb
-          call(t, a, L_PVCDone, OP_Update, oc_full(u_make(u_id(u), 1, u_vv(u))));
-          return;
-        }
-        default: /* L_PVCDone */ put_d(t, a, F_PC, B_PC, L_PVCStart); return;  // :690-693
-      }
-    } else {
-      // APIStart (:698-756): successor j serves the j-th pending request,
-      // then the pending list requests.
-      int k = j, c = 0;
-      for (; c < A; ++c) {                                      // the k-th pending request
-        if (!(fld_d(s, c, F_RQP, 1) && fld_d(s, c, F_RQST, 2) == ST_Pending)) continue;
-        if (k-- == 0) break;
-      }
-      if (c < A) {
-        const int oc = fld_d(s, c, F_RQOBJ, OBJB);
-        const int id = oc_id(oc);
-        const uint64_t api = s.w[0], same = api & id_mask(id);
-        int st = ST_Ok;
-        uint64_t nw = api;
-        switch (fld_d(s, c, F_RQOP, 3)) {
-          case OP_Create:                                       // :700-705
-            if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
+      } else {
+        switch (p) {
+          case L_CStart: {                                      // :528-549
+            const int sr = j == 0 ? 1 : g(w, F_SR, 1);
+            w = sw(w, F_SR, 1, sr);
+            if (sr) {
+              w = call_w(w, L_C1, OP_Force, oc_bare(ID_Secret));
+            } else {
+              w = push_list_w(w, L_C3);
+              w = sw(w, F_KIND, 2, K_Secret); w = sw(w, F_PC, B_PC, L_DoListRequest);
+            }
             break;
-          case OP_Force:                                        // :706-715
-            // variant 2 (seeded bug): add without replacing -> OnlyOneVersion fails
-            nw = (f.variant == 2 ? api : (api & ~same)) | (1ull << write_u(oc));
-            break;
-          case OP_Get:                                          // :716-728
-            if (same) {
-              put_d(t, c, F_RQOBJ, OBJB, oc_full(ctz(same)));     // CHOOSE o \in apiState
-              nw = read_map(api, same, c);
-            } else st = ST_Error;
-            break;
-          case OP_Delete: nw = api & ~same; break;              // :729-731
-          default: {                                            // Update :732-739
-            bool ok = false;
-            for (uint64_t x = same; x; x &= x - 1)
-              if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
-            if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
           }
+          case L_C1:                                            // :551-556
+            w = sw(w, F_PC, B_PC, g(w, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); break;
+          case L_C10: w = call_w(w, L_C11, OP_Force, oc_bare(ID_PVC)); break;   // :558-568
+          case L_C11:                                           // :570-575
+            w = sw(w, F_PC, B_PC, g(w, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); break;
+          case L_c12: w = call_w(w, L_C13, OP_Get, oc_bare(ID_PVC)); break;     // :577-587
+          case L_C13: {                                         // :589-594
+            bool go = g(w, F_RQST, 2) != ST_Ok;
+            if (!go) {
+              const int oc = g(w, F_RQOBJ, OBJB);
+              go = oc_id(oc) == ID_PVC && !(oc_is_full(oc) && u_spec(oc_u(oc)));
+            }
+            w = sw(w, F_PC, B_PC, go ? L_CStart : L_C2); break;
+          }
+          case L_C2: w = sw(w, F_SR, 1, 0); w = sw(w, F_PC, B_PC, L_C5); break;  // :596-602
+          case L_C3:                                            // :604-609
+            w = sw(w, F_PC, B_PC, g(w, F_LRST, 2) != ST_Ok ? L_CStart : L_C8); break;
+          case L_C8: w = sw(w, F_PC, B_PC, objs_d(s, a) == 0 ? L_C4 : L_C6); break;  // :611-616
+          case L_C6: {                                          // :618-629
+            const int u = nth_bit(objs_d(s, a), j);
+            w = call_w(w, L_C7, OP_Delete, oc_bare(u_id(u)));
+            break;
+          }
+          case L_C7: {                                          // :631-636
+            const bool go = g(w, F_RQST, 2) != ST_Ok || popc(objs_d(s, a)) > 1;
+            w = sw(w, F_PC, B_PC, go ? L_CStart : L_C4); break;
+          }
+          case L_C4: case L_C5: w = sw(w, F_PC, B_PC, p == L_C4 ? L_C5 : L_CStart); break;
+          case L_PVCStart:                                      // :655-663
+            w = push_list_w(w, L_PVCListedPVCs);
+            w = sw(w, F_KIND, 2, K_PVC); w = sw(w, F_PC, B_PC, L_DoListRequest); break;
+          case L_PVCListedPVCs: {                               // :665-671
+            const bool go = g(w, F_LRST, 2) != ST_Ok || unbound(objs_d(s, a)) == 0;
+            w = sw(w, F_PC, B_PC, go ? L_PVCStart : L_PVCHavePVCs); break;
+          }
+          case L_PVCHavePVCs: {                                 // :673-688
+            const int u = nth_bit(unbound(objs_d(s, a)), j);
+            // bound == "spec" :> ("pvname" :> unb.n) @@ unb
+            w = call_w(w, L_PVCDone, OP_Update, oc_full(u_make(u_id(u), 1, u_vv(u))));
+            break;
+          }
+          default: /* L_PVCDone */ w = sw(w, F_PC, B_PC, L_PVCStart); break;  // :690-693
         }
-        t.w[0] = nw;
-        put_d(t, c, F_RQST, 2, st);
-        return;
       }
-      for (c = 0; c < A; ++c) {                                 // :745-753
-        if (!(fld_d(s, c, F_LRP, 1) && fld_d(s, c, F_LRST, 2) == ST_Pending)) continue;
-        if (k-- == 0) break;
+      put_word_d(t, a, w);
+      return;
+    }
+    // APIStart (:698-756): successor j serves the j-th pending request (in
+    // actor order), then the pending list requests.
+    unsigned prq = 0, plr = 0;
+    static_for<A>([&](auto CI) {
+      constexpr int c = CI;
+      const uint64_t x = s.w[1 + c];
+      if (getf(x, F_RQP, 1) && getf(x, F_RQST, 2) == ST_Pending) prq |= 1u << c;
+      if (getf(x, F_LRP, 1) && getf(x, F_LRST, 2) == ST_Pending) plr |= 1u << c;
+    });
+    const int nrq = popc(prq);
+    const uint64_t api = s.w[0];
+    if (j < nrq) {
+      const int c = nth_bit(prq, j);
+      uint64_t w = aw_d(s, c);
+      const int oc = g(w, F_RQOBJ, OBJB);
+      const int id = oc_id(oc);
+      const uint64_t same = api & id_mask(id);
+      int st = ST_Ok;
+      uint64_t nw = api;
+      switch (g(w, F_RQOP, 3)) {
+        case OP_Create:                                         // :700-705
+          if (same) st = ST_Error; else nw = api | (1ull << write_u(oc));
+          break;
+        case OP_Force:                                          // :706-715
+          // variant 2 (seeded bug): add without replacing -> OnlyOneVersion fails
+          nw = (f.variant == 2 ? api : (api & ~same)) | (1ull << write_u(oc));
+          break;
+        case OP_Get:                                            // :716-728
+          if (same) {
+            w = sw(w, F_RQOBJ, OBJB, oc_full(ctz(same)));       // CHOOSE o \in apiState
+            nw = read_map(api, same, c);
+          } else st = ST_Error;
+          break;
+        case OP_Delete: nw = api & ~same; break;                // :729-731
+        default: {                                              // Update :732-739
+          bool ok = false;
+          for (uint64_t x = same; x; x &= x - 1)
+            if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
+          if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
+        }
       }
-      if (c < A) {
-        const uint64_t km = kind_mask(fld_d(s, c, F_LRK, 2)), api = s.w[0];
-        set_objs_d(t, c, api & km);
-        put_d(t, c, F_LRST, 2, ST_Ok);
-        t.w[0] = read_map(api, km, c);
-      }
+      t.w[0] = nw;
+      put_word_d(t, c, sw(w, F_RQST, 2, st));
+      return;
+    }
+    if (plr) {                                                  // :745-753
+      const int c = nth_bit(plr, j - nrq);
+      const uint64_t km = kind_mask(g(aw_d(s, c), F_LRK, 2));
+      set_objs_d(t, c, api & km);
+      put_word_d(t, c, sw(aw_d(s, c), F_LRST, 2, ST_Ok));
+      t.w[0] = read_map(api, km, c);
     }
   }
 
