@@ -58,20 +58,29 @@ def state_bytes(kw) -> int:
 def roofline_bfs(times, res, S):
     """Roofline of the dominant kernel from HIP-event times over the timed steps.
 
-    Algorithmic bytes per unit (DESIGN.md §5):
-      resolve: per parent S (state read) + 8 (new-mask/count write); per FPSet
-               probe 64 (one bucket line; the CAS lands in the same line)
-      expand : per parent S; per successor 16 (one batch-table entry)
-      emit   : per parent 8 (mask + offset); per new state S + 9 (frontier
-               write + parent pointer + ordinal)
+    Algorithmic bytes per unit (SURVEY.md §8(d); DESIGN.md §4):
+      claim  (k_claim)      : per parent S (frontier read); per GENERATED
+                              successor 64 (one 64-B probe line, SURVEY's FPSet
+                              op).  The kernel's LDS tile dedup lets about half
+                              of the successors skip their probe, so the
+                              achieved figure is an effective rate; `traffic`
+                              (PMC) is what the kernel actually moved.
+      settle (k_settle_rec) : per candidate 12 (record read) + 64 (probe line);
+                              per parent 8 (newmask + newcnt write)
+      emit   (k_emit)       : per parent 8 (mask + offset); per new state S + 9
+                              (frontier write + parent pointer + ordinal) + S
+                              (parent state re-read)
+      scan                  : per parent 8
     """
     parents = res["parents"]
     per_kernel = {
-        "resolve": parents * (S + 8) + res["probes"] * 64,
-        "expand": parents * S + res["succ"] * 16,
-        "emit": parents * 8 + res["new"] * (S + 9),
+        "expand": parents * S + res["succ"] * 64,
+        "resolve": res["settles"] * (12 + 64) + parents * 8,
+        "emit": parents * 8 + res["new"] * (2 * S + 9),
         "scan": parents * 8,
     }
+    kernel_names = {"expand": "k_claim", "resolve": "k_settle_rec", "emit": "k_emit",
+                    "scan": "rocprim scan"}
     name = max(times, key=lambda k: times[k][0])
     ms, launches = times[name]
     byts = per_kernel[name]
@@ -79,7 +88,7 @@ def roofline_bfs(times, res, S):
     return name, {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-        "kernel": f"k_{name}", "launches": launches,
+        "kernel": kernel_names[name], "launches": launches,
         "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2),
         "bytes_per_launch": int(byts / max(launches, 1)),
     }
@@ -127,7 +136,7 @@ def bench_single(args, kw, desc):
         mc.run()
     torch.cuda.synchronize()
     times = {"expand": [0.0, 0], "resolve": [0.0, 0], "scan": [0.0, 0], "emit": [0.0, 0]}
-    acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0}
+    acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0, "settles": 0}
     t0 = time.perf_counter()
     results = []
     for _ in range(args.steps):
@@ -139,6 +148,7 @@ def bench_single(args, kw, desc):
             times[k][1] += kt[k][1]
         acc["parents"] += r.distinct - r.queue_left
         acc["probes"] += r.fpset_probes
+        acc["settles"] += r.batch_inserts
         acc["succ"] += r.generated - r.init
         acc["new"] += r.distinct - r.init
     torch.cuda.synchronize()
@@ -158,7 +168,8 @@ def bench_single(args, kw, desc):
                    "constants": "REQUESTS_CAN_FAIL=TRUE,REQUESTS_CAN_TIMEOUT=TRUE",
                    "invariants": "TypeOK,OnlyOneVersion", "distinct": r.distinct,
                    "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU",
-                   "fpset_probes": r.fpset_probes, "chunks": r.levels_chunks},
+                   "claimset_probes": r.fpset_probes, "settle_reads": r.batch_inserts,
+                   "chunks": r.levels_chunks},
     }
     if not args.no_timing:
         name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, state_bytes(kw))
