@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the sharded (multi-GPU) stages even at N=1 (run under torch.distributed.run)")
     return ap.parse_args()
 
 
@@ -227,7 +229,7 @@ def main():
         out = bench_fpset(args)
     else:
         kw, desc = WORKLOADS[args.workload]
-        if args.gpus > 1:
+        if args.gpus > 1 or args.sharded:
             from kubecheck import distributed
 
             out = distributed.bench_sharded(args, kw, desc)

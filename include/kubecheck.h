@@ -188,7 +188,9 @@ uint64_t kc_shard_record_bytes(kc_shard *s);
 /* Write sum(counts) records, grouped by owner rank, into device memory. */
 int kc_shard_pack(kc_shard *s, void *send_dev);
 /* Dedup + insert `n_records` received records (device memory, sorted by
- * source rank); *n_new = states added to this rank's next frontier. */
+ * source rank); *n_new = states added to this rank's next frontier.  The
+ * library reads recv_dev on its own HIP stream: the caller must have
+ * completed every write to it (e.g. synchronised its all-to-all stream). */
 int kc_shard_insert(kc_shard *s, const void *recv_dev, uint64_t n_records, uint64_t *n_new,
                     uint64_t *err_key_out);
 /* The new states become the frontier (after the caller's agreement step). */

@@ -67,13 +67,13 @@ class CpuShard:
     def pack(self, send):
         rows = [r for p in self.per_owner for r in p]
         if rows:
-            arr = np.ascontiguousarray(np.stack(rows).astype(np.uint64)).view(np.uint8).reshape(-1)
-            send[: arr.size].copy_(torch.from_numpy(arr))
+            arr = np.ascontiguousarray(np.stack(rows).astype(np.uint64)).view(np.int64).reshape(-1)
+            send[: arr.size].copy_(torch.from_numpy(arr))      # int64 word buffer
 
     def insert(self, recv, n):
         err, batch, nxt, keys = NONE_KEY, set(), [], []
         if n:
-            recs = recv[: n * self.record_bytes].numpy().copy().view(np.uint64).reshape(n, self.W + 2)
+            recs = recv[: n * (self.W + 2)].numpy().copy().view(np.uint64).reshape(n, self.W + 2)
             for r in recs:
                 fp, key = int(r[self.W]), int(r[self.W + 1])
                 if fp in batch:

@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kw, outdir):
+def _worker(rank, world, port, kw, outdir, round_bytes=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tla-kubernetes_amd"))
@@ -32,13 +32,17 @@ def _worker(rank, world, port, kw, outdir):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = ModelConfig(**kw)
-    res = ShardedModelChecker(cfg, CpuShard(cfg, rank, world)).run()
+    mc = ShardedModelChecker(cfg, CpuShard(cfg, rank, world))
+    if round_bytes:
+        mc.A2A_ROUND_BYTES = round_bytes     # force the multi-round exchange
+    res = mc.run()
     json.dump(res, open(os.path.join(outdir, f"r{rank}.json"), "w"))
     dist.destroy_process_group()
 
 
-def run_sharded(tmp_path, world, **kw):
-    mp.spawn(_worker, args=(world, _free_port(), kw, str(tmp_path)), nprocs=world, join=True)
+def run_sharded(tmp_path, world, round_bytes=None, **kw):
+    mp.spawn(_worker, args=(world, _free_port(), kw, str(tmp_path), round_bytes), nprocs=world,
+             join=True)
     outs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     for o in outs:
         o.pop("seconds")
@@ -47,10 +51,12 @@ def run_sharded(tmp_path, world, **kw):
     return outs[0]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_counts_match_single(tmp_path, fixtures, world):
+@pytest.mark.parametrize("world,round_bytes", [(2, None), (3, None), (3, 4096)])
+def test_sharded_counts_match_single(tmp_path, fixtures, world, round_bytes):
+    # round_bytes=4096: the record exchange runs in many small all-to-all
+    # rounds (the path large levels take; kubecheck.distributed._exchange)
     fx = fixtures["model1_fail0_timeout0"]
-    r = run_sharded(tmp_path, world, can_fail=False, can_timeout=False)
+    r = run_sharded(tmp_path, world, round_bytes=round_bytes, can_fail=False, can_timeout=False)
     assert r["level_width"] == fx["level_width"]
     assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r["act_gen"] == fx["act_gen"]

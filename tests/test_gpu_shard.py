@@ -27,7 +27,7 @@ def emulate(R, **kw):
         for s in shards:
             c, e = s.expand()
             err = min(err, e)
-            buf = torch.empty(max(sum(c), 1) * rb, dtype=torch.uint8, device="cuda")
+            buf = torch.empty(max(sum(c), 1) * rb // 8, dtype=torch.int64, device="cuda")
             s.pack(buf)
             sends.append(buf)
             counts.append(c)
@@ -35,10 +35,10 @@ def emulate(R, **kw):
         for r, s in enumerate(shards):
             parts, m = [], 0
             for src in range(R):
-                off = sum(counts[src][:r]) * rb
-                parts.append(sends[src][off: off + counts[src][r] * rb])
+                off = sum(counts[src][:r]) * rb // 8
+                parts.append(sends[src][off: off + counts[src][r] * rb // 8])
                 m += counts[src][r]
-            recv = torch.cat(parts) if m else torch.empty(rb, dtype=torch.uint8, device="cuda")
+            recv = torch.cat(parts) if m else torch.empty(rb // 8, dtype=torch.int64, device="cuda")
             torch.cuda.synchronize()
             nn, e = s.insert(recv, m)
             err = min(err, e)
@@ -92,17 +92,19 @@ def emulate_levels(R, L, **kw):
         sends, counts = [], []
         for s in shards:
             c, _ = s.expand()
-            buf = torch.empty(max(sum(c), 1) * rb, dtype=torch.uint8, device="cuda")
+            buf = torch.empty(max(sum(c), 1) * rb // 8, dtype=torch.int64, device="cuda")
             s.pack(buf)
             sends.append(buf)
             counts.append(c)
         total = 0
         for r, s in enumerate(shards):
-            parts = [sends[src][sum(counts[src][:r]) * rb: (sum(counts[src][:r]) + counts[src][r]) * rb]
+            rw = rb // 8
+            parts = [sends[src][sum(counts[src][:r]) * rw: (sum(counts[src][:r]) + counts[src][r]) * rw]
                      for src in range(R)]
             m = sum(counts[src][r] for src in range(R))
-            torch.cuda.synchronize()
-            total += s.insert(torch.cat(parts), m)[0]
+            recv = torch.cat(parts)
+            torch.cuda.synchronize()          # the shard reads recv on its own stream
+            total += s.insert(recv, m)[0]
         for s in shards:
             s.advance()
         widths.append(total)

@@ -103,7 +103,7 @@ __device__ __forceinline__ int fpset_contains(const unsigned long long* __restri
 // ---------------------------------------------------------------- ClaimSet
 // The BFS engine's seen-set: the FPSet fused with the per-level "first
 // occurrence" table.  Open addressing with linear probing over 16-B slots
-// {fp, ~claim}, where claim = level << 40 | key and key = (parent index in
+// {fp, ~claim}, where claim = level << 44 | key and key = (parent index in
 // level) << 8 | (successor position).  A probe is ONE 16-B load (measured on
 // MI355X: one 16-B load per lane reaches ~48 G random probes/s at 16-64 GB
 // tables, a lane reading a whole 64-B bucket with four loads ~20 G/s;
@@ -115,9 +115,9 @@ __device__ __forceinline__ int fpset_contains(const unsigned long long* __restri
 // ~claim = 0 (never written) reads as "claim pending, current level".
 struct ClaimEntry {
   unsigned long long fp;
-  unsigned long long nclaim;  // ~(level << 40 | key); 0 = not yet set
+  unsigned long long nclaim;  // ~(level << 44 | key); 0 = not yet set
 };
-constexpr int CLAIM_KEY_BITS = 40;
+constexpr int CLAIM_KEY_BITS = 44;   // key: [rank 4 |] parent index 32 | position 8
 enum ClaimResult : int { CL_OLD = 0, CL_LOST = 1, CL_CUR = 2, CL_NEW = 3, CL_FULL = 4 };
 
 __host__ __device__ __forceinline__ uint64_t make_claim(uint32_t level, uint64_t key) {

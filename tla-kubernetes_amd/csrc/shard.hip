@@ -4,18 +4,22 @@
 //
 // owner(fp) = floor(fp * R / 2^63) (fps are uniform in [1, 2^63)), the top
 // bits of the fingerprint as in TLC's MultiFPSet [ext-TLC].  Per level:
-//   expand : k_expand (local dedup by min order key, generated counters,
-//            Assert/deadlock keys) + k_shard_count (representatives per
-//            owner, per parent) + one exclusive scan per owner
+//   expand : k_shard_count — LDS tile dedup of each 256-parent tile's
+//            successors (as k_claim), per-parent mask of the tile
+//            representatives and their count per owner; generated counters,
+//            Assert/deadlock keys — then one exclusive scan per owner
 //   pack   : k_shard_pack writes records {state, fp, key} into the caller's
 //            send buffer, grouped by owner, each group in (parent, t) order
 //   (all-to-all by the caller)
-//   insert : received records -> batch table (min key) -> FPSet shard ->
-//            new states compacted in key order into the next frontier, with
-//            parent keys (TLC trace file), invariant checks, counters
+//   insert : received records claim their fp in this rank's ClaimSet shard
+//            (k_shard_claim), candidates re-read their claim (k_shard_settle),
+//            and the winners are compacted in record order (= key order) into
+//            the next frontier with parent keys (TLC trace file), invariant
+//            checks and counters (k_shard_emit)
 // Keys: rank << 60 | parent index << 16 | successor position << 8 | low byte
-// (action id in records, ErrKind in error keys), so the same minimum is
-// taken everywhere and the result does not depend on arrival order.
+// (action id in records, ErrKind in error keys); the ClaimSet claim orders
+// them by (rank, parent, position), so the same minimum is taken everywhere
+// and the result does not depend on arrival order.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -45,43 +49,67 @@ struct Record {
 };
 
 template <class M>
-__global__ void __launch_bounds__(256)
-k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f,
-              const BatchEntry* __restrict__ bt, uint64_t bmask, uint32_t world,
-              uint32_t* __restrict__ cnt /* [world][n] */, uint32_t* __restrict__ repmask,
-              Counters* __restrict__ C) {
+__global__ void __launch_bounds__(CLAIM_TILE)
+k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, int check_deadlock,
+              uint32_t world, uint32_t* __restrict__ cnt /* [world][n] */,
+              uint32_t* __restrict__ repmask, Counters* __restrict__ C) {
+  __shared__ unsigned long long sh_fp[CLAIM_LDS];
+  __shared__ unsigned int sh_key[CLAIM_LDS];
+  __shared__ unsigned int sh_rep[CLAIM_TILE];
+  __shared__ unsigned int sh_cnt[16 * CLAIM_TILE];   // [owner][parent in tile]
   __shared__ unsigned int sh_act[A_COUNT];
+  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+    sh_fp[k] = 0ull;
+    sh_key[k] = ~0u;
+  }
+  for (int k = threadIdx.x; k < 16 * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
+  sh_rep[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * CLAIM_TILE + threadIdx.x;
   if (i < n) {
     const typename M::State s = load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
-    const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
+    if (pl.fail_pos >= 0)
+      atomicMin(&C->err_key, (i << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
+    else if (pl.total == 0 && check_deadlock)
+      atomicMin(&C->err_key, (i << 16) | E_DEADLOCK);
 #pragma unroll
     for (int slot = 0; slot < M::NSLOT; ++slot) {       // per-action "generated"
       const int c = (int)((pl.counts >> (6 * slot)) & 63);
       if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
     }
-    uint32_t c[16] = {};
-    uint32_t mask = 0;
+    int tot = pl.total;
+    if (tot > M::MAXSUCC) {
+      atomicAdd(&C->overflow, 1ull);
+      tot = M::MAXSUCC;
+    }
     for (int t = 0; t < tot; ++t) {
       int slot, j;
       M::locate(pl, t, slot, j);
       typename M::State x;
       M::apply(s, slot, j, f, x);
       const uint64_t fp = M::fingerprint(x);
-      if (batch_is_rep(bt, bmask, fp, (i << 8) | (uint64_t)t)) {
-        mask |= 1u << t;
-        const uint32_t o = owner_of(fp, world);
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) c[k] += (k == o);
+      if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0) {
+        // LDS table full: this copy is sent as its own representative
+        atomicOr(&sh_rep[threadIdx.x], 1u << t);
+        atomicAdd(&sh_cnt[owner_of(fp, world) * CLAIM_TILE + threadIdx.x], 1u);
       }
     }
-    repmask[i] = mask;
-    for (uint32_t k = 0; k < world; ++k) cnt[(uint64_t)k * n + i] = c[k];
   }
   __syncthreads();
+  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+    const unsigned long long fp = sh_fp[k];
+    if (!fp) continue;
+    const unsigned int lk = sh_key[k];
+    atomicOr(&sh_rep[lk >> 5], 1u << (lk & 31));
+    atomicAdd(&sh_cnt[owner_of(fp, world) * CLAIM_TILE + (lk >> 5)], 1u);
+  }
+  __syncthreads();
+  if (i < n) {
+    repmask[i] = sh_rep[threadIdx.x];
+    for (uint32_t o = 0; o < world; ++o) cnt[(uint64_t)o * n + i] = sh_cnt[o * CLAIM_TILE + threadIdx.x];
+  }
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
@@ -120,29 +148,34 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
   }
 }
 
-template <class M>
-__global__ void __launch_bounds__(256)
-k_shard_claim(const Record<M>* __restrict__ in, uint64_t n, BatchEntry* __restrict__ bt,
-              uint64_t bmask, Counters* __restrict__ C) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && !batch_insert_bounded(bt, bmask, in[i].fp, in[i].key)) atomicAdd(&C->overflow, 1ull);
+// claim order key of a record: (rank, parent index, successor position)
+__device__ __forceinline__ uint64_t record_ckey(uint64_t key) {
+  return ((key >> 60) << 40) | (((key >> 16) & 0xffffffffull) << 8) | ((key >> 8) & 0xff);
 }
 
 template <class M>
 __global__ void __launch_bounds__(256)
-k_shard_resolve(const Record<M>* __restrict__ in, uint64_t n, const BatchEntry* __restrict__ bt,
-                uint64_t bmask, unsigned long long* __restrict__ slots, uint64_t nbuckets,
-                uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+k_shard_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
+              uint64_t nslots, uint32_t level, uint32_t* __restrict__ cand,
+              Counters* __restrict__ C) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t nw = 0;
-  const uint64_t fp = in[i].fp;
-  if (batch_is_rep(bt, bmask, fp, in[i].key)) {
-    const int r = fpset_insert(slots, nbuckets, fp);
-    if (r == 1) nw = 1;
-    else if (r < 0) atomicAdd(&C->overflow, 1ull);
-  }
-  isnew[i] = nw;
+  const int r = claimset_claim(cs, nslots, in[i].fp, make_claim(level, record_ckey(in[i].key)), level);
+  if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
+  cand[i] = (r == CL_NEW || r == CL_CUR) ? 1u : 0u;
+}
+
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_settle(const Record<M>* __restrict__ in, uint64_t n, const ClaimEntry* __restrict__ cs,
+               uint64_t nslots, uint32_t level, const uint32_t* __restrict__ cand,
+               uint32_t* __restrict__ isnew) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w = 0;
+  if (cand[i])
+    w = ~claimset_get(cs, nslots, in[i].fp) == make_claim(level, record_ckey(in[i].key)) ? 1u : 0u;
+  isnew[i] = w;
 }
 
 template <class M>
@@ -223,17 +256,17 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
+    KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
     return 0;
   }
 
   int init(uint64_t* n_local) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
-    if (fps_.slots && fps_.capacity() >= fp_slots) {
-      KC_HIP_TRY(hipMemsetAsync(fps_.slots, 0, fps_.nbuckets * 64, st_));
-      fps_.count = 0;
+    if (cs_.t && cs_.capacity() >= fp_slots) {
+      KC_TRY(cs_.clear(st_));
     } else {
-      KC_TRY(fps_.init(fp_slots, st_));
+      KC_TRY(cs_.init(fp_slots, st_));
     }
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
     cand_total_ = 0;
@@ -266,12 +299,12 @@ class ShardT final : public ShardBase {
       uint64_t* d_fps = nullptr;
       KC_HIP_TRY(hipMalloc(&d_fps, n_ * 8));
       KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), n_ * 8, hipMemcpyHostToDevice, st_));
-      launch_fpset_insert_list(d_fps, n_, fps_, nullptr, st_);
+      launch_claimset_insert_list(d_fps, n_, cs_, 1u, nullptr, st_);
       KC_HIP_TRY(hipStreamSynchronize(st_));
       (void)hipFree(d_fps);
     }
     KC_HIP_TRY(hipStreamSynchronize(st_));
-    fps_.count = n_;
+    cs_.count = n_;
     *n_local = n_;
     return 0;
   }
@@ -285,17 +318,16 @@ class ShardT final : public ShardBase {
     *err_key = init_err_;
     init_err_ = ~0ull;
     if (n_ == 0) return 0;
-    const uint64_t bcap = next_pow2(2 * cand_ + 256);
-    KC_TRY(bt_.ensure(bcap, st_));
-    KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
-    const unsigned grid = (unsigned)((n_ + 255) / 256);
-    hipLaunchKernelGGL(k_expand<M>, dim3(grid), dim3(256), 0, st_, cur_, n_, 0ull, flags_,
-                       cfg_.check_deadlock, bt_.t, bcap - 1, d_ctr_);
+    if (n_ >= (1ull << 32)) {
+      set_error("kc_shard_expand: frontier wider than 2^32 states");
+      return -ENOMEM;
+    }
+    const unsigned grid = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
-    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(256), 0, st_, cur_, n_, flags_, bt_.t,
-                       bcap - 1, (uint32_t)world_, cnt_, repmask_, d_ctr_);
+    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(CLAIM_TILE), 0, st_, cur_, n_, flags_,
+                       cfg_.check_deadlock, (uint32_t)world_, cnt_, repmask_, d_ctr_);
     size_t tmp_bytes = 0;
     KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)n_, st_));
     KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
@@ -315,13 +347,14 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_expand: successor overflow / batch table full");
       return -ENOMEM;
     }
-    uint64_t base[16] = {};
+    uint64_t* base = h_owner_base_;      // pinned: the copy is asynchronous
+    for (int o = 0; o < 16; ++o) base[o] = 0;
     for (int o = 0; o < world_; ++o) {
       counts[o] = (uint64_t)lo[o] + lc[o];
       base[o] = send_total_;
       send_total_ += counts[o];
     }
-    KC_HIP_TRY(hipMemcpyAsync(d_owner_base_, base, sizeof base, hipMemcpyHostToDevice, st_));
+    KC_HIP_TRY(hipMemcpyAsync(d_owner_base_, base, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, st_));
     if (h_ctr_->err_key != ~0ull)
       *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_ctr_->err_key);
     return 0;
@@ -348,19 +381,19 @@ class ShardT final : public ShardBase {
     *err_key = ~0ull;
     next_n_ = 0;
     if (n) {
-      const uint64_t bcap = next_pow2(2 * n + 256);
-      KC_TRY(bt_.ensure(bcap, st_));
-      KC_HIP_TRY(hipMemsetAsync(bt_.t, 0, bcap * sizeof(BatchEntry), st_));
-      KC_TRY(fps_.reserve(n, st_));
+      KC_TRY(cs_.reserve(n, st_));
+      KC_TRY(grow_buffer(cand_buf_, cand_cap_, n, false, st_));
       KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
       KC_TRY(grow_buffer(ioff_, ioff_cap_, n, false, st_));
       KC_TRY(grow_buffer(next_, next_cap_, n, false, st_));
       const uint64_t next_gidx = level_base_.back() + n_;
       KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + n, true, st_));
       const unsigned grid = (unsigned)((n + 255) / 256);
-      hipLaunchKernelGGL(k_shard_claim<M>, dim3(grid), dim3(256), 0, st_, in, n, bt_.t, bcap - 1, d_ctr_);
-      hipLaunchKernelGGL(k_shard_resolve<M>, dim3(grid), dim3(256), 0, st_, in, n, bt_.t, bcap - 1,
-                         fps_.slots, fps_.nbuckets, isnew_, d_ctr_);
+      const uint32_t succ_level = (uint32_t)level_ + 1;
+      hipLaunchKernelGGL(k_shard_claim<M>, dim3(grid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
+                         succ_level, cand_buf_, d_ctr_);
+      hipLaunchKernelGGL(k_shard_settle<M>, dim3(grid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
+                         succ_level, cand_buf_, isnew_);
       size_t tmp_bytes = 0;
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
       KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
@@ -378,7 +411,17 @@ class ShardT final : public ShardBase {
         return -ENOMEM;
       }
       next_n_ = (uint64_t)lo + lc;
-      fps_.count += next_n_;
+      if (getenv("KC_SHARD_DEBUG")) {
+        std::vector<uint32_t> hc(n);
+        KC_HIP_TRY(hipMemcpy(hc.data(), cand_buf_, n * 4, hipMemcpyDeviceToHost));
+        uint64_t nc = 0;
+        for (auto v : hc) nc += v;
+        fprintf(stderr, "shard r%d level %d: records %llu candidates %llu new %llu slots %llu count %llu\n",
+                rank_, level_, (unsigned long long)n, (unsigned long long)nc,
+                (unsigned long long)next_n_, (unsigned long long)cs_.nslots,
+                (unsigned long long)cs_.count);
+      }
+      cs_.count += next_n_;
       next_cand_ = h_ctr_->next_cand() - cand_total_;
       cand_total_ += next_cand_;
       if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
@@ -430,8 +473,8 @@ class ShardT final : public ShardBase {
     }
     r->init = gen_init_;
     r->generated = gen;                 // successors generated by this rank's parents
-    r->distinct = fps_.count;
-    r->fpset_slots = fps_.capacity();
+    r->distinct = cs_.count;
+    r->fpset_slots = cs_.capacity();
     r->fpset_probes = h_ctr_->probes();
     r->nlevels = level_;
     return 0;
@@ -440,13 +483,13 @@ class ShardT final : public ShardBase {
  private:
   void release() {
     (void)hipSetDevice(cfg_.device);
-    fps_.release();
-    bt_.release();
+    cs_.release();
     for (void* p : {(void*)cur_, (void*)next_, (void*)pkeys_, (void*)cnt_, (void*)off_,
-                    (void*)repmask_, (void*)isnew_, (void*)ioff_, (void*)scan_tmp_, (void*)d_ctr_,
+                    (void*)repmask_, (void*)cand_buf_, (void*)isnew_, (void*)ioff_, (void*)scan_tmp_, (void*)d_ctr_,
                     (void*)d_owner_base_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (h_owner_base_) (void)hipHostFree(h_owner_base_);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
@@ -454,17 +497,19 @@ class ShardT final : public ShardBase {
   int rank_, world_;
   Flags flags_{};
   hipStream_t st_ = nullptr;
-  DevFpset fps_;
-  DevBatchTable bt_;
+  DevClaimSet cs_;
   State *cur_ = nullptr, *next_ = nullptr;
   uint64_t cur_cap_ = 0, next_cap_ = 0;
   unsigned long long* pkeys_ = nullptr;
   uint64_t pk_cap_ = 0;
   uint32_t *cnt_ = nullptr, *off_ = nullptr, *repmask_ = nullptr, *isnew_ = nullptr, *ioff_ = nullptr;
+  uint32_t* cand_buf_ = nullptr;
+  uint64_t cand_cap_ = 0;
   uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
   uint64_t* d_owner_base_ = nullptr;
+  uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
   uint64_t n_ = 0, next_n_ = 0, cand_ = 0, next_cand_ = 0, send_total_ = 0, gen_init_ = 0;
   uint64_t cand_total_ = 0;   // cumulative next_cand counter already consumed

@@ -109,8 +109,11 @@ class ShardedModelChecker:
         self.world = dist.get_world_size(group)
         self.dev = torch.device(backend.device_type, torch.cuda.current_device()) \
             if backend.device_type == "cuda" else torch.device("cpu")
-        self._send = torch.empty(0, dtype=torch.uint8, device=self.dev)
-        self._recv = torch.empty(0, dtype=torch.uint8, device=self.dev)
+        # exchange buffers in 8-byte words (records are whole words): element
+        # counts stay 8x below byte counts (a uint8 all-to-all of > 1 GiB
+        # came back corrupted through RCCL)
+        self._send = torch.empty(0, dtype=torch.int64, device=self.dev)
+        self._recv = torch.empty(0, dtype=torch.int64, device=self.dev)
         self.spec = Spec(cfg)
 
     # -- collectives -----------------------------------------------------
@@ -122,12 +125,57 @@ class ShardedModelChecker:
         self.dist.all_reduce(t, op=op, group=self.group)
         return [int(x) for x in t.tolist()]
 
-    def _buffer(self, name: str, nbytes: int):
+    def _buffer(self, name: str, nwords: int):
         buf = getattr(self, name)
-        if buf.numel() < nbytes:
-            buf = self.torch.empty(max(nbytes, 2 * buf.numel()), dtype=self.torch.uint8, device=self.dev)
+        if buf.numel() < nwords:
+            buf = self.torch.empty(max(nwords, 2 * buf.numel()), dtype=self.torch.int64, device=self.dev)
             setattr(self, name, buf)
         return buf
+
+    # RCCL through torch returned only the first half of an all_to_all_single
+    # larger than 1 GiB (MI355X, ROCm 7.2, torch 2.10): records move in
+    # rounds of at most this many bytes per collective.
+    A2A_ROUND_BYTES = 256 << 20
+
+    def _exchange(self, send, counts: List[int], rw: int):
+        """All-to-all of the owner-grouped records; returns (recv, n_records),
+        recv grouped by source rank (in rank order)."""
+        torch, dist, R = self.torch, self.dist, self.world
+        if R == 1:
+            return send, counts[0]
+        # the full counts matrix M[src][dst] on every rank (one all-gather),
+        # so every rank derives the same round schedule
+        cin = self._i64(counts)
+        mat = torch.empty(R * R, dtype=torch.int64, device=self.dev)
+        dist.all_gather_into_tensor(mat, cin, group=self.group)
+        M = [[int(x) for x in row] for row in mat.view(R, R).tolist()]
+        rcounts = [M[src][self.rank] for src in range(R)]
+        recv = self._buffer("_recv", max(sum(rcounts), 1) * rw)
+        q = max(1, self.A2A_ROUND_BYTES // (8 * rw * R))      # records per pair per round
+        rounds = max(1, -(-max(max(r) for r in M) // q))
+        if rounds == 1:
+            dist.all_to_all_single(recv[: sum(rcounts) * rw], send[: sum(counts) * rw],
+                                   output_split_sizes=[c * rw for c in rcounts],
+                                   input_split_sizes=[c * rw for c in counts], group=self.group)
+            return recv, sum(rcounts)
+        sbase = [sum(counts[:d]) for d in range(R)]
+        rbase = [sum(rcounts[:s]) for s in range(R)]
+        for k in range(rounds):
+            lo = k * q
+            ins = [min(q, max(0, counts[d] - lo)) for d in range(R)]
+            outs = [min(q, max(0, rcounts[s] - lo)) for s in range(R)]
+            tin = torch.cat([send[(sbase[d] + lo) * rw: (sbase[d] + lo + ins[d]) * rw] for d in range(R)])
+            tout = torch.empty(max(sum(outs), 1) * rw, dtype=torch.int64, device=self.dev)
+            dist.all_to_all_single(tout[: sum(outs) * rw], tin,
+                                   output_split_sizes=[c * rw for c in outs],
+                                   input_split_sizes=[c * rw for c in ins], group=self.group)
+            o = 0
+            for s_ in range(R):
+                if outs[s_]:
+                    recv[(rbase[s_] + lo) * rw: (rbase[s_] + lo + outs[s_]) * rw].copy_(
+                        tout[o * rw: (o + outs[s_]) * rw])
+                o += outs[s_]
+        return recv, sum(rcounts)
 
     def _sync(self):
         if self.dev.type == "cuda":
@@ -145,19 +193,12 @@ class ShardedModelChecker:
             if self.cfg.max_levels and level >= self.cfg.max_levels:
                 break
             counts, e1 = be.expand()
-            send = self._buffer("_send", max(sum(counts), 1) * rb)
+            rw = rb // 8                                  # record words
+            send = self._buffer("_send", max(sum(counts), 1) * rw)
             be.pack(send)
-            # exchange: counts first, then the records (one all-to-all each)
-            cin = self._i64(counts)
-            cout = self.torch.empty_like(cin)
-            dist.all_to_all_single(cout, cin, group=self.group)
-            rcounts = [int(x) for x in cout.tolist()]
-            recv = self._buffer("_recv", max(sum(rcounts), 1) * rb)
-            dist.all_to_all_single(recv[: sum(rcounts) * rb], send[: sum(counts) * rb],
-                                   output_split_sizes=[c * rb for c in rcounts],
-                                   input_split_sizes=[c * rb for c in counts], group=self.group)
+            recv, nrecv = self._exchange(send, counts, rw)
             self._sync()
-            n_new, e2 = be.insert(recv, sum(rcounts))
+            n_new, e2 = be.insert(recv, nrecv)
             e = min(e1, e2)
             [err] = self._allreduce([e if e < NONE_KEY else NONE_KEY], dist.ReduceOp.MIN)
             [total_new] = self._allreduce([n_new], dist.ReduceOp.SUM)
@@ -244,6 +285,8 @@ def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
     res = None
     for _ in range(args.steps):
         res = mc.run()
+        if not res["complete"] or res["error"]:
+            raise RuntimeError(f"sharded check incomplete: error={res['error']} depth={res['depth']}")
     torch.cuda.synchronize()
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")

@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Diagnostic: the sharded driver (kubecheck.distributed) on this process's
+GPU at world size 1 (RCCL), printing the result summary.
+
+  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 tools/exp_sharded.py [--np 2]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tla-kubernetes_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+from kubecheck import ModelConfig  # noqa: E402
+from kubecheck.distributed import HipShard, ShardedModelChecker  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--np", type=int, default=2)
+ap.add_argument("--nc", type=int, default=1)
+a = ap.parse_args()
+local = int(os.environ.get("LOCAL_RANK", "0"))
+torch.cuda.set_device(local)
+dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+cfg = ModelConfig(nc=a.nc, np=a.np, device=local, fpset_slots=1 << 20)
+r = ShardedModelChecker(cfg, HipShard(cfg, dist.get_rank(), dist.get_world_size())).run()
+if dist.get_rank() == 0:
+    print({k: r[k] for k in ("distinct", "generated", "depth", "error", "complete", "seconds")},
+          r.get("error_action"), r.get("error_invariant"), r.get("error_level"), r["level_width"][-5:], flush=True)
+dist.destroy_process_group()
