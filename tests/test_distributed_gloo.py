@@ -64,6 +64,13 @@ def test_sharded_counts_match_single(tmp_path, fixtures, world, round_bytes):
     assert r["complete"] and r["error"] is None
 
 
+def test_sharded_max_levels(tmp_path, fixtures):
+    fx = fixtures["model1_fail0_timeout0"]
+    r = run_sharded(tmp_path, 2, max_levels=20, can_fail=False, can_timeout=False)
+    assert r["level_width"] == fx["level_width"][:20] and r["depth"] == 20
+    assert not r["complete"] and r["error"] is None
+
+
 def test_sharded_assertion_trace(tmp_path, fixtures, oracle):
     fx = fixtures["nc2"]
     r = run_sharded(tmp_path, 2, nc=2)

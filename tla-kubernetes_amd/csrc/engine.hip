@@ -37,11 +37,19 @@ const char* kActionNames[A_COUNT] = {
 
 }  // namespace
 
-// chunk_base += (last exclusive offset + last count)
-__global__ void k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ cnt,
-                          uint64_t n, Counters* __restrict__ C) {
-  if (threadIdx.x == 0 && blockIdx.x == 0 && n > 0)
-    C->chunk_base += (unsigned long long)offsets[n - 1] + cnt[n - 1];
+// chunk_base += (last exclusive offset + last count); cand_total = sum of the
+// next_cand stripes (one 64-lane wave, one stripe per lane)
+__global__ void __launch_bounds__(64)
+k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ cnt, uint64_t n,
+          Counters* __restrict__ C) {
+  static_assert(CTR_STRIPES == 64, "one lane per stripe");
+  unsigned long long v = C->s[threadIdx.x].next_cand;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if (threadIdx.x == 0) {
+    C->cand_total = v;
+    if (n > 0) C->chunk_base += (unsigned long long)offsets[n - 1] + cnt[n - 1];
+  }
 }
 
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
@@ -240,7 +248,7 @@ class EngineT final : public EngineBase {
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newcnt_, cn, d_ctr_);
       }
       KC_HIP_TRY(hipGetLastError());
-      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
@@ -248,9 +256,6 @@ class EngineT final : public EngineBase {
         set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
         return -ENOMEM;
       }
-      uint64_t gen = 0;
-      for (int a = 0; a < A_COUNT; ++a) gen += c.act_gen(a);
-      res->generated = ni + gen;
       const uint64_t n_new = c.chunk_base;
       cs_.count += n_new;
       res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
@@ -262,9 +267,9 @@ class EngineT final : public EngineBase {
       }
       res->distinct += n_new;
       if (cfg_.verbose)
-        fprintf(stderr, "kubecheck: level %d width %llu -> %llu new, %llu distinct, %llu generated\n",
+        fprintf(stderr, "kubecheck: level %d width %llu -> %llu new, %llu distinct\n",
                 level, (unsigned long long)n, (unsigned long long)n_new,
-                (unsigned long long)res->distinct, (unsigned long long)res->generated);
+                (unsigned long long)res->distinct);
       if (capture_level_ == level + 1 && n_new) {
         captured_.resize(n_new);
         KC_HIP_TRY(hipMemcpy(captured_.data(), next_, n_new * sizeof(State), hipMemcpyDeviceToHost));
@@ -273,7 +278,7 @@ class EngineT final : public EngineBase {
       std::swap(cur_, next_);
       std::swap(cur_cap_, next_cap_);
       n = n_new;
-      cand = c.next_cand() - cand_total;
+      cand = c.cand_total - cand_total;
       cand_total += cand;
       ++level;
       if (n) {
@@ -425,10 +430,16 @@ class EngineT final : public EngineBase {
   }
 
   void finish(kc_result* res, std::chrono::steady_clock::time_point t0, uint64_t left) {
+    // the striped totals are read once, at the end (levels read only the head)
+    if (hipMemcpy(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost) != hipSuccess)
+      set_error("kubecheck: counter readback failed");
+    uint64_t gen = 0;
     for (int a = 0; a < A_COUNT; ++a) {
       res->act_gen[a] = h_ctr_->act_gen(a);
       res->act_dist[a] = h_ctr_->act_dist(a);
+      gen += res->act_gen[a];
     }
+    res->generated = res->init + gen;
     res->depth = res->nlevels;
     res->queue_left = left;
     res->complete = (left == 0 && res->err_kind == 0 && !(cfg_.max_levels && res->nlevels >= cfg_.max_levels && left));

@@ -49,7 +49,8 @@ struct Counters {
   unsigned long long chunk_base;  // next-frontier offset of the current chunk
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
   unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
-  unsigned long long head_pad[12];
+  unsigned long long cand_total;  // sum of the next_cand stripes (k_advance)
+  unsigned long long head_pad[11];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -70,6 +71,9 @@ struct Counters {
     return t;
   }
 };
+// bytes of the per-level head (err_key, chunk_base, overflow, batch_used,
+// cand_total): what the host reads back after every level
+constexpr size_t kCtrHead = 5 * sizeof(unsigned long long);
 __device__ __forceinline__ CtrStripe& stripe(Counters* C) {
   return C->s[blockIdx.x & (CTR_STRIPES - 1)];
 }

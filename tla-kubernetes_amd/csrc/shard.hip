@@ -56,13 +56,13 @@ k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, in
   __shared__ unsigned long long sh_fp[CLAIM_LDS];
   __shared__ unsigned int sh_key[CLAIM_LDS];
   __shared__ unsigned int sh_rep[CLAIM_TILE];
-  __shared__ unsigned int sh_cnt[16 * CLAIM_TILE];   // [owner][parent in tile]
+  extern __shared__ unsigned int sh_cnt[];           // [owner][parent in tile], world * 256
   __shared__ unsigned int sh_act[A_COUNT];
   for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
     sh_fp[k] = 0ull;
     sh_key[k] = ~0u;
   }
-  for (int k = threadIdx.x; k < 16 * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
+  for (uint32_t k = threadIdx.x; k < world * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
   sh_rep[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
@@ -117,8 +117,8 @@ k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, in
 template <class M>
 __global__ void __launch_bounds__(256)
 k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uint32_t world,
-             uint64_t rank, const uint32_t* __restrict__ off /* [world][n] exclusive */,
-             const uint64_t* __restrict__ owner_base, const uint32_t* __restrict__ repmask,
+             uint64_t rank, const uint32_t* __restrict__ off /* [world][n], one exclusive scan */,
+             const uint32_t* __restrict__ repmask,
              Record<M>* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -139,13 +139,23 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k)
       if (k == o) { r = c[k]; c[k] = r + 1; }
-    const uint64_t pos = owner_base[o] + off[(uint64_t)o * n + i] + r;
+    const uint64_t pos = (uint64_t)off[(uint64_t)o * n + i] + r;   // owner-major scan
     Record<M>* rec = out + pos;
 #pragma unroll
     for (int k = 0; k < M::W; ++k) rec->w[k] = x.w[k];
     rec->fp = fp;
     rec->key = (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot);
   }
+}
+
+// Records per owner from the owner-major exclusive scan of cnt[world][n].
+__global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                               uint64_t n, uint32_t world, uint64_t* __restrict__ tot) {
+  const uint32_t o = threadIdx.x;
+  if (o >= world) return;
+  const uint64_t end = (o + 1 < world) ? (uint64_t)off[(uint64_t)(o + 1) * n]
+                                       : (uint64_t)off[(uint64_t)world * n - 1] + cnt[(uint64_t)world * n - 1];
+  tot[o] = end - off[(uint64_t)o * n];
 }
 
 // claim order key of a record: (rank, parent index, successor position)
@@ -269,11 +279,9 @@ class ShardT final : public ShardBase {
       KC_TRY(cs_.init(fp_slots, st_));
     }
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
-    cand_total_ = 0;
     std::vector<State> mine;
     std::vector<unsigned long long> keys;
     std::vector<uint64_t> fps;
-    cand_ = 0;
     for (int k = 0; k < M::num_init(); ++k) {
       State s;
       M::init_state(k, s);
@@ -283,7 +291,6 @@ class ShardT final : public ShardBase {
       mine.push_back(s);
       keys.push_back(KEY_INIT | (uint64_t)k);
       fps.push_back(fp);
-      cand_ += (uint64_t)M::plan(s, flags_).total;
       if (M::check(s) >= 0 && init_err_ == ~0ull)
         init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
     }
@@ -292,7 +299,7 @@ class ShardT final : public ShardBase {
     level_base_.assign(1, 0);
     gen_init_ = n_;
     KC_TRY(grow_buffer(cur_, cur_cap_, std::max<uint64_t>(n_, 1), false, st_));
-    KC_TRY(grow_buffer(pkeys_, pk_cap_, std::max<uint64_t>(n_, 1) + cand_, false, st_));
+    KC_TRY(grow_buffer(pkeys_, pk_cap_, std::max<uint64_t>(n_, 1), false, st_));
     if (n_) {
       KC_HIP_TRY(hipMemcpyAsync(cur_, mine.data(), n_ * sizeof(State), hipMemcpyHostToDevice, st_));
       KC_HIP_TRY(hipMemcpyAsync(pkeys_, keys.data(), n_ * 8, hipMemcpyHostToDevice, st_));
@@ -326,35 +333,30 @@ class ShardT final : public ShardBase {
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
-    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(CLAIM_TILE), 0, st_, cur_, n_, flags_,
+    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(CLAIM_TILE),
+                       (size_t)world_ * CLAIM_TILE * sizeof(unsigned int), st_, cur_, n_, flags_,
                        cfg_.check_deadlock, (uint32_t)world_, cnt_, repmask_, d_ctr_);
+    // one exclusive scan over the owner-major matrix = every record's position
+    // in the owner-grouped send buffer
+    const uint64_t cells = n_ * (uint64_t)world_;
     size_t tmp_bytes = 0;
-    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)n_, st_));
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
     KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-    for (int o = 0; o < world_; ++o)
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_ + (uint64_t)o * n_,
-                                                  off_ + (uint64_t)o * n_, (int)n_, st_));
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
+    hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
+                       d_owner_base_);
     KC_HIP_TRY(hipGetLastError());
-    // per-owner totals = last offset + last count
-    std::vector<uint32_t> lo(world_), lc(world_);
-    for (int o = 0; o < world_; ++o) {
-      KC_HIP_TRY(hipMemcpyAsync(&lo[o], off_ + (uint64_t)o * n_ + n_ - 1, 4, hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipMemcpyAsync(&lc[o], cnt_ + (uint64_t)o * n_ + n_ - 1, 4, hipMemcpyDeviceToHost, st_));
-    }
-    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipMemcpyAsync(h_owner_base_, d_owner_base_, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
     if (h_ctr_->overflow || h_ctr_->batch_used) {
-      set_error("kc_shard_expand: successor overflow / batch table full");
+      set_error("kc_shard_expand: successor overflow");
       return -ENOMEM;
     }
-    uint64_t* base = h_owner_base_;      // pinned: the copy is asynchronous
-    for (int o = 0; o < 16; ++o) base[o] = 0;
     for (int o = 0; o < world_; ++o) {
-      counts[o] = (uint64_t)lo[o] + lc[o];
-      base[o] = send_total_;
+      counts[o] = h_owner_base_[o];
       send_total_ += counts[o];
     }
-    KC_HIP_TRY(hipMemcpyAsync(d_owner_base_, base, 16 * sizeof(uint64_t), hipMemcpyHostToDevice, st_));
     if (h_ctr_->err_key != ~0ull)
       *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_ctr_->err_key);
     return 0;
@@ -366,8 +368,8 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     if (n_ && send_total_) {
       hipLaunchKernelGGL(k_shard_pack<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
-                         cur_, n_, flags_, (uint32_t)world_, (uint64_t)rank_, off_,
-                         d_owner_base_, repmask_, (Rec*)send);
+                         cur_, n_, flags_, (uint32_t)world_, (uint64_t)rank_, off_, repmask_,
+                         (Rec*)send);
       KC_HIP_TRY(hipGetLastError());
     }
     KC_HIP_TRY(hipStreamSynchronize(st_));
@@ -404,7 +406,7 @@ class ShardT final : public ShardBase {
       uint32_t lo = 0, lc = 0;
       KC_HIP_TRY(hipMemcpyAsync(&lo, ioff_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipMemcpyAsync(&lc, isnew_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipStreamSynchronize(st_));
       if (h_ctr_->overflow || h_ctr_->batch_used) {
         set_error("kc_shard_insert: table full");
@@ -422,13 +424,7 @@ class ShardT final : public ShardBase {
                 (unsigned long long)cs_.count);
       }
       cs_.count += next_n_;
-      next_cand_ = h_ctr_->next_cand() - cand_total_;
-      cand_total_ += next_cand_;
       if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
-    } else {
-      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipStreamSynchronize(st_));
-      next_cand_ = 0;
     }
     *n_new = next_n_;
     return 0;
@@ -439,7 +435,6 @@ class ShardT final : public ShardBase {
     std::swap(cur_, next_);
     std::swap(cur_cap_, next_cap_);
     n_ = next_n_;
-    cand_ = next_cand_;
     ++level_;
     return 0;
   }
@@ -508,11 +503,10 @@ class ShardT final : public ShardBase {
   uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
-  uint64_t* d_owner_base_ = nullptr;
+  uint64_t* d_owner_base_ = nullptr;   // per-owner record totals (device / pinned host)
   uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
-  uint64_t n_ = 0, next_n_ = 0, cand_ = 0, next_cand_ = 0, send_total_ = 0, gen_init_ = 0;
-  uint64_t cand_total_ = 0;   // cumulative next_cand counter already consumed
+  uint64_t n_ = 0, next_n_ = 0, send_total_ = 0, gen_init_ = 0;
   uint64_t init_err_ = ~0ull;
   int level_ = 0;
   std::vector<uint64_t> level_base_;

@@ -137,18 +137,26 @@ class ShardedModelChecker:
     # rounds of at most this many bytes per collective.
     A2A_ROUND_BYTES = 256 << 20
 
-    def _exchange(self, send, counts: List[int], rw: int):
-        """All-to-all of the owner-grouped records; returns (recv, n_records),
-        recv grouped by source rank (in rank order)."""
+    def _gather_status(self, counts: List[int], n_new: int, err: int):
+        """One all-gather per level: every rank's record counts per owner plus
+        the (new states, error key) of the level it finished last.  Returns the
+        counts matrix M[src][dst], the new-state counts and the error keys."""
+        R = self.world
+        if R == 1:
+            return [list(counts)], [n_new], [err]
+        cin = self._i64(list(counts) + [n_new, err])
+        out = self.torch.empty(R * (R + 2), dtype=self.torch.int64, device=self.dev)
+        self.dist.all_gather_into_tensor(out, cin, group=self.group)
+        rows = out.view(R, R + 2).tolist()
+        return [r[:R] for r in rows], [r[R] for r in rows], [r[R + 1] for r in rows]
+
+    def _exchange(self, send, M: List[List[int]], rw: int):
+        """All-to-all of the owner-grouped records given the counts matrix
+        M[src][dst]; returns (recv, n_records), recv grouped by source rank."""
         torch, dist, R = self.torch, self.dist, self.world
+        counts = M[self.rank]
         if R == 1:
             return send, counts[0]
-        # the full counts matrix M[src][dst] on every rank (one all-gather),
-        # so every rank derives the same round schedule
-        cin = self._i64(counts)
-        mat = torch.empty(R * R, dtype=torch.int64, device=self.dev)
-        dist.all_gather_into_tensor(mat, cin, group=self.group)
-        M = [[int(x) for x in row] for row in mat.view(R, R).tolist()]
         rcounts = [M[src][self.rank] for src in range(R)]
         recv = self._buffer("_recv", max(sum(rcounts), 1) * rw)
         q = max(1, self.A2A_ROUND_BYTES // (8 * rw * R))      # records per pair per round
@@ -185,30 +193,44 @@ class ShardedModelChecker:
     def run(self) -> dict:
         dist, be, rb = self.dist, self.be, self.be.record_bytes
         t0 = time.perf_counter()
-        n_local = be.init()
-        width = self._allreduce([n_local], dist.ReduceOp.SUM)[0]
-        widths = [width]
-        level, err = 1, NONE_KEY
+        # One collective round trip per level: the all-gather that carries the
+        # next level's record counts also carries the previous level's
+        # (new states, error key).  Expanding a level before knowing that the
+        # previous one ended the check is harmless (an empty frontier expands
+        # to nothing; on an error the expansion is simply not used).
+        # (After an error, the partial generated count therefore includes the
+        # next level's expansion; TLC's partial counts at an error are not
+        # deterministic either, and the error, its level and trace are.)
+        status_new, status_err = be.init(), NONE_KEY
+        widths, level, err = [], 1, NONE_KEY
+        rw = rb // 8                                      # record words
         while True:
-            if self.cfg.max_levels and level >= self.cfg.max_levels:
+            last = bool(self.cfg.max_levels and level >= self.cfg.max_levels)
+            if last:                                      # record the width, expand nothing
+                counts, e1 = [0] * self.world, NONE_KEY
+            else:
+                counts, e1 = be.expand()                  # expand `level`
+            M, news, errs = self._gather_status(counts, status_new, status_err)
+            err = min(errs)
+            if err != NONE_KEY:                           # found while producing `level`
+                level -= 1
                 break
-            counts, e1 = be.expand()
-            rw = rb // 8                                  # record words
+            total = sum(news)                             # width of `level`
+            if total == 0:
+                level -= 1
+                break
+            widths.append(total)
+            if last:
+                break
             send = self._buffer("_send", max(sum(counts), 1) * rw)
             be.pack(send)
-            recv, nrecv = self._exchange(send, counts, rw)
+            recv, nrecv = self._exchange(send, M, rw)
             self._sync()
             n_new, e2 = be.insert(recv, nrecv)
             e = min(e1, e2)
-            [err] = self._allreduce([e if e < NONE_KEY else NONE_KEY], dist.ReduceOp.MIN)
-            [total_new] = self._allreduce([n_new], dist.ReduceOp.SUM)
-            if err != NONE_KEY:
-                break
-            if total_new == 0:
-                break
+            status_new, status_err = n_new, (e if e < NONE_KEY else NONE_KEY)
             be.advance()
             level += 1
-            widths.append(total_new)
         seconds = time.perf_counter() - t0
         res = be.result()
         agg = self._allreduce(res["act_gen"] + res["act_dist"] +

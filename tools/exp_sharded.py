@@ -19,13 +19,20 @@ from kubecheck.distributed import HipShard, ShardedModelChecker  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--np", type=int, default=2)
 ap.add_argument("--nc", type=int, default=1)
+ap.add_argument("--runs", type=int, default=2)
 a = ap.parse_args()
+for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0"), ("MASTER_ADDR", "127.0.0.1"),
+             ("MASTER_PORT", "29533")):
+    os.environ.setdefault(k, v)                     # world 1 without torchrun
 local = int(os.environ.get("LOCAL_RANK", "0"))
 torch.cuda.set_device(local)
 dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 cfg = ModelConfig(nc=a.nc, np=a.np, device=local, fpset_slots=1 << 20)
-r = ShardedModelChecker(cfg, HipShard(cfg, dist.get_rank(), dist.get_world_size())).run()
-if dist.get_rank() == 0:
-    print({k: r[k] for k in ("distinct", "generated", "depth", "error", "complete", "seconds")},
-          r.get("error_action"), r.get("error_invariant"), r.get("error_level"), r["level_width"][-5:], flush=True)
+mc = ShardedModelChecker(cfg, HipShard(cfg, dist.get_rank(), dist.get_world_size()))
+for _ in range(a.runs):
+    r = mc.run()
+    if dist.get_rank() == 0:
+        print({k: r[k] for k in ("distinct", "generated", "depth", "error", "complete", "seconds")},
+              r.get("error_action"), r.get("error_invariant"), r.get("error_level"), r["level_width"][-5:],
+              flush=True)
 dist.destroy_process_group()
