@@ -220,6 +220,10 @@ int kc_spec_successors(const kc_model_config *cfg, const uint64_t *tuple, int *a
 int kc_spec_check(const kc_model_config *cfg, const uint64_t *tuple);
 /* Fingerprint of the packed form of a canonical tuple. */
 int kc_spec_fingerprint(const kc_model_config *cfg, const uint64_t *tuple, uint64_t *fp_out);
+/* Self-check of the kernels' incremental fingerprint: the number of
+ * successors of `tuple` whose fingerprint_succ differs from a full
+ * fingerprint (0 expected), <0 on error. */
+int kc_spec_fp_selfcheck(const kc_model_config *cfg, const uint64_t *tuple);
 /* Packed <-> canonical conversion. */
 int kc_spec_pack(const kc_model_config *cfg, const uint64_t *tuple, uint64_t *packed_out);
 int kc_spec_unpack(const kc_model_config *cfg, const uint64_t *packed, uint64_t *tuple_out);

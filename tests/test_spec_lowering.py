@@ -24,6 +24,7 @@ def _bfs_compare(oracle, nc, np_, ns, max_levels=0, **flags):
         for s in frontier:
             ps, pf = sp.successors(s)
             os_, of = oracle.successors(ocfg, s)
+            assert sp.fp_selfcheck(s) == 0      # kernels' incremental fingerprint
             assert pf == of
             checked += 1
             if ps is None:

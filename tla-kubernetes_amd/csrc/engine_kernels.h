@@ -1,20 +1,10 @@
-// engine_kernels.h — the four per-level BFS kernels (gfx950).
+// engine_kernels.h — the per-level BFS kernels of the single-GPU engine
+// (gfx950): k_claim, k_settle_rec / k_settle_tile, k_emit.
 //
-// One lane = one parent state.  Each kernel re-derives the parent's
-// successor plan from its packed words (cheap integer work) instead of
-// materialising candidate states in HBM; the only random HBM traffic is the
-// FPSet probe of each level-unique successor.
-//
-//   k_expand  : plan + every successor's fingerprint -> batch table
-//               (min order key per fp); per-action "generated" counters;
-//               Assert-failure / deadlock error keys.
-//   k_resolve : the batch representative of each fp probes/inserts the
-//               FPSet; per-parent bitmask + count of NEW successors.
-//   (scan)    : exclusive prefix sum of the counts (hipcub).
-//   k_emit    : NEW successors written in (parent, successor) order to the
-//               next frontier, with parent pointers (TLC's trace file),
-//               invariant checks (TypeOK, OnlyOneVersion), per-action
-//               "distinct" counters and the next level's candidate count.
+// One lane = one parent state.  Each kernel re-derives a parent's successor
+// plan from its packed words (cheap integer work) instead of materialising
+// candidate states in HBM; the random HBM traffic is the ClaimSet probe of
+// each tile representative and the re-read of each candidate.
 //
 // Order key of a successor: (parent index within the level) << 8 | t, where
 // t is its position in TLC's enumeration order.  Error keys put the parent
@@ -97,120 +87,6 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
   ulonglong2* v = reinterpret_cast<ulonglong2*>(p + i);
 #pragma unroll
   for (int k = 0; k < M::W / 2; ++k) v[k] = make_ulonglong2(s.w[2 * k], s.w[2 * k + 1]);
-}
-
-// batch_insert with a bounded probe: returns false if the table is full.
-// One 16-B load reads {fp, ~key}; the atomicMax is skipped when the stored
-// ~key already dominates (nkey only grows, so a stale read is a lower bound).
-__device__ __forceinline__ bool batch_insert_bounded(BatchEntry* __restrict__ t, uint64_t mask,
-                                                     uint64_t fp, uint64_t key) {
-  const unsigned long long nk = ~(unsigned long long)key;
-  uint64_t i = batch_slot(fp, mask);
-  // a probe run this long means the table is overfull (at <= 50% load the
-  // chance is negligible): report it and let the host retry with 2x slots
-  const uint64_t max_probe = mask < 1024 ? mask : 1024;
-  for (uint64_t probe = 0; probe <= max_probe; ++probe) {
-    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&t[i]);
-    unsigned long long efp = e.x, ekey = e.y;
-    if (efp == 0ull) {
-      efp = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
-      if (efp == 0ull) {
-        atomicMax(&t[i].nkey, nk);
-        return true;
-      }
-      ekey = 0;
-    }
-    if (efp == fp) {
-      if (ekey < nk) atomicMax(&t[i].nkey, nk);
-      return true;
-    }
-    i = (i + 1) & mask;
-  }
-  return false;
-}
-
-template <class M>
-__global__ void __launch_bounds__(256)
-k_expand(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
-         int check_deadlock, BatchEntry* __restrict__ bt, uint64_t bmask, Counters* __restrict__ C) {
-  // Idempotent (batch-table claims and min error keys only), so the host can
-  // re-run a chunk with a larger table if a probe run reports overflow.
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const typename M::State s = load_state<M>(cur, i);
-  const typename M::Plan pl = M::plan(s, f);
-  const uint64_t pidx = base + i;
-  if (pl.fail_pos >= 0)
-    atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
-  else if (pl.total == 0 && check_deadlock)
-    atomicMin(&C->err_key, (pidx << 16) | E_DEADLOCK);
-  int tot = pl.total;
-  if (tot > M::MAXSUCC) {
-    atomicAdd(&C->overflow, 1ull);
-    tot = M::MAXSUCC;
-  }
-  for (int t = 0; t < tot; ++t) {
-    int slot, j;
-    M::locate(pl, t, slot, j);
-    typename M::State x;
-    M::apply(s, slot, j, f, x);
-    if (!batch_insert_bounded(bt, bmask, M::fingerprint(x), (pidx << 8) | (uint64_t)t))
-      atomicAdd(&C->batch_used, 1ull);      // batch table overfull: host retries
-  }
-}
-
-template <class M>
-__global__ void __launch_bounds__(256)
-k_resolve(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
-          const BatchEntry* __restrict__ bt, uint64_t bmask, unsigned long long* __restrict__ slots,
-          uint64_t nbuckets, uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
-          Counters* __restrict__ C) {
-  __shared__ unsigned int sh_act[A_COUNT];
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < n;
-  typename M::State s;
-  if (live) s = load_state<M>(cur, i);
-  else for (int k = 0; k < M::W; ++k) s.w[k] = 0;
-  const typename M::Plan pl = M::plan(s, f);
-  const uint64_t pidx = base + i;
-  const int tot = !live ? 0 : pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
-  uint32_t mask = 0;
-  unsigned probes = 0;
-  // per-action "generated" counters (TLC msg 2772, second number)
-  if (live) {
-#pragma unroll
-    for (int slot = 0; slot < M::NSLOT; ++slot) {
-      const int c = (int)((pl.counts >> (6 * slot)) & 63);
-      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
-    }
-  }
-  for (int t = 0; t < tot; ++t) {
-    int slot, j;
-    M::locate(pl, t, slot, j);
-    typename M::State x;
-    M::apply(s, slot, j, f, x);
-    const uint64_t fp = M::fingerprint(x);
-    if (batch_is_rep(bt, bmask, fp, (pidx << 8) | (uint64_t)t)) {
-      ++probes;
-      const int r = fpset_insert(slots, nbuckets, fp);
-      if (r == 1) mask |= 1u << t;
-      else if (r < 0) atomicAdd(&C->overflow, 1ull);
-    }
-  }
-  if (live) {
-    newmask[i] = mask;
-    newcnt[i] = (uint32_t)__popc(mask);
-  }
-  // probe count: one atomic per wave
-  unsigned long long pw = probes;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
-  if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
-  __syncthreads();
-  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
 // ------------------------------------------------------------------------
@@ -299,6 +175,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if (live) {
     const typename M::State s = load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
+    const uint64_t fold = M::fp_fold(s);
     const uint64_t pidx = base + i;
     if (ABL == 0) {
       if (pl.fail_pos >= 0)
@@ -321,8 +198,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       int slot, j;
       M::locate(pl, t, slot, j);
       typename M::State x;
-      M::apply(s, slot, j, f, x);
-      const uint64_t fp = M::fingerprint(x);
+      int who;
+      M::apply(s, slot, j, f, x, who);
+      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
       if (ABL == 2) {
         acc ^= fp;
         continue;
@@ -430,15 +308,17 @@ k_settle_tile(const typename M::State* __restrict__ cur, uint64_t n, uint64_t ba
     if (mask) {
       const typename M::State s = load_state<M>(cur, i);
       const typename M::Plan pl = M::plan(s, f);
+      const uint64_t fold = M::fp_fold(s);
       const uint64_t pidx = base + i;
       for (; mask; mask &= mask - 1) {
         const int t = __ffs(mask) - 1;
         int slot, j;
         M::locate(pl, t, slot, j);
         typename M::State x;
-        M::apply(s, slot, j, f, x);
+        int who;
+        M::apply(s, slot, j, f, x, who);
         ++reads;
-        const unsigned long long nc = claimset_get(cs, nbuckets, M::fingerprint(x));
+        const unsigned long long nc = claimset_get(cs, nbuckets, M::fingerprint_succ(s, fold, x, who));
         if (~nc == make_claim(level, (pidx << 8) | (uint64_t)t)) nm |= 1u << t;
       }
     }

@@ -448,7 +448,7 @@ struct Model {
   // Build successor j of slot `slot` into t (t starts as a copy of s).  One
   // copy of every action body, indexed by the runtime actor (apply is the
   // part of the kernel that runs once per successor).
-  KC_HD static void apply_rt(const State& s, int slot, int j, const Flags& f, State& t) {
+  KC_HD static int apply_rt(const State& s, int slot, int j, const Flags& f, State& t) {
     if (slot < 2 * A) {
       const int a = slot < A ? slot : slot - A;
       uint64_t w = aw_d(s, a);
@@ -532,7 +532,7 @@ struct Model {
         }
       }
       put_word_d(t, a, w);
-      return;
+      return a;
     }
     // APIStart (:698-756): successor j serves the j-th pending request (in
     // actor order), then the pending list requests.
@@ -577,7 +577,7 @@ struct Model {
       }
       t.w[0] = nw;
       put_word_d(t, c, sw(w, F_RQST, 2, st));
-      return;
+      return c;
     }
     if (plr) {                                                  // :745-753
       const int c = nth_bit(plr, j - nrq);
@@ -585,14 +585,21 @@ struct Model {
       set_objs_d(t, c, api & km);
       put_word_d(t, c, sw(aw_d(s, c), F_LRST, 2, ST_Ok));
       t.w[0] = read_map(api, km, c);
+      return c;
     }
+    return 0;
   }
 
-  // Build successor j of `slot` (KubeAPI.tla:471-756).
-  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t) {
+  // Build successor j of `slot` (KubeAPI.tla:471-756); `who` = the process
+  // whose word the action rewrote (for fingerprint_succ).
+  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t, int& who) {
 #pragma unroll
     for (int i = 0; i < W; ++i) t.w[i] = s.w[i];
-    apply_rt(s, slot, j, f, t);
+    who = apply_rt(s, slot, j, f, t);
+  }
+  KC_HD static void apply(const State& s, int slot, int j, const Flags& f, State& t) {
+    int who;
+    apply(s, slot, j, f, t, who);
   }
 
   // ------------------------------------------------------------ invariants
@@ -621,21 +628,69 @@ struct Model {
   // --------------------------------------------------------- fingerprint
   // 64-bit fingerprint of the canonical packed words, normalised the way the
   // FPSet stores it: MSB clear (TLC's disk FPSets reserve it), never 0.
-  KC_HD static uint64_t fingerprint(const State& s) {
-    uint64_t h = 0x6a09e667f3bcc909ull ^ (uint64_t)(W * 0x9e3779b97f4a7c15ull);
+  //
+  // Zobrist-style: fp = final(XOR_k mix(w_k, k)), every mix and the final
+  // step a bijection of 64-bit words (xor-shifts and odd multiplies).  A
+  // successor differs from its parent in at most three words — apiState, the
+  // acting process's word and that process's listRequests.objs word — so the
+  // kernels fold the parent once and re-mix only the changed words
+  // (fingerprint_succ); two states collide only if the XOR of their words'
+  // mix differences vanishes (probability ~2^-64 per pair, as for TLC's
+  // polynomial FP64, which is also linear over GF(2)).
+  KC_HD static uint64_t word_mix(uint64_t w, int k) {
+    uint64_t z = w ^ (0x6a09e667f3bcc909ull + (uint64_t)k * 0x9e3779b97f4a7c15ull);
+    z *= 0xbf58476d1ce4e5b9ull;
+    z ^= z >> 31;
+    z *= 0x94d049bb133111ebull;
+    return z ^ (z >> 29);
+  }
+  KC_HD static uint64_t fp_fold(const State& s) {
+    uint64_t x = 0;
 #pragma unroll
-    for (int i = 0; i < W_RAW; ++i) {
-      uint64_t k = s.w[i] * 0x87c37b91114253d5ull;
-      k = (k << 31) | (k >> 33);
-      k *= 0x4cf5ad432745937full;
-      h ^= k;
-      h = ((h << 27) | (h >> 37)) * 5 + 0x52dce729ull;
-    }
+    for (int i = 0; i < W_RAW; ++i) x ^= word_mix(s.w[i], i);
+    return x;
+  }
+  KC_HD static uint64_t fp_final(uint64_t h) {
     h ^= h >> 33; h *= 0xff51afd7ed558ccdull;
     h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
     h ^= h >> 33;
     h &= 0x7fffffffffffffffull;
     return h ? h : 1;
+  }
+  KC_HD static uint64_t fingerprint(const State& s) { return fp_final(fp_fold(s)); }
+
+  // Fingerprint of successor x of s, given s's fold and the process `who`
+  // whose word the action rewrote (apply's out-parameter).  Equal to
+  // fingerprint(x).
+  KC_HD static uint64_t fingerprint_succ(const State& s, uint64_t fold_s, const State& x, int who) {
+    uint64_t h = fold_s;
+    if (x.w[0] != s.w[0]) h ^= word_mix(s.w[0], 0) ^ word_mix(x.w[0], 0);
+    {
+      uint64_t o = s.w[1], nw = x.w[1];
+#pragma unroll
+      for (int k = 1; k < A; ++k) {
+        uint64_t vo = s.w[1 + k], vn = x.w[1 + k];
+        opaque(vo);
+        opaque(vn);
+        o = (who == k) ? vo : o;
+        nw = (who == k) ? vn : nw;
+      }
+      if (o != nw) h ^= word_mix(o, 1 + who) ^ word_mix(nw, 1 + who);
+    }
+    {
+      const int wi = 1 + A + who / OBJ_PER_WORD;
+      uint64_t o = s.w[1 + A], nw = x.w[1 + A];
+#pragma unroll
+      for (int k = 1; k < OBJ_WORDS; ++k) {
+        uint64_t vo = s.w[1 + A + k], vn = x.w[1 + A + k];
+        opaque(vo);
+        opaque(vn);
+        o = (wi == 1 + A + k) ? vo : o;
+        nw = (wi == 1 + A + k) ? vn : nw;
+      }
+      if (o != nw) h ^= word_mix(o, wi) ^ word_mix(nw, wi);
+    }
+    return fp_final(h);
   }
 
   // ------------------------------------------------ canonical tuple (ABI)

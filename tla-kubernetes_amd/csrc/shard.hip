@@ -70,6 +70,7 @@ k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, in
   if (i < n) {
     const typename M::State s = load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
+    const uint64_t fold = M::fp_fold(s);
     if (pl.fail_pos >= 0)
       atomicMin(&C->err_key, (i << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
     else if (pl.total == 0 && check_deadlock)
@@ -88,8 +89,9 @@ k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, in
       int slot, j;
       M::locate(pl, t, slot, j);
       typename M::State x;
-      M::apply(s, slot, j, f, x);
-      const uint64_t fp = M::fingerprint(x);
+      int who;
+      M::apply(s, slot, j, f, x, who);
+      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
       if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0) {
         // LDS table full: this copy is sent as its own representative
         atomicOr(&sh_rep[threadIdx.x], 1u << t);
@@ -126,14 +128,16 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
   if (!mask) return;
   const typename M::State s = load_state<M>(cur, i);
   const typename M::Plan pl = M::plan(s, f);
+  const uint64_t fold = M::fp_fold(s);
   uint32_t c[16] = {};
   for (; mask; mask &= mask - 1) {
     const int t = __ffs(mask) - 1;
     int slot, j;
     M::locate(pl, t, slot, j);
     typename M::State x;
-    M::apply(s, slot, j, f, x);
-    const uint64_t fp = M::fingerprint(x);
+    int who;
+    M::apply(s, slot, j, f, x, who);
+    const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
     const uint32_t o = owner_of(fp, world);
     uint32_t r = 0;
 #pragma unroll

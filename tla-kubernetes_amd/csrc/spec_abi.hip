@@ -237,6 +237,27 @@ int kc_spec_fingerprint(const kc_model_config* cfg, const uint64_t* tuple, uint6
   });
 }
 
+int kc_spec_fp_selfcheck(const kc_model_config* cfg, const uint64_t* tuple) {
+  if (!cfg || !tuple) { set_error("kc_spec_fp_selfcheck: NULL"); return -EINVAL; }
+  return with_model(cfg->nc, cfg->np, cfg->ns, [&](auto m) {
+    using M = decltype(m);
+    typename M::State s;
+    if (!M::from_tuple(tuple, s)) { set_error("kc_spec_fp_selfcheck: bad tuple"); return -EINVAL; }
+    const Flags f{cfg->can_fail, cfg->can_timeout, cfg->variant};
+    const typename M::Plan pl = M::plan(s, f);
+    const uint64_t fold = M::fp_fold(s);
+    int bad = 0;
+    for (int t = 0; t < pl.total; ++t) {
+      int slot, j, who;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      M::apply(s, slot, j, f, x, who);
+      if (M::fingerprint_succ(s, fold, x, who) != M::fingerprint(x)) ++bad;
+    }
+    return bad;
+  });
+}
+
 int kc_spec_pack(const kc_model_config* cfg, const uint64_t* tuple, uint64_t* packed) {
   if (!cfg || !tuple || !packed) { set_error("kc_spec_pack: NULL"); return -EINVAL; }
   return with_model(cfg->nc, cfg->np, cfg->ns, [&](auto m) {

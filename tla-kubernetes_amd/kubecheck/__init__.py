@@ -321,6 +321,12 @@ class Spec:
         check("kc_spec_fingerprint", self._lib.kc_spec_fingerprint(C.byref(self._c), _u64(t), C.byref(fp)))
         return fp.value
 
+    def fp_selfcheck(self, tup) -> int:
+        """Successors whose incremental (kernel) fingerprint differs from the
+        full one; 0 expected."""
+        t = np.ascontiguousarray(tup, dtype=np.uint64)
+        return check("kc_spec_fp_selfcheck", self._lib.kc_spec_fp_selfcheck(C.byref(self._c), _u64(t)))
+
     def pack(self, tup) -> np.ndarray:
         t = np.ascontiguousarray(tup, dtype=np.uint64)
         out = np.zeros(self.state_words, dtype=np.uint64)

@@ -104,6 +104,7 @@ SIGNATURES = [
     ("kc_spec_successors", C.c_int, [C.POINTER(KcModelConfig), _U64P, _IP, _U64P, C.c_int, _IP]),
     ("kc_spec_check", C.c_int, [C.POINTER(KcModelConfig), _U64P]),
     ("kc_spec_fingerprint", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
+    ("kc_spec_fp_selfcheck", C.c_int, [C.POINTER(KcModelConfig), _U64P]),
     ("kc_spec_pack", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
     ("kc_spec_unpack", C.c_int, [C.POINTER(KcModelConfig), _U64P, _U64P]),
 ]
