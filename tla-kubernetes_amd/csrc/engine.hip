@@ -187,7 +187,6 @@ class EngineT final : public EngineBase {
         KC_TRY(grow_buffer(ord_, ord_cap_, next_gidx + cand + 1, true, st_));
       }
       KC_TRY(cs_.reserve(cand, st_));
-      KC_TRY(grow_buffer(curmask_, cur_mcap_, std::min(n, chunk), false, st_));
       {
         const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
         KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
@@ -209,7 +208,7 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             curmask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+                             abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
@@ -225,12 +224,12 @@ class EngineT final : public EngineBase {
           });
         }
         timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_settle_rec, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
+          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
                              d_ctr_);
-          hipLaunchKernelGGL(k_settle_tile<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
-                             cn, start, flags_, cs_.t, cs_.nslots, succ_level, rcount_, curmask_,
-                             newmask_, newcnt_, d_ctr_);
+          hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
+                             d_ctr_);
         });
         size_t tmp_bytes = 0;
         KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt_, offsets_, (int)cn, st_));
@@ -454,7 +453,7 @@ class EngineT final : public EngineBase {
   void release() {
     (void)hipSetDevice(cfg_.device);
     cs_.release();
-    for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)curmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
+    for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
                     (void*)newcnt_, (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
@@ -471,13 +470,12 @@ class EngineT final : public EngineBase {
   uint8_t* ord_ = nullptr;
   uint64_t par_cap_ = 0, ord_cap_ = 0;
   uint32_t *newmask_ = nullptr, *newcnt_ = nullptr, *offsets_ = nullptr;
-  uint32_t* curmask_ = nullptr;
   uint32_t* abl_mask_ = nullptr;
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
   uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;
   uint64_t abl_cap_ = 0;
-  uint64_t cur_mcap_ = 0, mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
+  uint64_t mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
   Counters* d_ctr_ = nullptr;

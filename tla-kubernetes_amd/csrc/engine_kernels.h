@@ -1,5 +1,5 @@
 // engine_kernels.h — the per-level BFS kernels of the single-GPU engine
-// (gfx950): k_claim, k_settle_rec / k_settle_tile, k_emit.
+// (gfx950): k_claim, k_settle_rec, k_emit.
 //
 // One lane = one parent state.  Each kernel re-derives a parent's successor
 // plan from its packed words (cheap integer work) instead of materialising
@@ -99,33 +99,32 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 //              so about half of all successors die here without touching HBM.
 //              Then each tile representative claims its fp in the ClaimSet
 //              (one 64-B bucket read; atomics only for current-level fps).
-//              Per parent: bitmask of successors that may have won (curmask);
-//              per tile: the list of those candidates {fp, tile-local key}.
-//   k_settle_rec : re-reads each candidate's claim and keeps those whose
-//              claim is the stored minimum -> newmask / newcnt (scan + emit);
-//              no successor is re-derived.
-//   k_settle_tile: the same for a tile whose candidate list overflowed, by
-//              re-deriving its curmask successors.
+//              Per tile: the list of candidates that may win
+//              {fp, tile-local key, inserted-here flag}.
+//   k_settle_rec<0>, <1> : the claimants fold their claims into the slots,
+//              then every candidate keeps its successor iff its claim is the
+//              stored minimum -> newmask / newcnt (scan + emit); no successor
+//              is re-derived.
 // Tile-local dedup only ever discards a copy whose fp is held by a smaller
 // key of the same tile, which can never be the level minimum; an LDS table
 // overflow just sends the copy to the ClaimSet directly.
 constexpr int CLAIM_TILE = 256;
 constexpr int CLAIM_LDS_BITS = 11;
 constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
-// Candidate records per tile (tile representatives whose claim may have won):
-// fp + tile-local key, for k_settle_rec.  A tile with more candidates than
-// CLAIM_RCAP is settled by k_settle_tile (re-derivation from curmask).
-constexpr int CLAIM_RCAP = 1024;
+// Candidate records per tile (tile representatives whose claim may win):
+// fp + tile-local key (bit 31: this lane inserted the fp), for the settle
+// passes.  A tile has at most CLAIM_TILE * 32 successors, so the list cannot
+// overflow.
+constexpr int CLAIM_RCAP = CLAIM_TILE * 32;
+constexpr unsigned int CAND_INSERTER = 1u << 31;
 
 __device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t tile,
                                                unsigned long long* __restrict__ rec_fp,
                                                unsigned int* __restrict__ rec_lk, uint64_t fp,
                                                unsigned int lk) {
   const unsigned int k = atomicAdd(sh_rc, 1u);
-  if (k < CLAIM_RCAP) {
-    rec_fp[tile * CLAIM_RCAP + k] = fp;
-    rec_lk[tile * CLAIM_RCAP + k] = lk;
-  }
+  rec_fp[tile * CLAIM_RCAP + k] = fp;
+  rec_lk[tile * CLAIM_RCAP + k] = lk;
 }
 
 __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int* sh_key,
@@ -152,7 +151,7 @@ template <class M, int ABL = 0>
 __global__ void __launch_bounds__(CLAIM_TILE)
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-        uint32_t* __restrict__ curmask, unsigned int* __restrict__ rcount,
+        uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         Counters* __restrict__ C) {
   __shared__ unsigned long long sh_fp[CLAIM_LDS];
@@ -208,14 +207,13 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
         // LDS table full: claim this copy directly
         ++probes;
-        const int r = claimset_claim(cs, nbuckets, fp, make_claim(level, (pidx << 8) | (uint64_t)t), level);
+        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | (uint64_t)t), level);
         if (r >= CL_CUR) {
-          if (r == CL_FULL) {
+          if (r == CL_FULL)
             atomicAdd(&C->overflow, 1ull);
-          } else {
-            atomicOr(&sh_cur[threadIdx.x], 1u << t);
-            push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
-          }
+          else
+            push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp,
+                           ((threadIdx.x << 5) | (unsigned)t) | (r == CL_NEW ? CAND_INSERTER : 0u));
         }
       }
     }
@@ -223,7 +221,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   __syncthreads();
   if (ABL != 0) {
-    if (live) curmask[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
+    if (live) scratch[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
     return;
   }
   // every tile representative claims its fp in the ClaimSet
@@ -234,18 +232,15 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const unsigned int lp = lk >> 5, t = lk & 31;
     const uint64_t pidx = base + tile0 + lp;
     ++probes;
-    const int r = claimset_claim(cs, nbuckets, fp, make_claim(level, (pidx << 8) | t), level);
+    const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | t), level);
     if (r >= CL_CUR) {
-      if (r == CL_FULL) {
+      if (r == CL_FULL)
         atomicAdd(&C->overflow, 1ull);
-      } else {
-        atomicOr(&sh_cur[lp], 1u << t);
-        push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk);
-      }
+      else
+        push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk | (r == CL_NEW ? CAND_INSERTER : 0u));
     }
   }
   __syncthreads();
-  if (live) curmask[i] = sh_cur[threadIdx.x];
   if (threadIdx.x == 0) rcount[blockIdx.x] = sh_rc;
   unsigned long long pw = probes;
 #pragma unroll
@@ -255,75 +250,43 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
-// k_settle_rec: one workgroup per claim tile; each candidate record re-reads
-// its claim (one bucket line) and wins iff the stored claim is its own.
+// k_settle_rec<PASS>: one workgroup per claim tile (STORE-claim protocol,
+// fpset_dev.h).  PASS 0: every claimant candidate folds its claim into its
+// slot with atomicMax.  PASS 1 (a later launch): every candidate, inserter or
+// claimant, wins iff the stored claim is its own -> newmask / newcnt.  No
+// successor is re-derived.
+template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
-k_settle_rec(uint64_t n, uint64_t base, const ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
              uint32_t level, const unsigned int* __restrict__ rcount,
              const unsigned long long* __restrict__ rec_fp, const unsigned int* __restrict__ rec_lk,
              uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt, Counters* __restrict__ C) {
   __shared__ unsigned int sh_new[CLAIM_TILE];
   const unsigned int cnt = rcount[blockIdx.x];
-  if (cnt > CLAIM_RCAP) return;                   // k_settle_tile's tile
-  sh_new[threadIdx.x] = 0;
+  if (PASS == 1) sh_new[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
   unsigned reads = 0;
   for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
     const uint64_t r = (uint64_t)blockIdx.x * CLAIM_RCAP + k;
-    const unsigned long long fp = rec_fp[r];
     const unsigned int lk = rec_lk[r];
-    const uint64_t pidx = base + tile0 + (lk >> 5);
+    if (PASS == 0 && (lk & CAND_INSERTER)) continue;
+    const unsigned long long fp = rec_fp[r];
+    const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
+    const uint64_t claim = make_claim(level, ((base + tile0 + lp) << 8) | t);
     ++reads;
-    if (~claimset_get(cs, nbuckets, fp) == make_claim(level, (pidx << 8) | (lk & 31)))
-      atomicOr(&sh_new[lk >> 5], 1u << (lk & 31));
+    if (PASS == 0) {
+      claimset_store_claim(cs, nbuckets, fp, claim);
+    } else if (~claimset_get(cs, nbuckets, fp) == claim) {
+      atomicOr(&sh_new[lp], 1u << t);
+    }
   }
+  if (PASS == 0) return;
   __syncthreads();
   const uint64_t i = tile0 + threadIdx.x;
   if (i < n) {
     newmask[i] = sh_new[threadIdx.x];
     newcnt[i] = (uint32_t)__popc(sh_new[threadIdx.x]);
-  }
-  unsigned long long rw = reads;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
-  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
-}
-
-// k_settle_tile: the tiles whose candidate list overflowed CLAIM_RCAP
-// re-derive their curmask successors (every other tile returns at once).
-template <class M>
-__global__ void __launch_bounds__(CLAIM_TILE)
-k_settle_tile(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
-              const ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-              const unsigned int* __restrict__ rcount, const uint32_t* __restrict__ curmask,
-              uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt,
-              Counters* __restrict__ C) {
-  if (rcount[blockIdx.x] <= CLAIM_RCAP) return;
-  const uint64_t i = (uint64_t)blockIdx.x * CLAIM_TILE + threadIdx.x;
-  uint32_t nm = 0;
-  unsigned reads = 0;
-  if (i < n) {
-    uint32_t mask = curmask[i];
-    if (mask) {
-      const typename M::State s = load_state<M>(cur, i);
-      const typename M::Plan pl = M::plan(s, f);
-      const uint64_t fold = M::fp_fold(s);
-      const uint64_t pidx = base + i;
-      for (; mask; mask &= mask - 1) {
-        const int t = __ffs(mask) - 1;
-        int slot, j;
-        M::locate(pl, t, slot, j);
-        typename M::State x;
-        int who;
-        M::apply(s, slot, j, f, x, who);
-        ++reads;
-        const unsigned long long nc = claimset_get(cs, nbuckets, M::fingerprint_succ(s, fold, x, who));
-        if (~nc == make_claim(level, (pidx << 8) | (uint64_t)t)) nm |= 1u << t;
-      }
-    }
-    newmask[i] = nm;
-    newcnt[i] = (uint32_t)__popc(nm);
   }
   unsigned long long rw = reads;
 #pragma unroll

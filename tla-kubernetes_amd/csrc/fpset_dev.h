@@ -159,6 +159,59 @@ __device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64
   return CL_FULL;
 }
 
+// STORE-claim protocol (the single-GPU engine; one atomic per new state):
+//   claim kernel — the lane whose CAS inserts fp writes its claim with a
+//     PLAIN store (it is the slot's only writer in this kernel).  A lane that
+//     finds fp stored by an earlier level: CL_OLD.  Finds a smaller claim
+//     already stored: CL_LOST (no write).  Otherwise (claim word still 0, or
+//     larger than its own): CL_CUR, a candidate, still without any write.
+//   settle pass A (next kernel) — every CL_CUR candidate atomicMax'es its
+//     claim into the slot (claimset_store_claim), so the slot ends with the
+//     minimum over the inserter and all candidates;
+//   settle pass B (next kernel) — every candidate and inserter wins iff the
+//     stored claim is its own.
+// Stale copies in another XCD's L2 can only show a slot empty or its claim
+// word 0, which makes a lane a candidate (conservative); the CAS result is
+// authoritative for the fp.
+__device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, uint64_t nslots,
+                                                    uint64_t fp, uint64_t claim, uint32_t level) {
+  const unsigned long long nc = ~(unsigned long long)claim;
+  uint64_t i = bucket_of(fp, nslots);
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+    unsigned long long f = e.x, seen = e.y;
+    if (f == 0ull) {
+      f = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (f == 0ull) {
+        t[i].nclaim = nc;
+        return CL_NEW;
+      }
+      seen = 0ull;
+    }
+    if (f == fp) {
+      if (seen != 0ull && ((~seen) >> CLAIM_KEY_BITS) < level) return CL_OLD;
+      return (seen != 0ull && seen >= nc) ? CL_LOST : CL_CUR;
+    }
+    i = (i + 1 == nslots) ? 0 : i + 1;
+  }
+  return CL_FULL;
+}
+
+// Settle pass A of a CL_CUR candidate: fold its claim into the slot.
+__device__ __forceinline__ void claimset_store_claim(ClaimEntry* __restrict__ t, uint64_t nslots,
+                                                     uint64_t fp, uint64_t claim) {
+  uint64_t i = bucket_of(fp, nslots);
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    const unsigned long long f = t[i].fp;
+    if (f == fp) {
+      atomicMax(&t[i].nclaim, ~(unsigned long long)claim);
+      return;
+    }
+    if (f == 0ull) return;
+    i = (i + 1 == nslots) ? 0 : i + 1;
+  }
+}
+
 // ~claim stored for fp (0 if absent).  Called in a later kernel than the
 // claims, so every claim is visible.
 __device__ __forceinline__ unsigned long long claimset_get(const ClaimEntry* __restrict__ t,
