@@ -201,16 +201,27 @@ class ShardedModelChecker:
         # (After an error, the partial generated count therefore includes the
         # next level's expansion; TLC's partial counts at an error are not
         # deterministic either, and the error, its level and trace are.)
+        prof = self._prof = {} if os.environ.get("KC_DRIVER_PROFILE") else None
+        tick = time.perf_counter
+
+        def lap(name, t):
+            if prof is not None:
+                prof[name] = prof.get(name, 0.0) + tick() - t
+            return tick()
+
         status_new, status_err = be.init(), NONE_KEY
         widths, level, err = [], 1, NONE_KEY
         rw = rb // 8                                      # record words
         while True:
+            t = tick()
             last = bool(self.cfg.max_levels and level >= self.cfg.max_levels)
             if last:                                      # record the width, expand nothing
                 counts, e1 = [0] * self.world, NONE_KEY
             else:
                 counts, e1 = be.expand()                  # expand `level`
+            t = lap("expand", t)
             M, news, errs = self._gather_status(counts, status_new, status_err)
+            t = lap("gather", t)
             err = min(errs)
             if err != NONE_KEY:                           # found while producing `level`
                 level -= 1
@@ -224,12 +235,15 @@ class ShardedModelChecker:
                 break
             send = self._buffer("_send", max(sum(counts), 1) * rw)
             be.pack(send)
+            t = lap("pack", t)
             recv, nrecv = self._exchange(send, M, rw)
             self._sync()
+            t = lap("exchange", t)
             n_new, e2 = be.insert(recv, nrecv)
             e = min(e1, e2)
             status_new, status_err = n_new, (e if e < NONE_KEY else NONE_KEY)
             be.advance()
+            t = lap("insert", t)
             level += 1
         seconds = time.perf_counter() - t0
         res = be.result()

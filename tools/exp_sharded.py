@@ -35,4 +35,6 @@ for _ in range(a.runs):
         print({k: r[k] for k in ("distinct", "generated", "depth", "error", "complete", "seconds")},
               r.get("error_action"), r.get("error_invariant"), r.get("error_level"), r["level_width"][-5:],
               flush=True)
+        if getattr(mc, "_prof", None):
+            print({k: round(v * 1e3, 1) for k, v in mc._prof.items()}, "ms", flush=True)
 dist.destroy_process_group()
