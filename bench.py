@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
+    ap.add_argument("--fp-count", type=float, default=1e10,
+                    help="fpset workload: fingerprints inserted (and looked up) per step")
+    ap.add_argument("--fp-load", type=float, default=0.5, choices=[0.5, 0.75],
+                    help="fpset workload: table load after the inserts")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded (multi-GPU) stages even at N=1 (run under torch.distributed.run)")
     return ap.parse_args()
@@ -186,24 +190,36 @@ def bench_single(args, kw, desc):
 
 
 def bench_fpset(args):
+    """BASELINE config 4: insert fp_count device-generated fingerprints into a
+    table sized for a final load of fp_load, then look up as many (half
+    present, half absent).  One 64-B HBM burst per random probe is the
+    algorithmic traffic of an insert (the 16-B pair it reads lives in it)."""
     import torch
     import kubecheck
 
-    n = 1 << 30                      # fingerprints inserted per step
+    n = int(args.fp_count)
     batch = 1 << 24
-    s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))   # lands at 50% load
+    cap = int(n / args.fp_load * 3 / 4)   # kc_fpset_create sizes slots = 4/3 * capacity
+    s = None
     for _ in range(args.warmup):
-        s.close()
-        s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))
+        if s is not None:
+            s.close()
+        s = kubecheck.FPSet(capacity=cap)
         s.stress(0x5EED0000, n, batch, n)
     torch.cuda.synchronize()
     tin = tlk = 0.0
     for k in range(args.steps):
-        s.close()
-        s = kubecheck.FPSet(capacity=int(n * 2 * 3 / 4))
+        if s is not None:
+            s.close()
+        s = kubecheck.FPSet(capacity=cap)
         ti, tl, found = s.stress(0x5EED0000 + k, n, batch, n)
+        # 63-bit fingerprints: ~n^2/2^64 genuine duplicates in the stream
+        if not n - n * n / 2**60 - 64 <= s.size() <= n:
+            raise RuntimeError(f"fpset stress: size {s.size()} for {n} inserts")
         tin += ti
         tlk += tl
+    load, table_bytes = s.size() / s.capacity(), s.capacity() * 8
+    s.close()
     gbs = n * args.steps * 64 / tin / 1e9
     return {
         "metric": "FPSet probe HBM GB/s (insert)", "value": round(gbs, 1), "unit": "GB/s",
@@ -211,9 +227,11 @@ def bench_fpset(args):
         "ms_per_step": round(tin * 1e3 / args.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic splitmix64 fingerprints generated on device",
-        "config": {"workload": f"FPSet stress: {n} inserts + {n} lookups at 50% load, batch {batch}",
+        "config": {"workload": f"FPSet stress: {n} inserts + {n} lookups to {load:.0%} load, batch {batch}",
+                   "table_bytes": table_bytes,
                    "inserts_per_s": round(n * args.steps / tin, 1),
-                   "lookups_per_s": round(n * args.steps / tlk, 1)},
+                   "lookups_per_s": round(n * args.steps / tlk, 1),
+                   "lookups_found": int(found)},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "k_stress_insert"},

@@ -80,7 +80,7 @@ int kc_fpset_contains_batch_dev(kc_fpset *s, uint64_t *fps_dev, size_t n, uint8_
                                 void *hip_stream);
 /* Distinct fingerprints stored. */
 uint64_t kc_fpset_size(const kc_fpset *s);
-/* Slot capacity (8 per 64-B bucket). */
+/* Slot capacity (u64 fingerprint slots, linear probing). */
 uint64_t kc_fpset_capacity(const kc_fpset *s);
 /* TLC checkFPs(): the minimum gap between any two stored fingerprints
  * (sorted), from which TLC derives "based on the actual fingerprints"

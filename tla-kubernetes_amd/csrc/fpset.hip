@@ -201,6 +201,14 @@ void DevBatchTable::release() {
 }
 
 // --------------------------------------------------------------- kernels
+// Batch statistics [new, full, found, -] live in STAT_ROWS 64-B rows, one
+// picked per block: a per-wave atomic on one shared address serialises the
+// whole grid (the same effect the engine's striped Counters avoid).
+constexpr int STAT_ROWS = 64;
+constexpr size_t STAT_BYTES = STAT_ROWS * 8 * sizeof(unsigned long long);
+__device__ __forceinline__ unsigned long long* stat_row(unsigned long long* stats) {
+  return stats + (blockIdx.x & (STAT_ROWS - 1)) * 8;
+}
 __global__ void k_normalize(uint64_t* __restrict__ fps, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) fps[i] = normalize_fp(fps[i]);
@@ -226,11 +234,11 @@ __global__ void k_batch_put(const uint64_t* __restrict__ fps, uint64_t n,
     }
     seen[i] = s;
   }
-  // one atomic per wave
+  // one atomic per wave, into this block's stats row
   const unsigned long long bw = __ballot(nw != 0), bf = __ballot(full != 0);
   if ((threadIdx.x & 63) == 0) {
-    if (bw) atomicAdd(&stats[0], (unsigned long long)__popcll(bw));
-    if (bf) atomicAdd(&stats[1], (unsigned long long)__popcll(bf));
+    if (bw) atomicAdd(&stat_row(stats)[0], (unsigned long long)__popcll(bw));
+    if (bf) atomicAdd(&stat_row(stats)[1], (unsigned long long)__popcll(bf));
   }
 }
 __global__ void k_contains(const uint64_t* __restrict__ fps, uint64_t n,
@@ -254,7 +262,7 @@ k_stress_insert(uint64_t seed, uint64_t start, uint64_t n, unsigned long long* _
   unsigned long long nw = 0;
   if (i < n) nw = fpset_insert(slots, nbuckets, normalize_fp(splitmix64(seed + start + i))) == 1;
   const unsigned long long b = __ballot(nw != 0);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stats[0], (unsigned long long)__popcll(b));
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[0], (unsigned long long)__popcll(b));
 }
 // Stress lookup: even i -> an inserted fp, odd i -> one from a second stream.
 __global__ void __launch_bounds__(256)
@@ -269,7 +277,7 @@ k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t n, const unsigned long l
     f = fpset_contains(slots, nbuckets, fp);
   }
   const unsigned long long b = __ballot(f != 0);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stats[2], (unsigned long long)__popcll(b));
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[2], (unsigned long long)__popcll(b));
 }
 __global__ void k_compact_fps(const unsigned long long* __restrict__ slots, uint64_t nslots,
                               unsigned long long* __restrict__ out, unsigned long long* __restrict__ n) {
@@ -294,9 +302,21 @@ struct kc_fpset {
   uint64_t* d_fps = nullptr;
   uint8_t* d_seen = nullptr;
   uint64_t stage_cap = 0;
-  unsigned long long* d_stats = nullptr;  // [new, full, found, spare]
+  unsigned long long* d_stats = nullptr;  // STAT_ROWS rows of [new, full, found, -]
   std::mutex mu;
 };
+
+// Sum the striped stats rows (syncs the stream).
+static int read_stats(kc_fpset* s, hipStream_t st, unsigned long long out[4]) {
+  unsigned long long rows[STAT_ROWS * 8];
+  KC_HIP_TRY(hipMemcpyAsync(rows, s->d_stats, STAT_BYTES, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  for (int k = 0; k < 4; ++k) {
+    out[k] = 0;
+    for (int r = 0; r < STAT_ROWS; ++r) out[k] += rows[r * 8 + k];
+  }
+  return 0;
+}
 
 static int stage(kc_fpset* s, uint64_t n) {
   if (n <= s->stage_cap) return 0;
@@ -322,13 +342,12 @@ static int put_dev(kc_fpset* s, uint64_t* fps, size_t n, uint8_t* seen, hipStrea
   KC_HIP_TRY(hipMemsetAsync(s->bt.t, 0, cap * sizeof(BatchEntry), st));
   hipLaunchKernelGGL(k_batch_claim, dim3(grid), dim3(256), 0, st, fps, (uint64_t)n, s->bt.t, cap - 1);
   KC_TRY(s->fs.reserve(n, st));
-  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, STAT_BYTES, st));
   hipLaunchKernelGGL(k_batch_put, dim3(grid), dim3(256), 0, st, fps, (uint64_t)n, s->bt.t, cap - 1,
                      s->fs.slots, s->fs.nbuckets, seen, s->d_stats);
   KC_HIP_TRY(hipGetLastError());
   unsigned long long stats[4];
-  KC_HIP_TRY(hipMemcpyAsync(stats, s->d_stats, sizeof stats, hipMemcpyDeviceToHost, st));
-  KC_HIP_TRY(hipStreamSynchronize(st));
+  KC_TRY(read_stats(s, st, stats));
   if (stats[1]) {
     set_error("fpset full");
     return -ENOMEM;
@@ -355,7 +374,7 @@ int kc_fpset_create(uint64_t capacity_fps, int device, kc_fpset** out) {
   int rc = 0;
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = -EIO;
   if (!rc) rc = s->fs.init(capacity_fps * 4 / 3 + 8, s->stream);
-  if (!rc && hipMalloc(&s->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess) rc = -ENOMEM;
+  if (!rc && hipMalloc(&s->d_stats, STAT_BYTES) != hipSuccess) rc = -ENOMEM;
   if (!rc && hipStreamSynchronize(s->stream) != hipSuccess) rc = -EIO;
   if (rc) { kc_fpset_destroy(s); if (rc == -EIO) set_error("kc_fpset_create: HIP failure"); return rc; }
   *out = s;
@@ -487,7 +506,7 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   KC_HIP_TRY(hipEventCreate(&e0));
   KC_HIP_TRY(hipEventCreate(&e1));
   KC_HIP_TRY(hipEventCreate(&e2));
-  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, STAT_BYTES, st));
   KC_HIP_TRY(hipEventRecord(e0, st));
   for (uint64_t off = 0; off < n; off += batch) {
     const uint64_t m = std::min(batch, n - off);
@@ -503,8 +522,7 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   KC_HIP_TRY(hipEventRecord(e2, st));
   KC_HIP_TRY(hipGetLastError());
   unsigned long long stats[4];
-  KC_HIP_TRY(hipMemcpyAsync(stats, s->d_stats, sizeof stats, hipMemcpyDeviceToHost, st));
-  KC_HIP_TRY(hipStreamSynchronize(st));
+  KC_TRY(read_stats(s, st, stats));
   float ms1 = 0, ms2 = 0;
   KC_HIP_TRY(hipEventElapsedTime(&ms1, e0, e1));
   KC_HIP_TRY(hipEventElapsedTime(&ms2, e1, e2));

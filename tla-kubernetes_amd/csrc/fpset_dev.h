@@ -55,47 +55,47 @@ __device__ __forceinline__ uint64_t batch_slot(uint64_t fp, uint64_t mask) {
   return (h >> 21) & mask;
 }
 
+// The FPSet is one array of u64 slots (nbuckets * 8 of them; the 64-B
+// "bucket" is only the allocation unit) probed linearly from
+// bucket_of(fp, nslots).  Each probe step reads one aligned 16-B pair, so a
+// lane issues one load per two slots instead of four per eight; at <= 1/2
+// load almost every probe ends inside its first pair.
+//
 // Insert: 1 = newly inserted, 0 = already present, -1 = table full.
 __device__ __forceinline__ int fpset_insert(unsigned long long* __restrict__ slots,
                                             uint64_t nbuckets, uint64_t fp) {
-  uint64_t b = bucket_of(fp, nbuckets);
-  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
-    unsigned long long* bk = slots + b * 8;
-    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(bk);
-    ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
-    unsigned long long e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (e[k] == fp) return 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (e[k] == 0) {
-        const unsigned long long old = atomicCAS(bk + k, 0ull, (unsigned long long)fp);
+  const uint64_t ns = nbuckets * 8;
+  uint64_t i = bucket_of(fp, ns);
+  for (uint64_t probe = 0; probe < ns;) {
+    const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(slots + (i & ~1ull));
+    // slots i (and i+1 when i is even) in probe order
+    for (int k = (int)(i & 1); k < 2; ++k, ++probe) {
+      const unsigned long long e = k ? q.y : q.x;
+      if (e == fp) return 0;
+      if (e == 0ull) {
+        const unsigned long long old = atomicCAS(slots + (i & ~1ull) + k, 0ull, (unsigned long long)fp);
         if (old == 0ull) return 1;
         if (old == fp) return 0;
       }
     }
-    b = (b + 1 == nbuckets) ? 0 : b + 1;
+    i = (i | 1ull) + 1 == ns ? 0 : (i | 1ull) + 1;
   }
   return -1;
 }
 
-// Lookup: 1 = present, 0 = absent.
+// Lookup: 1 = present, 0 = absent (stops at the first empty slot).
 __device__ __forceinline__ int fpset_contains(const unsigned long long* __restrict__ slots,
                                               uint64_t nbuckets, uint64_t fp) {
-  uint64_t b = bucket_of(fp, nbuckets);
-  for (uint64_t probe = 0; probe < nbuckets; ++probe) {
-    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(slots + b * 8);
-    ulonglong2 q0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
-    unsigned long long e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-    bool empty = false;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (e[k] == fp) return 1;
-      empty |= (e[k] == 0);
+  const uint64_t ns = nbuckets * 8;
+  uint64_t i = bucket_of(fp, ns);
+  for (uint64_t probe = 0; probe < ns;) {
+    const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(slots + (i & ~1ull));
+    for (int k = (int)(i & 1); k < 2; ++k, ++probe) {
+      const unsigned long long e = k ? q.y : q.x;
+      if (e == fp) return 1;
+      if (e == 0ull) return 0;
     }
-    if (empty) return 0;
-    b = (b + 1 == nbuckets) ? 0 : b + 1;
+    i = (i | 1ull) + 1 == ns ? 0 : (i | 1ull) + 1;
   }
   return 0;
 }
