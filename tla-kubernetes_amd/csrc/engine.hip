@@ -4,7 +4,7 @@
 //
 // Per level (all on one HIP stream, one host sync per level):
 //   for each chunk of <= chunk_states parents:
-//     k_claim (LDS tile dedup + ClaimSet claims); k_settle (winners);
+//     k_claim (LDS tile dedup + ClaimSet claims); k_settle_rec<0>, <1> (winners);
 //     hipcub exclusive scan; k_emit; k_advance
 //   read {next width, next candidates, error key} back.
 // The frontier buffers are the StateQueue: double-buffered packed states
@@ -40,7 +40,7 @@ const char* kActionNames[A_COUNT] = {
 // chunk_base += (last exclusive offset + last count); cand_total = sum of the
 // next_cand stripes (one 64-lane wave, one stripe per lane)
 __global__ void __launch_bounds__(64)
-k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ cnt, uint64_t n,
+k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask, uint64_t n,
           Counters* __restrict__ C) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
   unsigned long long v = C->s[threadIdx.x].next_cand;
@@ -48,7 +48,7 @@ k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ cnt
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   if (threadIdx.x == 0) {
     C->cand_total = v;
-    if (n > 0) C->chunk_base += (unsigned long long)offsets[n - 1] + cnt[n - 1];
+    if (n > 0) C->chunk_base += (unsigned long long)offsets[n - 1] + NewCount()(newmask[n - 1]);
   }
 }
 
@@ -194,7 +194,6 @@ class EngineT final : public EngineBase {
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
-      KC_TRY(grow_buffer(newcnt_, cnt_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
       // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
@@ -208,35 +207,34 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
           timed(KA_LDS, [&] {
             hipLaunchKernelGGL((k_claim<M, 1>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
           });
           timed(KA_COMPUTE, [&] {
             hipLaunchKernelGGL((k_claim<M, 2>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, d_ctr_);
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
           });
         }
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
-                             d_ctr_);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, newcnt_,
-                             d_ctr_);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
         });
         size_t tmp_bytes = 0;
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt_, offsets_, (int)cn, st_));
+        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)cn, st_));
         KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
         hipError_t scan_err = hipSuccess;
         timed(KK_SCAN, [&] {
-          scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt_, offsets_, (int)cn, st_);
+          scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)cn, st_);
         });
         KC_HIP_TRY(scan_err);
         timed(KK_EMIT, [&] {
@@ -244,7 +242,7 @@ class EngineT final : public EngineBase {
                              flags_, newmask_, offsets_, next_, level_gidx, next_gidx, parent_, ord_,
                              cfg_.keep_trace, d_ctr_);
         });
-        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newcnt_, cn, d_ctr_);
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_);
       }
       KC_HIP_TRY(hipGetLastError());
       KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
@@ -454,7 +452,7 @@ class EngineT final : public EngineBase {
     (void)hipSetDevice(cfg_.device);
     cs_.release();
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
-                    (void*)newcnt_, (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
+                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     for (auto& e : ev_pool_) (void)hipEventDestroy(e);
@@ -469,13 +467,13 @@ class EngineT final : public EngineBase {
   unsigned long long* parent_ = nullptr;
   uint8_t* ord_ = nullptr;
   uint64_t par_cap_ = 0, ord_cap_ = 0;
-  uint32_t *newmask_ = nullptr, *newcnt_ = nullptr, *offsets_ = nullptr;
+  uint32_t *newmask_ = nullptr, *offsets_ = nullptr;
   uint32_t* abl_mask_ = nullptr;
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
   uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;
   uint64_t abl_cap_ = 0;
-  uint64_t mask_cap_ = 0, cnt_cap_ = 0, off_cap_ = 0;
+  uint64_t mask_cap_ = 0, off_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
   Counters* d_ctr_ = nullptr;

@@ -98,25 +98,31 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 //              produce the same state often (diamonds: a-then-b = b-then-a),
 //              so about half of all successors die here without touching HBM.
 //              Then each tile representative claims its fp in the ClaimSet
-//              (one 64-B bucket read; atomics only for current-level fps).
-//              Per tile: the list of candidates that may win
-//              {fp, tile-local key, inserted-here flag}.
-//   k_settle_rec<0>, <1> : the claimants fold their claims into the slots,
-//              then every candidate keeps its successor iff its claim is the
-//              stored minimum -> newmask / newcnt (scan + emit); no successor
-//              is re-derived.
+//              (one 16-B slot read; a CAS only for a new fp).  The lane that
+//              inserts an fp sets its bit in its parent's newmask word (a
+//              provisional win).  A claimant that finds a larger claim
+//              stored (or none yet) is a candidate: per tile, a list of
+//              {fp, tile-local key}.
+//   k_settle_rec<0> : every candidate folds its claim into its slot
+//              (atomicMax).  One that displaces a claim clears the displaced
+//              claim's newmask bit (its parent index and position are the
+//              claim's key) and flags itself a displacer.
+//   k_settle_rec<1> : every displacer wins iff the stored claim is still
+//              its own -> sets its newmask bit.
+// Inserters never re-read their slot: only a displacement can take their
+// win away, and it clears their bit itself.  The scan then runs over
+// popcount(newmask); no successor is re-derived.
 // Tile-local dedup only ever discards a copy whose fp is held by a smaller
 // key of the same tile, which can never be the level minimum; an LDS table
 // overflow just sends the copy to the ClaimSet directly.
 constexpr int CLAIM_TILE = 256;
 constexpr int CLAIM_LDS_BITS = 11;
 constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
-// Candidate records per tile (tile representatives whose claim may win):
-// fp + tile-local key (bit 31: this lane inserted the fp), for the settle
-// passes.  A tile has at most CLAIM_TILE * 32 successors, so the list cannot
-// overflow.
+// Candidate records per tile (claimants whose claim may win): fp + tile-local
+// key (bit 31: set by settle pass A on a displacer).  A tile has at most
+// CLAIM_TILE * 32 successors, so the list cannot overflow.
 constexpr int CLAIM_RCAP = CLAIM_TILE * 32;
-constexpr unsigned int CAND_INSERTER = 1u << 31;
+constexpr unsigned int CAND_DISPLACER = 1u << 31;
 
 __device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t tile,
                                                unsigned long long* __restrict__ rec_fp,
@@ -153,10 +159,10 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-        Counters* __restrict__ C) {
+        uint32_t* __restrict__ newmask, Counters* __restrict__ C) {
   __shared__ unsigned long long sh_fp[CLAIM_LDS];
   __shared__ unsigned int sh_key[CLAIM_LDS];
-  __shared__ unsigned int sh_cur[CLAIM_TILE];
+  __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_rc;
   if (threadIdx.x == 0) sh_rc = 0;
@@ -208,13 +214,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         // LDS table full: claim this copy directly
         ++probes;
         const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | (uint64_t)t), level);
-        if (r >= CL_CUR) {
-          if (r == CL_FULL)
-            atomicAdd(&C->overflow, 1ull);
-          else
-            push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp,
-                           ((threadIdx.x << 5) | (unsigned)t) | (r == CL_NEW ? CAND_INSERTER : 0u));
-        }
+        if (r == CL_NEW)
+          atomicOr(&sh_cur[threadIdx.x], 1u << t);
+        else if (r == CL_CUR)
+          push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
+        else if (r == CL_FULL)
+          atomicAdd(&C->overflow, 1ull);
       }
     }
     if (ABL == 2) sh_cur[threadIdx.x] = (unsigned)acc;
@@ -233,15 +238,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const uint64_t pidx = base + tile0 + lp;
     ++probes;
     const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | t), level);
-    if (r >= CL_CUR) {
-      if (r == CL_FULL)
-        atomicAdd(&C->overflow, 1ull);
-      else
-        push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk | (r == CL_NEW ? CAND_INSERTER : 0u));
-    }
+    if (r == CL_NEW)
+      atomicOr(&sh_cur[lp], 1u << t);
+    else if (r == CL_CUR)
+      push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk);
+    else if (r == CL_FULL)
+      atomicAdd(&C->overflow, 1ull);
   }
   __syncthreads();
   if (threadIdx.x == 0) rcount[blockIdx.x] = sh_rc;
+  if (live) newmask[i] = sh_cur[threadIdx.x];
   unsigned long long pw = probes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
@@ -251,48 +257,56 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 }
 
 // k_settle_rec<PASS>: one workgroup per claim tile (STORE-claim protocol,
-// fpset_dev.h).  PASS 0: every claimant candidate folds its claim into its
-// slot with atomicMax.  PASS 1 (a later launch): every candidate, inserter or
-// claimant, wins iff the stored claim is its own -> newmask / newcnt.  No
-// successor is re-derived.
+// fpset_dev.h).  PASS 0: every candidate folds its claim into its slot; one
+// that lowers the stored claim clears the displaced claim's newmask bit and
+// flags itself.  PASS 1 (a later launch): every displacer whose claim is
+// still the stored one sets its newmask bit.  Displaced claims always belong
+// to this chunk: earlier chunks' claims are smaller and final.
 template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
              uint32_t level, const unsigned int* __restrict__ rcount,
-             const unsigned long long* __restrict__ rec_fp, const unsigned int* __restrict__ rec_lk,
-             uint32_t* __restrict__ newmask, uint32_t* __restrict__ newcnt, Counters* __restrict__ C) {
-  __shared__ unsigned int sh_new[CLAIM_TILE];
+             const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C) {
   const unsigned int cnt = rcount[blockIdx.x];
-  if (PASS == 1) sh_new[threadIdx.x] = 0;
-  __syncthreads();
   const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
   unsigned reads = 0;
   for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
     const uint64_t r = (uint64_t)blockIdx.x * CLAIM_RCAP + k;
     const unsigned int lk = rec_lk[r];
-    if (PASS == 0 && (lk & CAND_INSERTER)) continue;
+    if (PASS == 1 && !(lk & CAND_DISPLACER)) continue;
     const unsigned long long fp = rec_fp[r];
     const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
     const uint64_t claim = make_claim(level, ((base + tile0 + lp) << 8) | t);
     ++reads;
     if (PASS == 0) {
-      claimset_store_claim(cs, nbuckets, fp, claim);
+      const unsigned long long prev = claimset_store_claim(cs, nbuckets, fp, claim);
+      if (prev < ~claim) {                       // displaced ~prev (or found no claim)
+        const uint64_t pkey = (~prev) & ((1ull << CLAIM_KEY_BITS) - 1);
+        const uint64_t pp = (pkey >> 8) - base;
+        if (prev == 0ull || ((~prev) >> CLAIM_KEY_BITS) != level || pp >= n) {
+          atomicAdd(&C->overflow, 1ull);         // protocol violation: fail loudly
+        } else {
+          atomicAnd(&newmask[pp], ~(1u << (pkey & 31)));
+          rec_lk[r] = lk | CAND_DISPLACER;
+        }
+      }
     } else if (~claimset_get(cs, nbuckets, fp) == claim) {
-      atomicOr(&sh_new[lp], 1u << t);
+      atomicOr(&newmask[tile0 + lp], 1u << t);
     }
-  }
-  if (PASS == 0) return;
-  __syncthreads();
-  const uint64_t i = tile0 + threadIdx.x;
-  if (i < n) {
-    newmask[i] = sh_new[threadIdx.x];
-    newcnt[i] = (uint32_t)__popc(sh_new[threadIdx.x]);
   }
   unsigned long long rw = reads;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
   if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
 }
+
+// popcount(newmask): the scan's input (new states per parent)
+struct NewCount {
+  __host__ __device__ __forceinline__ uint32_t operator()(uint32_t m) const {
+    return (uint32_t)__builtin_popcount(m);
+  }
+};
 
 template <class M>
 __global__ void __launch_bounds__(256)

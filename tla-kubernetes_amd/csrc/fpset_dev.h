@@ -170,6 +170,8 @@ __device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64
 //     minimum over the inserter and all candidates;
 //   settle pass B (next kernel) — every candidate and inserter wins iff the
 //     stored claim is its own.
+// The engine keeps the winners as per-parent bit masks and so re-reads only
+// the displacers (engine_kernels.h, k_claim / k_settle_rec).
 // Stale copies in another XCD's L2 can only show a slot empty or its claim
 // word 0, which makes a lane a candidate (conservative); the CAS result is
 // authoritative for the fp.
@@ -198,18 +200,19 @@ __device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, 
 }
 
 // Settle pass A of a CL_CUR candidate: fold its claim into the slot.
-__device__ __forceinline__ void claimset_store_claim(ClaimEntry* __restrict__ t, uint64_t nslots,
-                                                     uint64_t fp, uint64_t claim) {
+// Returns the ~claim the slot held before (0 if fp is absent, which the
+// protocol never produces).
+__device__ __forceinline__ unsigned long long claimset_store_claim(ClaimEntry* __restrict__ t,
+                                                                   uint64_t nslots, uint64_t fp,
+                                                                   uint64_t claim) {
   uint64_t i = bucket_of(fp, nslots);
   for (uint64_t probe = 0; probe < nslots; ++probe) {
     const unsigned long long f = t[i].fp;
-    if (f == fp) {
-      atomicMax(&t[i].nclaim, ~(unsigned long long)claim);
-      return;
-    }
-    if (f == 0ull) return;
+    if (f == fp) return atomicMax(&t[i].nclaim, ~(unsigned long long)claim);
+    if (f == 0ull) return 0ull;
     i = (i + 1 == nslots) ? 0 : i + 1;
   }
+  return 0ull;
 }
 
 // ~claim stored for fp (0 if absent).  Called in a later kernel than the
