@@ -153,8 +153,11 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
 
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
 // KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only.
+// Occupancy: the LDS table (24 KB) allows 6 workgroups = 6 waves per SIMD;
+// the claims are latency-bound random probes, so the register budget is
+// pinned to match (one wave less measured +15 ms per NP=2 check).
 template <class M, int ABL = 0>
-__global__ void __launch_bounds__(CLAIM_TILE)
+__global__ void __launch_bounds__(CLAIM_TILE) __attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,

@@ -629,31 +629,40 @@ struct Model {
   // 64-bit fingerprint of the canonical packed words, normalised the way the
   // FPSet stores it: MSB clear (TLC's disk FPSets reserve it), never 0.
   //
-  // Zobrist-style: fp = final(XOR_k mix(w_k, k)), every mix and the final
-  // step a bijection of 64-bit words (xor-shifts and odd multiplies).  A
-  // successor differs from its parent in at most three words — apiState, the
-  // acting process's word and that process's listRequests.objs word — so the
-  // kernels fold the parent once and re-mix only the changed words
-  // (fingerprint_succ); two states collide only if the XOR of their words'
-  // mix differences vanishes (probability ~2^-64 per pair, as for TLC's
-  // polynomial FP64, which is also linear over GF(2)).
-  KC_HD static uint64_t word_mix(uint64_t w, int k) {
-    uint64_t z = w ^ (0x6a09e667f3bcc909ull + (uint64_t)k * 0x9e3779b97f4a7c15ull);
+  // Zobrist-style: fp = final(XOR_k mix(w_k, k)), every mix a bijection of
+  // 64-bit words (xor-shifts and odd multiplies) and final() only the
+  // normalisation (a further bijective finaliser could not change which
+  // states collide, and the XOR of mixes is already uniform in every bit).
+  // A successor differs from its parent in at most three words — apiState,
+  // the acting process's word and that process's listRequests.objs word — so
+  // the kernels fold the parent once and re-mix only the changed words of
+  // each successor (fingerprint_succ); two states collide
+  // only if the XOR of their words' mix differences vanishes (probability
+  // ~2^-63 per pair, as for TLC's polynomial FP64, which is also linear over
+  // GF(2)).  64-bit multiplies are quarter-rate on CDNA, so this matters.
+  static constexpr uint64_t salt_c(int k) {
+    return 0x6a09e667f3bcc909ull + (uint64_t)k * 0x9e3779b97f4a7c15ull;
+  }
+  KC_HD static uint64_t salt(int k) {          // runtime k: a select, no multiply
+    uint64_t r = salt_c(0);
+#pragma unroll
+    for (int i = 1; i < W_RAW; ++i) r = (k == i) ? salt_c(i) : r;
+    return r;
+  }
+  KC_HD static uint64_t mix_salted(uint64_t z) {
     z *= 0xbf58476d1ce4e5b9ull;
     z ^= z >> 31;
     z *= 0x94d049bb133111ebull;
     return z ^ (z >> 29);
   }
+  KC_HD static uint64_t word_mix(uint64_t w, int k) { return mix_salted(w ^ salt(k)); }
   KC_HD static uint64_t fp_fold(const State& s) {
     uint64_t x = 0;
 #pragma unroll
-    for (int i = 0; i < W_RAW; ++i) x ^= word_mix(s.w[i], i);
+    for (int i = 0; i < W_RAW; ++i) x ^= mix_salted(s.w[i] ^ salt_c(i));
     return x;
   }
   KC_HD static uint64_t fp_final(uint64_t h) {
-    h ^= h >> 33; h *= 0xff51afd7ed558ccdull;
-    h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
-    h ^= h >> 33;
     h &= 0x7fffffffffffffffull;
     return h ? h : 1;
   }
@@ -661,10 +670,12 @@ struct Model {
 
   // Fingerprint of successor x of s, given s's fold and the process `who`
   // whose word the action rewrote (apply's out-parameter).  Equal to
-  // fingerprint(x).
+  // fingerprint(x).  (Caching the parent's per-word mixes instead of
+  // re-mixing the old words costs 15 VGPRs, one wave per SIMD of k_claim's
+  // occupancy, and measured slower.)
   KC_HD static uint64_t fingerprint_succ(const State& s, uint64_t fold_s, const State& x, int who) {
     uint64_t h = fold_s;
-    if (x.w[0] != s.w[0]) h ^= word_mix(s.w[0], 0) ^ word_mix(x.w[0], 0);
+    if (x.w[0] != s.w[0]) h ^= mix_salted(s.w[0] ^ salt_c(0)) ^ mix_salted(x.w[0] ^ salt_c(0));
     {
       uint64_t o = s.w[1], nw = x.w[1];
 #pragma unroll
@@ -675,7 +686,10 @@ struct Model {
         o = (who == k) ? vo : o;
         nw = (who == k) ? vn : nw;
       }
-      if (o != nw) h ^= word_mix(o, 1 + who) ^ word_mix(nw, 1 + who);
+      if (o != nw) {
+        const uint64_t sl = salt(1 + who);
+        h ^= mix_salted(o ^ sl) ^ mix_salted(nw ^ sl);
+      }
     }
     {
       const int wi = 1 + A + who / OBJ_PER_WORD;
@@ -688,7 +702,10 @@ struct Model {
         o = (wi == 1 + A + k) ? vo : o;
         nw = (wi == 1 + A + k) ? vn : nw;
       }
-      if (o != nw) h ^= word_mix(o, wi) ^ word_mix(nw, wi);
+      if (o != nw) {
+        const uint64_t sl = salt(wi);
+        h ^= mix_salted(o ^ sl) ^ mix_salted(nw ^ sl);
+      }
     }
     return fp_final(h);
   }
