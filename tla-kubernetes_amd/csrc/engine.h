@@ -13,7 +13,7 @@ namespace kc {
 enum KernelKind { KK_EXPAND = 0, KK_RESOLVE = 1, KK_SCAN = 2, KK_EMIT = 3, KK_COUNT = 4 };
 // diagnostic-only ablation timings (KC_ABLATE=1 in the environment): extra
 // launches of cut-down k_claim variants on scratch buffers, printed to stderr
-enum AblateKind { KA_LDS = KK_COUNT, KA_COMPUTE = KK_COUNT + 1, KA_TOTAL = KK_COUNT + 2 };
+enum AblateKind { KA_LDS = KK_COUNT, KA_COMPUTE = KK_COUNT + 1, KA_PLAN = KK_COUNT + 2, KA_TOTAL = KK_COUNT + 3 };
 
 class EngineBase {
  public:

@@ -152,7 +152,8 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
 }
 
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
-// KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only.
+// KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only,
+// 3 = plan + fold only (no successor).
 // Occupancy: the LDS table (24 KB) allows 6 workgroups = 6 waves per SIMD;
 // the claims are latency-bound random probes, so the register budget is
 // pinned to match (one wave less measured +15 ms per NP=2 check).
@@ -201,7 +202,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       if (ABL == 0) atomicAdd(&C->overflow, 1ull);
       tot = M::MAXSUCC;
     }
-    uint64_t acc = 0;
+    uint64_t acc = fold ^ pl.counts;
+    if (ABL == 3) tot = 0;
     for (int t = 0; t < tot; ++t) {
       int slot, j;
       M::locate(pl, t, slot, j);
@@ -225,7 +227,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
           atomicAdd(&C->overflow, 1ull);
       }
     }
-    if (ABL == 2) sh_cur[threadIdx.x] = (unsigned)acc;
+    if (ABL >= 2) sh_cur[threadIdx.x] = (unsigned)acc;
   }
   __syncthreads();
   if (ABL != 0) {

@@ -185,7 +185,9 @@ __device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, 
     if (f == 0ull) {
       f = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
       if (f == 0ull) {
-        t[i].nclaim = nc;
+        // agent-scope store: written through this XCD's L2, so claimants on
+        // other XCDs see the claim (and lose at once) instead of a 0 word
+        __hip_atomic_store(&t[i].nclaim, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return CL_NEW;
       }
       seen = 0ull;
