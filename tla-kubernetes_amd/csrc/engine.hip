@@ -207,31 +207,31 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
           timed(KA_LDS, [&] {
             hipLaunchKernelGGL((k_claim<M, 1>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
           });
           timed(KA_COMPUTE, [&] {
             hipLaunchKernelGGL((k_claim<M, 2>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
           });
           timed(KA_PLAN, [&] {
             hipLaunchKernelGGL((k_claim<M, 3>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
           });
         }
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
         });
         size_t tmp_bytes = 0;
         const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());

@@ -40,7 +40,8 @@ struct Counters {
   unsigned long long overflow;    // states with > MAXSUCC successors, full tables
   unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
   unsigned long long cand_total;  // sum of the next_cand stripes (k_advance)
-  unsigned long long head_pad[11];
+  unsigned long long level_new;   // sharded insert: new states of the level (local + records)
+  unsigned long long head_pad[10];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -62,8 +63,8 @@ struct Counters {
   }
 };
 // bytes of the per-level head (err_key, chunk_base, overflow, batch_used,
-// cand_total): what the host reads back after every level
-constexpr size_t kCtrHead = 5 * sizeof(unsigned long long);
+// cand_total, level_new): what the host reads back after every level
+constexpr size_t kCtrHead = 6 * sizeof(unsigned long long);
 __device__ __forceinline__ CtrStripe& stripe(Counters* C) {
   return C->s[blockIdx.x & (CTR_STRIPES - 1)];
 }
@@ -151,29 +152,53 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
   return -1;
 }
 
+// Fingerprint-owner sharding (shard.hip, SH = true): a rank claims only the
+// fingerprints it owns, owner(fp) = floor(fp * R / 2^63); every other tile
+// representative is marked in repmask and counted per owner for the record
+// exchange.  Claim keys carry the rank above the parent index.
+constexpr int CLAIM_RANK_SHIFT = 40;
+struct ShardArgs {
+  uint32_t world = 1, rank = 0;
+  uint32_t* repmask = nullptr;   // [n]: remote representatives of each parent
+  uint32_t* cnt = nullptr;       // [world][n]: remote representatives per owner and parent
+};
+__device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
+  return (uint32_t)__umul64hi(fp << 1, (uint64_t)world);
+}
+
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
 // KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only,
 // 3 = plan + fold only (no successor).
 // Occupancy: the LDS table (24 KB) allows 6 workgroups = 6 waves per SIMD;
 // the claims are latency-bound random probes, so the register budget is
 // pinned to match (one wave less measured +15 ms per NP=2 check).
-template <class M, int ABL = 0>
+template <class M, int ABL = 0, bool SH = false>
 __global__ void __launch_bounds__(CLAIM_TILE) __attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-        uint32_t* __restrict__ newmask, Counters* __restrict__ C) {
+        uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh) {
   __shared__ unsigned long long sh_fp[CLAIM_LDS];
   __shared__ unsigned int sh_key[CLAIM_LDS];
   __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_rc;
+  // SH only (dynamic LDS): remote representatives per parent, then their
+  // counts per owner packed 4 owners x 8 bits per word (a parent has <= 32)
+  extern __shared__ unsigned int sh_dyn[];
+  unsigned int* sh_rep = sh_dyn;
+  unsigned int* sh_cnt = sh_dyn + CLAIM_TILE;
   if (threadIdx.x == 0) sh_rc = 0;
   for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
     sh_fp[k] = 0ull;
     sh_key[k] = ~0u;
   }
+  if (SH) {
+    sh_rep[threadIdx.x] = 0;
+    for (uint32_t k = threadIdx.x; k < ((sh.world + 3) / 4) * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
+  }
+  const uint64_t kbase = SH ? ((uint64_t)sh.rank << CLAIM_RANK_SHIFT) : 0ull;
   sh_cur[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
@@ -216,9 +241,17 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         continue;
       }
       if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
-        // LDS table full: claim this copy directly
+        // LDS table full: claim (or send) this copy directly
+        if (SH) {
+          const uint32_t o = owner_of(fp, sh.world);
+          if (o != sh.rank) {
+            atomicOr(&sh_rep[threadIdx.x], 1u << t);
+            atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + threadIdx.x], 1u << (8 * (o & 3)));
+            continue;
+          }
+        }
         ++probes;
-        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | (uint64_t)t), level);
+        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | (uint64_t)t), level);
         if (r == CL_NEW)
           atomicOr(&sh_cur[threadIdx.x], 1u << t);
         else if (r == CL_CUR)
@@ -241,8 +274,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const unsigned int lk = sh_key[k];
     const unsigned int lp = lk >> 5, t = lk & 31;
     const uint64_t pidx = base + tile0 + lp;
+    if (SH) {
+      const uint32_t o = owner_of(fp, sh.world);
+      if (o != sh.rank) {
+        atomicOr(&sh_rep[lp], 1u << t);
+        atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + lp], 1u << (8 * (o & 3)));
+        continue;
+      }
+    }
     ++probes;
-    const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, (pidx << 8) | t), level);
+    const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level);
     if (r == CL_NEW)
       atomicOr(&sh_cur[lp], 1u << t);
     else if (r == CL_CUR)
@@ -253,6 +294,11 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   __syncthreads();
   if (threadIdx.x == 0) rcount[blockIdx.x] = sh_rc;
   if (live) newmask[i] = sh_cur[threadIdx.x];
+  if (SH && live) {
+    sh.repmask[i] = sh_rep[threadIdx.x];
+    for (uint32_t o = 0; o < sh.world; ++o)
+      sh.cnt[(uint64_t)o * n + i] = (sh_cnt[(o >> 2) * CLAIM_TILE + threadIdx.x] >> (8 * (o & 3))) & 0xffu;
+  }
   unsigned long long pw = probes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
@@ -261,18 +307,43 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
 }
 
+// A claim displaced the stored ~prev in settle pass A: clear the displaced
+// claim's newmask bit when it is this rank's (parent index - base, position),
+// and flag the displacer (*flag_at = flag_val).
+__device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_t level, uint32_t rank,
+                                                uint64_t base, uint64_t n, uint32_t* __restrict__ newmask,
+                                                Counters* __restrict__ C, unsigned int* flag_at,
+                                                unsigned int flag_val) {
+  const uint64_t pkey = (~prev) & ((1ull << CLAIM_KEY_BITS) - 1);
+  if (prev == 0ull || ((~prev) >> CLAIM_KEY_BITS) != level) {
+    atomicAdd(&C->overflow, 1ull);               // protocol violation: fail loudly
+    return;
+  }
+  if ((uint32_t)(pkey >> CLAIM_RANK_SHIFT) == rank) {
+    const uint64_t pp = ((pkey >> 8) & 0xffffffffull) - base;
+    if (pp >= n) {
+      atomicAdd(&C->overflow, 1ull);
+      return;
+    }
+    atomicAnd(&newmask[pp], ~(1u << (pkey & 31)));
+  }
+  *flag_at = flag_val;
+}
+
 // k_settle_rec<PASS>: one workgroup per claim tile (STORE-claim protocol,
 // fpset_dev.h).  PASS 0: every candidate folds its claim into its slot; one
 // that lowers the stored claim clears the displaced claim's newmask bit and
 // flags itself.  PASS 1 (a later launch): every displacer whose claim is
 // still the stored one sets its newmask bit.  Displaced claims always belong
-// to this chunk: earlier chunks' claims are smaller and final.
+// to this chunk: earlier chunks' claims are smaller and final.  Sharded: a
+// displaced claim of another rank (a received record's) has no bit here;
+// records re-read their claims themselves (shard.hip).
 template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
              uint32_t level, const unsigned int* __restrict__ rcount,
              const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C) {
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank) {
   const unsigned int cnt = rcount[blockIdx.x];
   const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
   unsigned reads = 0;
@@ -282,20 +353,13 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
     if (PASS == 1 && !(lk & CAND_DISPLACER)) continue;
     const unsigned long long fp = rec_fp[r];
     const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
-    const uint64_t claim = make_claim(level, ((base + tile0 + lp) << 8) | t);
+    const uint64_t claim =
+        make_claim(level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | ((base + tile0 + lp) << 8) | t);
     ++reads;
     if (PASS == 0) {
       const unsigned long long prev = claimset_store_claim(cs, nbuckets, fp, claim);
-      if (prev < ~claim) {                       // displaced ~prev (or found no claim)
-        const uint64_t pkey = (~prev) & ((1ull << CLAIM_KEY_BITS) - 1);
-        const uint64_t pp = (pkey >> 8) - base;
-        if (prev == 0ull || ((~prev) >> CLAIM_KEY_BITS) != level || pp >= n) {
-          atomicAdd(&C->overflow, 1ull);         // protocol violation: fail loudly
-        } else {
-          atomicAnd(&newmask[pp], ~(1u << (pkey & 31)));
-          rec_lk[r] = lk | CAND_DISPLACER;
-        }
-      }
+      if (prev < ~claim)                         // displaced ~prev (or found no claim)
+        settle_displace(prev, level, rank, base, n, newmask, C, &rec_lk[r], lk | CAND_DISPLACER);
     } else if (~claimset_get(cs, nbuckets, fp) == claim) {
       atomicOr(&newmask[tile0 + lp], 1u << t);
     }

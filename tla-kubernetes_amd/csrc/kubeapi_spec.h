@@ -638,8 +638,8 @@ struct Model {
   // the kernels fold the parent once and re-mix only the changed words of
   // each successor (fingerprint_succ); two states collide
   // only if the XOR of their words' mix differences vanishes (probability
-  // ~2^-63 per pair, as for TLC's polynomial FP64, which is also linear over
-  // GF(2)).  64-bit multiplies are quarter-rate on CDNA, so this matters.
+  // ~2^-59 per pair within an owner class, below; TLC's polynomial FP64 is
+  // also linear over GF(2)).  64-bit multiplies are quarter-rate on CDNA, so this matters.
   static constexpr uint64_t salt_c(int k) {
     return 0x6a09e667f3bcc909ull + (uint64_t)k * 0x9e3779b97f4a7c15ull;
   }
@@ -662,11 +662,31 @@ struct Model {
     for (int i = 0; i < W_RAW; ++i) x ^= mix_salted(s.w[i] ^ salt_c(i));
     return x;
   }
-  KC_HD static uint64_t fp_final(uint64_t h) {
-    h &= 0x7fffffffffffffffull;
+  // Owner bits.  Fingerprint-owner sharding (shard.hip) gives a state to
+  // rank floor(fp * R / 2^63), i.e. to the fingerprint's top bits.  Those
+  // OWNER_BITS bits are a hash of a projection of the state — apiState and
+  // the first PVC controller's word — not of the whole state: 97% of all
+  // actions leave apiState alone and an action changes one process's word,
+  // so about 2/3 of successors keep their parent's owner (measured on the
+  // NP=2 model, levels 1-38) and siblings stay together for the LDS tile
+  // dedup, while the classes still spread evenly over 8 ranks (max/mean
+  // 1.10).  For R dividing 2^OWNER_BITS the owner depends on these bits
+  // only.  The other 59 bits are the Zobrist fold, so two states collide
+  // only if their projections hash alike and 59 fold bits agree.
+  static constexpr int OWNER_BITS = 4;
+  static constexpr int OWNER_WORD = 1 + (NP > 0 ? NC : 0);   // first PVC controller (else client)
+  KC_HD static uint64_t owner_hash(uint64_t w0, uint64_t wo) {
+    uint64_t z = w0 * 0x9e3779b97f4a7c15ull + wo;
+    z ^= z >> 31;
+    z *= 0xbf58476d1ce4e5b9ull;
+    return z >> (64 - OWNER_BITS);
+  }
+  KC_HD static uint64_t fp_final(uint64_t h, const State& x) {
+    h = (h & ((1ull << (63 - OWNER_BITS)) - 1)) |
+        (owner_hash(x.w[0], x.w[OWNER_WORD]) << (63 - OWNER_BITS));
     return h ? h : 1;
   }
-  KC_HD static uint64_t fingerprint(const State& s) { return fp_final(fp_fold(s)); }
+  KC_HD static uint64_t fingerprint(const State& s) { return fp_final(fp_fold(s), s); }
 
   // Fingerprint of successor x of s, given s's fold and the process `who`
   // whose word the action rewrote (apply's out-parameter).  Equal to
@@ -707,7 +727,7 @@ struct Model {
         h ^= mix_salted(o ^ sl) ^ mix_salted(nw ^ sl);
       }
     }
-    return fp_final(h);
+    return fp_final(h, x);
   }
 
   // ------------------------------------------------ canonical tuple (ABI)

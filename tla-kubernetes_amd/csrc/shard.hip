@@ -4,22 +4,28 @@
 //
 // owner(fp) = floor(fp * R / 2^63) (fps are uniform in [1, 2^63)), the top
 // bits of the fingerprint as in TLC's MultiFPSet [ext-TLC].  Per level:
-//   expand : k_shard_count — LDS tile dedup of each 256-parent tile's
-//            successors (as k_claim), per-parent mask of the tile
-//            representatives and their count per owner; generated counters,
-//            Assert/deadlock keys — then one exclusive scan per owner
-//   pack   : k_shard_pack writes records {state, fp, key} into the caller's
-//            send buffer, grouped by owner, each group in (parent, t) order
+//   expand : the engine's k_claim in shard mode (engine_kernels.h): LDS tile
+//            dedup, then every tile representative this rank owns claims its
+//            fp in the local ClaimSet shard (STORE-claim + newmask protocol);
+//            the others are marked and counted per owner -> one exclusive
+//            scan over the owner-major count matrix
+//   pack   : k_shard_pack writes one record per remote representative
+//            {state words, key} into the caller's send buffer, grouped by
+//            owner, each group in (parent, t) order
 //   (all-to-all by the caller)
-//   insert : received records claim their fp in this rank's ClaimSet shard
-//            (k_shard_claim), candidates re-read their claim (k_shard_settle),
-//            and the winners are compacted in record order (= key order) into
-//            the next frontier with parent keys (TLC trace file), invariant
-//            checks and counters (k_shard_emit)
+//   insert : received records claim their fp in the same ClaimSet
+//            (k_rec_claim, same protocol), then settle pass A (local and
+//            record candidates fold their claims; a displaced local claim
+//            loses its newmask bit), pass B (local displacers, record
+//            inserters and displacers re-read their claim), two scans, and
+//            the emit of the winners — this rank's own successors first (in
+//            parent order), then the records' (in receive order) — with parent
+//            keys (TLC trace file), invariant checks and counters.
+// With R = 1 nothing is sent and the level is the single-GPU engine's.
 // Keys: rank << 60 | parent index << 16 | successor position << 8 | low byte
-// (action id in records, ErrKind in error keys); the ClaimSet claim orders
-// them by (rank, parent, position), so the same minimum is taken everywhere
-// and the result does not depend on arrival order.
+// (action id in records and parent keys, ErrKind in error keys); the
+// ClaimSet claim orders them by (rank, parent, position), so the same minimum
+// is taken everywhere and the result does not depend on arrival order.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -37,83 +43,37 @@ namespace kc {
 
 constexpr uint64_t KEY_INIT = 0xFull << 60;   // parent key of an Init state (| init index)
 
-__device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
-  return (uint32_t)__umul64hi(fp << 1, (uint64_t)world);
-}
-
+// A record: the successor's W_RAW canonical words, then its key, padded to a
+// multiple of 16 B (48 B for NP = 2).  The receiver recomputes the
+// fingerprint instead of receiving it.
 template <class M>
 struct Record {
-  uint64_t w[M::W];
-  uint64_t fp;
-  uint64_t key;
+  static constexpr int RW = (M::W_RAW + 2) & ~1;
+  uint64_t w[RW];
 };
-
 template <class M>
-__global__ void __launch_bounds__(CLAIM_TILE)
-k_shard_count(const typename M::State* __restrict__ cur, uint64_t n, Flags f, int check_deadlock,
-              uint32_t world, uint32_t* __restrict__ cnt /* [world][n] */,
-              uint32_t* __restrict__ repmask, Counters* __restrict__ C) {
-  __shared__ unsigned long long sh_fp[CLAIM_LDS];
-  __shared__ unsigned int sh_key[CLAIM_LDS];
-  __shared__ unsigned int sh_rep[CLAIM_TILE];
-  extern __shared__ unsigned int sh_cnt[];           // [owner][parent in tile], world * 256
-  __shared__ unsigned int sh_act[A_COUNT];
-  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
-    sh_fp[k] = 0ull;
-    sh_key[k] = ~0u;
-  }
-  for (uint32_t k = threadIdx.x; k < world * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
-  sh_rep[threadIdx.x] = 0;
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * CLAIM_TILE + threadIdx.x;
-  if (i < n) {
-    const typename M::State s = load_state<M>(cur, i);
-    const typename M::Plan pl = M::plan(s, f);
-    const uint64_t fold = M::fp_fold(s);
-    if (pl.fail_pos >= 0)
-      atomicMin(&C->err_key, (i << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
-    else if (pl.total == 0 && check_deadlock)
-      atomicMin(&C->err_key, (i << 16) | E_DEADLOCK);
+__device__ __forceinline__ void load_record(const Record<M>* __restrict__ in, uint64_t i,
+                                            typename M::State& x, uint64_t& key) {
+  const ulonglong2* v = reinterpret_cast<const ulonglong2*>(in + i);
+  uint64_t r[Record<M>::RW];
 #pragma unroll
-    for (int slot = 0; slot < M::NSLOT; ++slot) {       // per-action "generated"
-      const int c = (int)((pl.counts >> (6 * slot)) & 63);
-      if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
-    }
-    int tot = pl.total;
-    if (tot > M::MAXSUCC) {
-      atomicAdd(&C->overflow, 1ull);
-      tot = M::MAXSUCC;
-    }
-    for (int t = 0; t < tot; ++t) {
-      int slot, j;
-      M::locate(pl, t, slot, j);
-      typename M::State x;
-      int who;
-      M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
-      if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0) {
-        // LDS table full: this copy is sent as its own representative
-        atomicOr(&sh_rep[threadIdx.x], 1u << t);
-        atomicAdd(&sh_cnt[owner_of(fp, world) * CLAIM_TILE + threadIdx.x], 1u);
-      }
-    }
+  for (int k = 0; k < Record<M>::RW / 2; ++k) {
+    const ulonglong2 q = v[k];
+    r[2 * k] = q.x;
+    r[2 * k + 1] = q.y;
   }
-  __syncthreads();
-  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
-    const unsigned long long fp = sh_fp[k];
-    if (!fp) continue;
-    const unsigned int lk = sh_key[k];
-    atomicOr(&sh_rep[lk >> 5], 1u << (lk & 31));
-    atomicAdd(&sh_cnt[owner_of(fp, world) * CLAIM_TILE + (lk >> 5)], 1u);
-  }
-  __syncthreads();
-  if (i < n) {
-    repmask[i] = sh_rep[threadIdx.x];
-    for (uint32_t o = 0; o < world; ++o) cnt[(uint64_t)o * n + i] = sh_cnt[o * CLAIM_TILE + threadIdx.x];
-  }
-  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+#pragma unroll
+  for (int k = 0; k < M::W; ++k) x.w[k] = k < M::W_RAW ? r[k] : 0ull;
+  key = r[M::W_RAW];
+}
+template <class M>
+__device__ __forceinline__ uint64_t record_key(const Record<M>* __restrict__ in, uint64_t i) {
+  return in[i].w[M::W_RAW];
+}
+
+// claim order key of a record key: (rank, parent index, successor position)
+__device__ __forceinline__ uint64_t record_ckey(uint64_t key) {
+  return ((key >> 60) << CLAIM_RANK_SHIFT) | (((key >> 16) & 0xffffffffull) << 8) | ((key >> 8) & 0xff);
 }
 
 template <class M>
@@ -144,11 +104,13 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
     for (uint32_t k = 0; k < 16; ++k)
       if (k == o) { r = c[k]; c[k] = r + 1; }
     const uint64_t pos = (uint64_t)off[(uint64_t)o * n + i] + r;   // owner-major scan
-    Record<M>* rec = out + pos;
+    uint64_t w[Record<M>::RW];
 #pragma unroll
-    for (int k = 0; k < M::W; ++k) rec->w[k] = x.w[k];
-    rec->fp = fp;
-    rec->key = (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot);
+    for (int k = 0; k < Record<M>::RW; ++k) w[k] = k < M::W_RAW ? x.w[k] : 0ull;
+    w[M::W_RAW] = (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot);
+    ulonglong2* v = reinterpret_cast<ulonglong2*>(out + pos);
+#pragma unroll
+    for (int k = 0; k < Record<M>::RW / 2; ++k) v[k] = make_ulonglong2(w[2 * k], w[2 * k + 1]);
   }
 }
 
@@ -162,41 +124,133 @@ __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t*
   tot[o] = end - off[(uint64_t)o * n];
 }
 
-// claim order key of a record: (rank, parent index, successor position)
-__device__ __forceinline__ uint64_t record_ckey(uint64_t key) {
-  return ((key >> 60) << 40) | (((key >> 16) & 0xffffffffull) << 8) | ((key >> 8) & 0xff);
-}
+// Record flags: 0 = out, 1 = candidate, 2 = inserted its fp, 3 = displacer.
+enum : unsigned int { RF_OUT = 0, RF_CAND = 1, RF_INSERTER = 2, RF_DISPLACER = 3 };
 
 template <class M>
 __global__ void __launch_bounds__(256)
-k_shard_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
-              uint64_t nslots, uint32_t level, uint32_t* __restrict__ cand,
-              Counters* __restrict__ C) {
+k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
+            uint64_t nslots, uint32_t level, unsigned long long* __restrict__ rfp,
+            unsigned int* __restrict__ flag, Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long probes = 0;
+  if (i < n) {
+    typename M::State x;
+    uint64_t key;
+    load_record<M>(in, i, x, key);
+    const uint64_t fp = M::fingerprint(x);
+    rfp[i] = fp;
+    const int r = claimset_claim_store(cs, nslots, fp, make_claim(level, record_ckey(key)), level);
+    if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
+    flag[i] = r == CL_NEW ? RF_INSERTER : (r == CL_CUR ? RF_CAND : RF_OUT);
+    probes = 1;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off, 64);
+  if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&stripe(C).probes, probes);
+}
+
+// PASS 0: candidates fold their claims (a displaced local claim loses its
+// newmask bit, the displacer is flagged); PASS 1: inserters and displacers
+// win iff the stored claim is still theirs.
+template <class M, int PASS>
+__global__ void __launch_bounds__(256)
+k_rec_settle(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
+             uint64_t nslots, uint32_t level, uint32_t rank,
+             const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
+             uint32_t* __restrict__ newmask, uint64_t nlocal, uint32_t* __restrict__ isnew,
+             Counters* __restrict__ C) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int r = claimset_claim(cs, nslots, in[i].fp, make_claim(level, record_ckey(in[i].key)), level);
-  if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
-  cand[i] = (r == CL_NEW || r == CL_CUR) ? 1u : 0u;
+  const unsigned int fl = flag[i];
+  if (PASS == 0) {
+    if (fl != RF_CAND) return;
+    const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
+    const unsigned long long prev = claimset_store_claim(cs, nslots, rfp[i], claim);
+    if (prev < ~claim) settle_displace(prev, level, rank, 0, nlocal, newmask, C, &flag[i], RF_DISPLACER);
+  } else {
+    uint32_t w = 0;
+    if (fl >= RF_INSERTER) {
+      const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
+      w = ~claimset_get(cs, nslots, rfp[i]) == claim ? 1u : 0u;
+    }
+    isnew[i] = w;
+  }
 }
 
+// chunk_base = this rank's own new states (the records' emit base);
+// level_new = all new states of the level
+__global__ void k_shard_base(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask,
+                             uint64_t nlocal, const uint32_t* __restrict__ ioff,
+                             const uint32_t* __restrict__ isnew, uint64_t nrec, Counters* __restrict__ C) {
+  if (threadIdx.x != 0) return;
+  const uint64_t lt = nlocal ? (uint64_t)offsets[nlocal - 1] + NewCount()(newmask[nlocal - 1]) : 0;
+  const uint64_t rt = nrec ? (uint64_t)ioff[nrec - 1] + isnew[nrec - 1] : 0;
+  C->chunk_base = lt;
+  C->level_new = lt + rt;
+}
+
+// cand_total = sum of the next_cand stripes (one lane per stripe)
+__global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C) {
+  static_assert(CTR_STRIPES == 64, "one lane per stripe");
+  unsigned long long v = C->s[threadIdx.x].next_cand;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if (threadIdx.x == 0) C->cand_total = v;
+}
+
+// The winners among this rank's own successors (newmask), in parent order.
 template <class M>
 __global__ void __launch_bounds__(256)
-k_shard_settle(const Record<M>* __restrict__ in, uint64_t n, const ClaimEntry* __restrict__ cs,
-               uint64_t nslots, uint32_t level, const uint32_t* __restrict__ cand,
-               uint32_t* __restrict__ isnew) {
+k_shard_emit_local(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uint64_t rank,
+                   const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
+                   typename M::State* __restrict__ next, unsigned long long* __restrict__ pkeys,
+                   uint64_t next_gidx, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned long long sh_cand;
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sh_cand = 0;
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t w = 0;
-  if (cand[i])
-    w = ~claimset_get(cs, nslots, in[i].fp) == make_claim(level, record_ckey(in[i].key)) ? 1u : 0u;
-  isnew[i] = w;
+  unsigned long long cand = 0;
+  if (i < n) {
+    uint32_t mask = newmask[i];
+    if (mask) {
+      const typename M::State s = load_state<M>(cur, i);
+      const typename M::Plan pl = M::plan(s, f);
+      uint64_t o = offsets[i];
+      for (; mask; mask &= mask - 1) {
+        const int t = __ffs(mask) - 1;
+        int slot, j;
+        M::locate(pl, t, slot, j);
+        typename M::State x;
+        M::apply(s, slot, j, f, x);
+        store_state<M>(next, o, x);
+        const int act = M::slot_action(s, slot);
+        const uint64_t key = (rank << 60) | (i << 16) | ((uint64_t)t << 8);
+        pkeys[next_gidx + o] = key | (uint64_t)act;
+        if (M::check(x) >= 0) atomicMin(&C->err_key, key | E_INVARIANT);
+        atomicAdd(&sh_act[act], 1u);
+        cand += (unsigned long long)M::plan(x, f).total;
+        ++o;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
+    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
 
+// The winners among the received records, after the local ones.
 template <class M>
 __global__ void __launch_bounds__(256)
-k_shard_emit(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
-             const uint32_t* __restrict__ offsets, Flags f, typename M::State* __restrict__ next,
-             unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C) {
+k_shard_emit_rec(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
+                 const uint32_t* __restrict__ ioff, Flags f, typename M::State* __restrict__ next,
+                 unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C) {
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned long long sh_cand;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
@@ -206,9 +260,9 @@ k_shard_emit(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __res
   unsigned long long cand = 0;
   if (i < n && isnew[i]) {
     typename M::State x;
-#pragma unroll
-    for (int k = 0; k < M::W; ++k) x.w[k] = in[i].w[k];
-    const uint64_t key = in[i].key, o = offsets[i];
+    uint64_t key;
+    load_record<M>(in, i, x, key);
+    const uint64_t o = C->chunk_base + ioff[i];
     store_state<M>(next, o, x);
     pkeys[next_gidx + o] = key;
     if (M::check(x) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
@@ -286,6 +340,7 @@ class ShardT final : public ShardBase {
     std::vector<State> mine;
     std::vector<unsigned long long> keys;
     std::vector<uint64_t> fps;
+    cand_ = 0;
     for (int k = 0; k < M::num_init(); ++k) {
       State s;
       M::init_state(k, s);
@@ -295,6 +350,7 @@ class ShardT final : public ShardBase {
       mine.push_back(s);
       keys.push_back(KEY_INIT | (uint64_t)k);
       fps.push_back(fp);
+      cand_ += (uint64_t)M::plan(s, flags_).total;
       if (M::check(s) >= 0 && init_err_ == ~0ull)
         init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
     }
@@ -302,6 +358,7 @@ class ShardT final : public ShardBase {
     level_ = 1;
     level_base_.assign(1, 0);
     gen_init_ = n_;
+    cand_total_ = 0;
     KC_TRY(grow_buffer(cur_, cur_cap_, std::max<uint64_t>(n_, 1), false, st_));
     KC_TRY(grow_buffer(pkeys_, pk_cap_, std::max<uint64_t>(n_, 1), false, st_));
     if (n_) {
@@ -320,6 +377,7 @@ class ShardT final : public ShardBase {
     return 0;
   }
 
+  // Claims this rank's own successors of the level; counts the rest per owner.
   int expand(uint64_t* counts, uint64_t* err_key) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
@@ -333,13 +391,25 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_expand: frontier wider than 2^32 states");
       return -ENOMEM;
     }
-    const unsigned grid = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
+    KC_TRY(cs_.reserve(cand_, st_));
+    const uint64_t tiles = (n_ + CLAIM_TILE - 1) / CLAIM_TILE;
+    KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
+    KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
+    KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+    KC_TRY(grow_buffer(newmask_, mask_cap_, n_, false, st_));
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
-    hipLaunchKernelGGL(k_shard_count<M>, dim3(grid), dim3(CLAIM_TILE),
-                       (size_t)world_ * CLAIM_TILE * sizeof(unsigned int), st_, cur_, n_, flags_,
-                       cfg_.check_deadlock, (uint32_t)world_, cnt_, repmask_, d_ctr_);
+    ShardArgs sh;
+    sh.world = (uint32_t)world_;
+    sh.rank = (uint32_t)rank_;
+    sh.repmask = repmask_;
+    sh.cnt = cnt_;
+    const size_t dyn = (size_t)(CLAIM_TILE + ((world_ + 3) / 4) * CLAIM_TILE) * sizeof(unsigned int);
+    hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
+                       cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                       (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                       d_ctr_, sh);
     // one exclusive scan over the owner-major matrix = every record's position
     // in the owner-grouped send buffer
     const uint64_t cells = n_ * (uint64_t)world_;
@@ -354,7 +424,7 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
     if (h_ctr_->overflow || h_ctr_->batch_used) {
-      set_error("kc_shard_expand: successor overflow");
+      set_error("kc_shard_expand: successor overflow or full table");
       return -ENOMEM;
     }
     for (int o = 0; o < world_; ++o) {
@@ -380,56 +450,86 @@ class ShardT final : public ShardBase {
     return 0;
   }
 
+  // Claims the received records, settles local and record claims together,
+  // emits the winners.  `recv` must be complete (caller's stream synced).
   int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     const Rec* in = (const Rec*)recv;
     *n_new = 0;
     *err_key = ~0ull;
     next_n_ = 0;
+    if (n_ == 0 && n == 0) return 0;
+    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
+    KC_TRY(cs_.reserve(cand_ + n, st_));     // count excludes this level's local inserts (<= cand_)
+    const uint32_t succ_level = (uint32_t)level_ + 1;
+    const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
+    const unsigned rgrid = (unsigned)((n + 255) / 256);
     if (n) {
-      KC_TRY(cs_.reserve(n, st_));
-      KC_TRY(grow_buffer(cand_buf_, cand_cap_, n, false, st_));
+      KC_TRY(grow_buffer(rfp_, rfp_cap_, n, false, st_));
+      KC_TRY(grow_buffer(flag_, flag_cap_, n, false, st_));
       KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
       KC_TRY(grow_buffer(ioff_, ioff_cap_, n, false, st_));
-      KC_TRY(grow_buffer(next_, next_cap_, n, false, st_));
-      const uint64_t next_gidx = level_base_.back() + n_;
-      KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + n, true, st_));
-      const unsigned grid = (unsigned)((n + 255) / 256);
-      const uint32_t succ_level = (uint32_t)level_ + 1;
-      hipLaunchKernelGGL(k_shard_claim<M>, dim3(grid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
-                         succ_level, cand_buf_, d_ctr_);
-      hipLaunchKernelGGL(k_shard_settle<M>, dim3(grid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
-                         succ_level, cand_buf_, isnew_);
-      size_t tmp_bytes = 0;
+      hipLaunchKernelGGL(k_rec_claim<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
+                         succ_level, rfp_, flag_, d_ctr_);
+    }
+    // settle pass A (local tiles, records), then pass B
+    if (n_)
+      hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, n_, (uint64_t)0,
+                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_,
+                         (uint32_t)rank_);
+    if (n)
+      hipLaunchKernelGGL((k_rec_settle<M, 0>), dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t,
+                         cs_.nslots, succ_level, (uint32_t)rank_, rfp_, flag_, newmask_, n_, isnew_,
+                         d_ctr_);
+    if (n_)
+      hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, n_, (uint64_t)0,
+                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_,
+                         (uint32_t)rank_);
+    if (n)
+      hipLaunchKernelGGL((k_rec_settle<M, 1>), dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t,
+                         cs_.nslots, succ_level, (uint32_t)rank_, rfp_, flag_, newmask_, n_, isnew_,
+                         d_ctr_);
+    // positions: this rank's own winners first, then the records'
+    size_t tmp_bytes = 0;
+    if (n_) {
+      KC_TRY(grow_buffer(offsets_, offsets_cap_, n_, false, st_));
+      const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+    }
+    if (n) {
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
       KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
-      hipLaunchKernelGGL(k_shard_emit<M>, dim3(grid), dim3(256), 0, st_, in, n, isnew_, ioff_,
-                         flags_, next_, pkeys_, next_gidx, d_ctr_);
-      KC_HIP_TRY(hipGetLastError());
-      uint32_t lo = 0, lc = 0;
-      KC_HIP_TRY(hipMemcpyAsync(&lo, ioff_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipMemcpyAsync(&lc, isnew_ + n - 1, 4, hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
-      KC_HIP_TRY(hipStreamSynchronize(st_));
-      if (h_ctr_->overflow || h_ctr_->batch_used) {
-        set_error("kc_shard_insert: table full");
-        return -ENOMEM;
-      }
-      next_n_ = (uint64_t)lo + lc;
-      if (getenv("KC_SHARD_DEBUG")) {
-        std::vector<uint32_t> hc(n);
-        KC_HIP_TRY(hipMemcpy(hc.data(), cand_buf_, n * 4, hipMemcpyDeviceToHost));
-        uint64_t nc = 0;
-        for (auto v : hc) nc += v;
-        fprintf(stderr, "shard r%d level %d: records %llu candidates %llu new %llu slots %llu count %llu\n",
-                rank_, level_, (unsigned long long)n, (unsigned long long)nc,
-                (unsigned long long)next_n_, (unsigned long long)cs_.nslots,
-                (unsigned long long)cs_.count);
-      }
-      cs_.count += next_n_;
-      if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
     }
+    hipLaunchKernelGGL(k_shard_base, dim3(1), dim3(64), 0, st_, offsets_, newmask_, n_, ioff_, isnew_,
+                       n, d_ctr_);
+    // capacity: at most one new state per own successor and per record
+    const uint64_t bound = cand_ + n;
+    KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
+    const uint64_t next_gidx = level_base_.back() + n_;
+    KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + bound + 1, true, st_));
+    if (n_)
+      hipLaunchKernelGGL(k_shard_emit_local<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
+                         cur_, n_, flags_, (uint64_t)rank_, newmask_, offsets_, next_, pkeys_, next_gidx,
+                         d_ctr_);
+    if (n)
+      hipLaunchKernelGGL(k_shard_emit_rec<M>, dim3(rgrid), dim3(256), 0, st_, in, n, isnew_, ioff_,
+                         flags_, next_, pkeys_, next_gidx, d_ctr_);
+    hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (h_ctr_->overflow || h_ctr_->batch_used) {
+      set_error("kc_shard_insert: table full or claim protocol violation");
+      return -ENOMEM;
+    }
+    next_n_ = h_ctr_->level_new;
+    next_cand_ = h_ctr_->cand_total - cand_total_;
+    cand_total_ = h_ctr_->cand_total;
+    cs_.count += next_n_;
+    if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
     *n_new = next_n_;
     return 0;
   }
@@ -439,6 +539,8 @@ class ShardT final : public ShardBase {
     std::swap(cur_, next_);
     std::swap(cur_cap_, next_cap_);
     n_ = next_n_;
+    cand_ = next_cand_;
+    next_cand_ = 0;
     ++level_;
     return 0;
   }
@@ -475,6 +577,7 @@ class ShardT final : public ShardBase {
     r->distinct = cs_.count;
     r->fpset_slots = cs_.capacity();
     r->fpset_probes = h_ctr_->probes();
+    r->batch_inserts = h_ctr_->settles();
     r->nlevels = level_;
     return 0;
   }
@@ -484,8 +587,9 @@ class ShardT final : public ShardBase {
     (void)hipSetDevice(cfg_.device);
     cs_.release();
     for (void* p : {(void*)cur_, (void*)next_, (void*)pkeys_, (void*)cnt_, (void*)off_,
-                    (void*)repmask_, (void*)cand_buf_, (void*)isnew_, (void*)ioff_, (void*)scan_tmp_, (void*)d_ctr_,
-                    (void*)d_owner_base_})
+                    (void*)repmask_, (void*)newmask_, (void*)offsets_, (void*)rcount_, (void*)rec_fp_,
+                    (void*)rec_lk_, (void*)rfp_, (void*)flag_, (void*)isnew_, (void*)ioff_,
+                    (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_owner_base_) (void)hipHostFree(h_owner_base_);
@@ -501,16 +605,24 @@ class ShardT final : public ShardBase {
   uint64_t cur_cap_ = 0, next_cap_ = 0;
   unsigned long long* pkeys_ = nullptr;
   uint64_t pk_cap_ = 0;
-  uint32_t *cnt_ = nullptr, *off_ = nullptr, *repmask_ = nullptr, *isnew_ = nullptr, *ioff_ = nullptr;
-  uint32_t* cand_buf_ = nullptr;
-  uint64_t cand_cap_ = 0;
-  uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
+  // expand: owner counts / scan, remote representatives, local claim tiles
+  uint32_t *cnt_ = nullptr, *off_ = nullptr, *repmask_ = nullptr, *newmask_ = nullptr, *offsets_ = nullptr;
+  uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, mask_cap_ = 0, offsets_cap_ = 0;
+  unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
+  unsigned long long* rec_fp_ = nullptr;
+  uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;
+  // insert: per received record
+  unsigned long long* rfp_ = nullptr;
+  unsigned int* flag_ = nullptr;
+  uint32_t *isnew_ = nullptr, *ioff_ = nullptr;
+  uint64_t rfp_cap_ = 0, flag_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
   uint64_t* d_owner_base_ = nullptr;   // per-owner record totals (device / pinned host)
   uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
   uint64_t n_ = 0, next_n_ = 0, send_total_ = 0, gen_init_ = 0;
+  uint64_t cand_ = 0, next_cand_ = 0, cand_total_ = 0;   // successors of the frontier
   uint64_t init_err_ = ~0ull;
   int level_ = 0;
   std::vector<uint64_t> level_base_;
