@@ -180,17 +180,26 @@ int kc_shard_create(const kc_model_config *cfg, int rank, int world, kc_shard **
 void kc_shard_destroy(kc_shard *s);
 /* Adopt (insert + enqueue) the Init states this rank owns. */
 int kc_shard_init(kc_shard *s, uint64_t *n_local);
-/* Expand the frontier; counts_out[r] = records destined to rank r (world
- * entries); *err_key_out = this rank's min Assert/deadlock key or ~0. */
+/* Run every stage on the caller's HIP stream (e.g. the one its RCCL
+ * collectives use) instead of the shard's own: pack() then returns without a
+ * host sync and insert() may read a recv buffer written earlier on that
+ * stream (NULL = the default stream).  Call before kc_shard_init. */
+int kc_shard_set_stream(kc_shard *s, void *hip_stream);
+/* Expand the frontier: claim the successors this rank owns in place;
+ * counts_out[r] = records destined to rank r (world entries, 0 for this
+ * rank); *err_key_out = this rank's min Assert/deadlock key or ~0. */
 int kc_shard_expand(kc_shard *s, uint64_t *counts_out, uint64_t *err_key_out);
-/* Bytes per record: 8*state_words + 16 (state, fingerprint, key). */
+/* Bytes per record: the state's canonical words and the key, padded to 16 B
+ * (the receiver recomputes the fingerprint). */
 uint64_t kc_shard_record_bytes(kc_shard *s);
-/* Write sum(counts) records, grouped by owner rank, into device memory. */
+/* Write sum(counts) records, grouped by owner rank, into device memory
+ * (complete on return unless a caller stream was set). */
 int kc_shard_pack(kc_shard *s, void *send_dev);
-/* Dedup + insert `n_records` received records (device memory, sorted by
- * source rank); *n_new = states added to this rank's next frontier.  The
- * library reads recv_dev on its own HIP stream: the caller must have
- * completed every write to it (e.g. synchronised its all-to-all stream). */
+/* Dedup + insert `n_records` received records (device memory, grouped by
+ * source rank) together with this rank's own claims of the level;
+ * *n_new = states added to this rank's next frontier.  Without a caller
+ * stream the library reads recv_dev on its own HIP stream: the caller must
+ * have completed every write to it (e.g. synchronised its all-to-all). */
 int kc_shard_insert(kc_shard *s, const void *recv_dev, uint64_t n_records, uint64_t *n_new,
                     uint64_t *err_key_out);
 /* The new states become the frontier (after the caller's agreement step). */

@@ -282,6 +282,7 @@ class ShardBase {
  public:
   virtual ~ShardBase() = default;
   virtual int setup() = 0;
+  virtual int set_stream(hipStream_t st) = 0;
   virtual int init(uint64_t* n_local) = 0;
   virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
   virtual uint64_t record_bytes() const = 0;
@@ -325,6 +326,13 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
+    return 0;
+  }
+
+  int set_stream(hipStream_t st) override {
+    if (own_st_ && st_) KC_HIP_TRY(hipStreamDestroy(st_));
+    st_ = st;
+    own_st_ = false;
     return 0;
   }
 
@@ -446,7 +454,7 @@ class ShardT final : public ShardBase {
                          (Rec*)send);
       KC_HIP_TRY(hipGetLastError());
     }
-    KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (own_st_) KC_HIP_TRY(hipStreamSynchronize(st_));   // else stream-ordered with the caller
     return 0;
   }
 
@@ -593,13 +601,14 @@ class ShardT final : public ShardBase {
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_owner_base_) (void)hipHostFree(h_owner_base_);
-    if (st_) (void)hipStreamDestroy(st_);
+    if (st_ && own_st_) (void)hipStreamDestroy(st_);
   }
 
   kc_model_config cfg_;
   int rank_, world_;
   Flags flags_{};
   hipStream_t st_ = nullptr;
+  bool own_st_ = true;
   DevClaimSet cs_;
   State *cur_ = nullptr, *next_ = nullptr;
   uint64_t cur_cap_ = 0, next_cap_ = 0;
@@ -663,6 +672,10 @@ void kc_shard_destroy(kc_shard* s) { delete s; }
 int kc_shard_init(kc_shard* s, uint64_t* n_local) {
   if (!s || !n_local) { set_error("kc_shard_init: NULL"); return -EINVAL; }
   return s->impl->init(n_local);
+}
+int kc_shard_set_stream(kc_shard* s, void* stream) {
+  if (!s) { set_error("kc_shard_set_stream: NULL"); return -EINVAL; }   // stream 0: the default stream
+  return s->impl->set_stream((hipStream_t)stream);
 }
 int kc_shard_expand(kc_shard* s, uint64_t* counts, uint64_t* err_key) {
   if (!s || !counts || !err_key) { set_error("kc_shard_expand: NULL"); return -EINVAL; }
