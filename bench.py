@@ -220,6 +220,7 @@ def bench_fpset(args):
         tlk += tl
     load, table_bytes = s.size() / s.capacity(), s.capacity() * 8
     s.close()
+    traffic, tsrc = pmc_traffic("fpset", "k_stress_insert")
     gbs = n * args.steps * 64 / tin / 1e9
     return {
         "metric": "FPSet probe HBM GB/s (insert)", "value": round(gbs, 1), "unit": "GB/s",
@@ -233,8 +234,10 @@ def bench_fpset(args):
                    "lookups_per_s": round(n * args.steps / tlk, 1),
                    "lookups_found": int(found)},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_stress_insert"},
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_stress_insert", "bytes_per_launch": batch * 64,
+                     "traffic_unit": "HBM bytes per launch (PMC, one launch = one batch)",
+                     "traffic_source": tsrc},
     }
 
 

@@ -32,4 +32,18 @@ step write
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $BENCH > $O/write.log 2>&1 || { echo WRITE_FAIL; tail -20 $O/write.log; exit 1; }
 cd $R
 python3 tools/pmc_summary.py --trace $O/trace --fetch $O/fetch --write $O/write --out $O/summary.json --command "rocprofv3 -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-timing"
+# FPSet stress (BASELINE config 4): the bench line at 1e10 fps, PMC passes at 2^30
+step bench_fpset
+timeout -k 10 300 python -u bench.py --workload fpset --steps 2 --warmup 1 > $O/bench_fpset.json 2> $O/bench_fpset.err || { echo BENCHF_FAIL; tail -20 $O/bench_fpset.err; exit 1; }
+cat $O/bench_fpset.json
+FBENCH="$R/bench.py --workload fpset --fp-count 1073741824 --steps 1 --warmup 0"
+cd /tmp
+step fpset_trace
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ftrace -o run -- python3 $FBENCH > $O/ftrace.log 2>&1 || { echo FTRACE_FAIL; tail -20 $O/ftrace.log; exit 1; }
+step fpset_fetch
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/ffetch -o run -- python3 $FBENCH > $O/ffetch.log 2>&1 || { echo FFETCH_FAIL; tail -20 $O/ffetch.log; exit 1; }
+step fpset_write
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/fwrite -o run -- python3 $FBENCH > $O/fwrite.log 2>&1 || { echo FWRITE_FAIL; tail -20 $O/fwrite.log; exit 1; }
+cd $R
+python3 tools/pmc_summary.py --trace $O/ftrace --fetch $O/ffetch --write $O/fwrite --out $O/fpset_summary.json --command "rocprofv3 -- python3 bench.py --workload fpset --fp-count 1073741824 --steps 1 --warmup 0"
 step done
