@@ -184,12 +184,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_rc;
+  __shared__ unsigned int sh_nrep;                // tile representatives
   // SH only (dynamic LDS): remote representatives per parent, then their
   // counts per owner packed 4 owners x 8 bits per word (a parent has <= 32)
   extern __shared__ unsigned int sh_dyn[];
   unsigned int* sh_rep = sh_dyn;
   unsigned int* sh_cnt = sh_dyn + CLAIM_TILE;
-  if (threadIdx.x == 0) sh_rc = 0;
+  if (threadIdx.x == 0) {
+    sh_rc = 0;
+    sh_nrep = 0;
+  }
   for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
     sh_fp[k] = 0ull;
     sh_key[k] = ~0u;
@@ -267,10 +271,36 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     if (live) scratch[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
     return;
   }
+  // compact the tile representatives to the front of the LDS table, so a
+  // lane claims ~3 dense entries in a row instead of scanning 8 sparse ones
+  // (each scan step costs its wave one probe round trip)
+  {
+    constexpr int PER = CLAIM_LDS / CLAIM_TILE;
+    unsigned long long efp[PER];
+    unsigned int ekey[PER];
+    unsigned int mine = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      efp[j] = sh_fp[threadIdx.x + j * CLAIM_TILE];
+      ekey[j] = sh_key[threadIdx.x + j * CLAIM_TILE];
+      mine += efp[j] != 0ull;
+    }
+    unsigned int pos = mine ? atomicAdd(&sh_nrep, mine) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (efp[j]) {
+        sh_fp[pos] = efp[j];
+        sh_key[pos] = ekey[j];
+        ++pos;
+      }
+    }
+    __syncthreads();
+  }
   // every tile representative claims its fp in the ClaimSet
-  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+  const int nrep = (int)sh_nrep;
+  for (int k = threadIdx.x; k < nrep; k += CLAIM_TILE) {
     const unsigned long long fp = sh_fp[k];
-    if (!fp) continue;
     const unsigned int lk = sh_key[k];
     const unsigned int lp = lk >> 5, t = lk & 31;
     const uint64_t pidx = base + tile0 + lp;

@@ -175,12 +175,18 @@ __device__ __forceinline__ int claimset_claim(ClaimEntry* __restrict__ t, uint64
 // Stale copies in another XCD's L2 can only show a slot empty or its claim
 // word 0, which makes a lane a candidate (conservative); the CAS result is
 // authoritative for the fp.
-__device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, uint64_t nslots,
-                                                    uint64_t fp, uint64_t claim, uint32_t level) {
+// The first probe's 16-B load split out, so a caller can issue the loads of
+// several claims back to back (claimset_claim_store_from takes the slot index
+// and the pair it loaded).
+__device__ __forceinline__ ulonglong2 claimset_first(const ClaimEntry* __restrict__ t, uint64_t i) {
+  return *reinterpret_cast<const ulonglong2*>(t + i);
+}
+__device__ __forceinline__ int claimset_claim_store_from(ClaimEntry* __restrict__ t, uint64_t nslots,
+                                                         uint64_t fp, uint64_t claim, uint32_t level,
+                                                         uint64_t i, ulonglong2 e) {
   const unsigned long long nc = ~(unsigned long long)claim;
-  uint64_t i = bucket_of(fp, nslots);
   for (uint64_t probe = 0; probe < nslots; ++probe) {
-    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+    if (probe) e = *reinterpret_cast<const ulonglong2*>(t + i);
     unsigned long long f = e.x, seen = e.y;
     if (f == 0ull) {
       f = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
@@ -199,6 +205,11 @@ __device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, 
     i = (i + 1 == nslots) ? 0 : i + 1;
   }
   return CL_FULL;
+}
+__device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, uint64_t nslots,
+                                                    uint64_t fp, uint64_t claim, uint32_t level) {
+  const uint64_t i = bucket_of(fp, nslots);
+  return claimset_claim_store_from(t, nslots, fp, claim, level, i, claimset_first(t, i));
 }
 
 // Settle pass A of a CL_CUR candidate: fold its claim into the slot.
