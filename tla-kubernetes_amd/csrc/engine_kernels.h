@@ -421,32 +421,61 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long cand = 0;
+  // Wave-balanced like k_claim: the wave's new states are dealt out 64 per
+  // round in order, lane g of a round writes next[obase + g], so the stores
+  // of a round are one contiguous run.
+  uint32_t mask = 0;
+  uint64_t counts = 0;
+  uint32_t obase = 0;
   if (i < n) {
-    uint32_t mask = newmask[i];
-    if (mask) {
-      const typename M::State s = load_state<M>(cur, i);
-      const typename M::Plan pl = M::plan(s, f);
-      const uint64_t pidx = base + i;
-      uint64_t o = C->chunk_base + offsets[i];
-      for (; mask; mask &= mask - 1) {
-        const int t = __ffs(mask) - 1;
-        int slot, j;
-        M::locate(pl, t, slot, j);
-        typename M::State x;
-        M::apply(s, slot, j, f, x);
-        store_state<M>(next, o, x);
-        if (keep_trace) {
-          parent[next_gidx + o] = level_gidx + pidx;
-          ord[next_gidx + o] = (uint8_t)t;
-        }
-        if (M::check(x) >= 0)
-          atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
-        atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
-        const typename M::Plan px = M::plan(x, f);
-        cand += (unsigned long long)px.total;
-        ++o;
-      }
+    mask = newmask[i];
+    if (mask) counts = M::plan(load_state<M>(cur, i), f).counts;
+  }
+  const int cnt = __builtin_popcount(mask);
+  const int lane = (int)(threadIdx.x & 63);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  const int wtot = __shfl(incl, 63, 64);
+  const int excl = incl - cnt;
+  if (wtot) obase = __shfl(i < n ? offsets[i] - (uint32_t)excl : 0u, 0, 64);
+  const uint64_t wave0 = i - (uint64_t)lane;
+  for (int r = 0; r < wtot; r += 64) {
+    const int g = r + lane;
+    int p = 0;                                       // last lane with excl <= g
+#pragma unroll
+    for (int b = 32; b > 0; b >>= 1) {
+      const int e = __shfl(excl, p + b, 64);
+      if (e <= g) p += b;
     }
+    int k = g - __shfl(excl, p, 64);
+    uint32_t m = (uint32_t)__shfl((int)mask, p, 64);
+    const uint64_t pc = __shfl(counts, p, 64);
+    if (g >= wtot) continue;
+    for (; k > 0; --k) m &= m - 1;
+    const int t = __ffs(m) - 1;
+    const uint64_t pi = wave0 + (uint64_t)p;
+    const uint64_t pidx = base + pi;
+    const typename M::State s = load_state<M>(cur, pi);
+    const typename M::Plan pl{pc, 0, -1, -1};
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    typename M::State x;
+    M::apply(s, slot, j, f, x);
+    const uint64_t o = C->chunk_base + obase + (uint64_t)g;
+    store_state<M>(next, o, x);
+    if (keep_trace) {
+      parent[next_gidx + o] = level_gidx + pidx;
+      ord[next_gidx + o] = (uint8_t)t;
+    }
+    if (M::check(x) >= 0)
+      atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
+    atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
+    const typename M::Plan px = M::plan(x, f);
+    cand += (unsigned long long)px.total;
   }
   // wave reduction of the candidate count, then one LDS atomic per wave
 #pragma unroll
