@@ -52,6 +52,18 @@ k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ new
   }
 }
 
+// Per-level counter head reset (err_key = ~0; chunk_base, overflow,
+// batch_used = 0), enqueued behind the previous level's head read-back so
+// it runs while the host waits, not after it.
+__global__ void k_level_reset(Counters* __restrict__ C) {
+  if (threadIdx.x == 0) {
+    C->err_key = ~0ull;
+    C->chunk_base = 0;
+    C->overflow = 0;
+    C->batch_used = 0;
+  }
+}
+
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
 
 template <class M>
@@ -171,6 +183,8 @@ class EngineT final : public EngineBase {
     // default: one chunk per level; chunk_states bounds the per-chunk
     // buffers.  Claims are level-global (keys grow with the parent index),
     // so a chunk's winners are final once its own claim pass is done.
+    // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
+    hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
     const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 40)) + 255) / 256 * 256;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
@@ -195,9 +209,6 @@ class EngineT final : public EngineBase {
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
-      // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
-      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
-      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->chunk_base, 0, 3 * 8, st_));
       const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
       for (uint64_t start = 0; start < n; start += chunk) {
         const uint64_t cn = std::min(chunk, n - start);
@@ -251,6 +262,7 @@ class EngineT final : public EngineBase {
       }
       KC_HIP_TRY(hipGetLastError());
       KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+      hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);   // next level's head
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
