@@ -45,6 +45,9 @@ def parse():
                     help="budget of the CPU baseline sample (oracle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--all-kernel-timing", action="store_true",
+                    help="HIP events on every kernel (default: on the roofline kernel k_claim only;"
+                         " events on all five per-level launches cost the NP=2 check ~6 ms)")
     ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
     ap.add_argument("--fp-count", type=float, default=1e10,
                     help="fpset workload: fingerprints inserted (and looked up) per step")
@@ -135,7 +138,8 @@ def bench_single(args, kw, desc):
     import torch
     import kubecheck
 
-    cfg = kubecheck.ModelConfig(**kw, keep_trace=True, timing=not args.no_timing,
+    cfg = kubecheck.ModelConfig(**kw, keep_trace=True,
+                                timing=0 if args.no_timing else (1 if args.all_kernel_timing else 2),
                                 fpset_slots=1 << 20, chunk_states=args.chunk)
     mc = kubecheck.ModelChecker(cfg)
     for _ in range(args.warmup):
@@ -184,7 +188,7 @@ def bench_single(args, kw, desc):
             roof["traffic_unit"] = "HBM bytes per launch (PMC)"
             roof["traffic_source"] = src
         out["roofline"] = roof
-        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items()}
+        out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items() if v[0] > 0}
     mc.close()
     return out
 

@@ -117,7 +117,8 @@ typedef struct {
   uint64_t fpset_slots;    /* initial FPSet slots; 0 = default */
   uint64_t chunk_states;   /* parents per expansion chunk; 0 = default */
   int verbose;             /* progress lines to stderr */
-  int timing;              /* 1 = time every kernel launch with HIP events */
+  int timing;              /* 1 = time every kernel launch with HIP events,
+                              2 = only k_claim (the roofline kernel) */
 } kc_model_config;
 
 typedef struct {
@@ -160,7 +161,8 @@ int kc_engine_trace_tuple(kc_engine *e, int i, uint64_t *out);
 int64_t kc_engine_level_tuples(kc_engine *e, int level, uint64_t *out, uint64_t cap_states);
 /* Ask run() to keep a host copy of level `level`'s packed states. */
 int kc_engine_capture_level(kc_engine *e, int level);
-/* Per-kernel device timings of the last run (ms; needs cfg.timing=1):
+/* Per-kernel device timings of the last run (ms; needs cfg.timing=1, or 2
+ * for expand alone):
  * expand, resolve, scan, emit; and the number of launches of each. */
 int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
 

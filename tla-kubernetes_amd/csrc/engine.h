@@ -27,7 +27,7 @@ class EngineBase {
   virtual int state_words() const = 0;
   virtual int tuple_words() const = 0;
   void set_capture(int level) { capture_level_ = level; }
-  void set_timing(bool on) { timing_ = on; }
+  void set_timing(bool on) { timing_ = on ? 1 : 0; }
   void kernel_times(double* ms, uint64_t* launches) const {
     for (int k = 0; k < KK_COUNT; ++k) {
       if (ms) ms[k] = ktime_ms_[k];
@@ -38,7 +38,7 @@ class EngineBase {
  protected:
   kc_model_config cfg_;
   int capture_level_ = 0;
-  bool timing_ = false;
+  int timing_ = 0;   // 1: HIP events on every kernel; 2: on k_claim only
   double ktime_ms_[KA_TOTAL] = {};
   uint64_t klaunch_[KA_TOTAL] = {};
   bool ablate_ = false;

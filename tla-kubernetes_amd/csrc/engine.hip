@@ -73,10 +73,10 @@ class EngineT final : public EngineBase {
  public:
   explicit EngineT(const kc_model_config& cfg) : EngineBase(cfg) {
     flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
-    timing_ = cfg.timing != 0;
+    timing_ = cfg.timing == 2 ? 2 : (cfg.timing != 0 ? 1 : 0);
     const char* ab = getenv("KC_ABLATE");
     ablate_ = ab && ab[0] == '1';
-    if (ablate_) timing_ = true;
+    if (ablate_) timing_ = 1;
   }
   ~EngineT() override { release(); }
 
@@ -341,7 +341,9 @@ class EngineT final : public EngineBase {
  private:
   template <class F>
   void timed(int k, F&& f) {
-    if (timing_) {
+    // (timing 2: events bracket the roofline kernel only; ten events per
+    // level cost the NP=2 check 6 ms and Model_1 4 ms of host/queue time)
+    if (timing_ == 1 || (timing_ == 2 && k == KK_EXPAND)) {
       if (ev_used_ + 2 > ev_pool_.size()) {
         hipEvent_t a, b;
         (void)hipEventCreate(&a);

@@ -50,7 +50,7 @@ class ModelConfig:
     fpset_slots: int = 0
     chunk_states: int = 0
     verbose: int = 0
-    timing: bool = False        # per-kernel HIP-event timing (kernel_times())
+    timing: int = 0             # HIP-event timing (kernel_times()): 1 every kernel, 2 k_claim only
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()
