@@ -11,9 +11,11 @@ FPSet with nothing precomputed.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload np2|model1|fpset]
 
-N>1 runs one process per GPU (torch.distributed.run) with the state space
-sharded by fingerprint owner and one RCCL all-to-all per BFS level
-(kubecheck.distributed); rank 0 prints one JSON line.
+N>1 runs one process per GPU (torch.distributed.run; a plain `python bench.py
+--gpus N` starts that launcher itself as a child process) with the state
+space sharded by fingerprint owner and one RCCL all-to-all per BFS level
+(kubecheck.distributed); rank 0 prints one JSON line.  Every run's counts
+are checked against the committed golden fixtures (tests/golden/).
 """
 from __future__ import annotations
 
@@ -166,6 +168,8 @@ def bench_single(args, kw, desc):
     r = results[-1]
     assert all((x.distinct, x.generated) == (r.distinct, r.generated) for x in results)
     assert r.complete and r.error is None
+    golden = golden_check(args.workload, {"distinct": r.distinct, "generated": r.generated,
+                                          "depth": r.depth, "level_width": r.level_width})
     out = {
         "metric": "distinct states/sec (KubeAPI TLC BFS)",
         "value": round(r.distinct * args.steps / dt, 1),
@@ -178,6 +182,7 @@ def bench_single(args, kw, desc):
                    "constants": "REQUESTS_CAN_FAIL=TRUE,REQUESTS_CAN_TIMEOUT=TRUE",
                    "invariants": "TypeOK,OnlyOneVersion", "distinct": r.distinct,
                    "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU",
+                   "path": "single-GPU engine (kc_engine_run)", "golden_check": golden,
                    "claimset_probes": r.fpset_probes, "settle_reads": r.batch_inserts,
                    "chunks": r.levels_chunks},
     }
@@ -209,7 +214,7 @@ def bench_fpset(args):
         if s is not None:
             s.close()
         s = kubecheck.FPSet(capacity=cap)
-        s.stress(0x5EED0000, n, batch, n)
+        s.stress(0x5EED0000, n, batch, n)   # perm63 stream (kc_fpset_stress)
     torch.cuda.synchronize()
     tin = tlk = 0.0
     for k in range(args.steps):
@@ -217,9 +222,9 @@ def bench_fpset(args):
             s.close()
         s = kubecheck.FPSet(capacity=cap)
         ti, tl, found = s.stress(0x5EED0000 + k, n, batch, n)
-        # 63-bit fingerprints: ~n^2/2^64 genuine duplicates in the stream
-        if not n - n * n / 2**60 - 64 <= s.size() <= n:
-            raise RuntimeError(f"fpset stress: size {s.size()} for {n} inserts")
+        # the perm63 stream has no duplicates: every count is exact
+        if s.size() != n or found != (n + 1) // 2:
+            raise RuntimeError(f"fpset stress: size {s.size()} found {found} for {n} inserts")
         tin += ti
         tlk += tl
     load, table_bytes = s.size() / s.capacity(), s.capacity() * 8
@@ -231,7 +236,7 @@ def bench_fpset(args):
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(tin * 1e3 / args.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u64",
-        "data": "synthetic splitmix64 fingerprints generated on device",
+        "data": "synthetic perm63 fingerprint stream generated on device",
         "config": {"workload": f"FPSet stress: {n} inserts + {n} lookups to {load:.0%} load, batch {batch}",
                    "table_bytes": table_bytes,
                    "inserts_per_s": round(n * args.steps / tin, 1),
@@ -245,19 +250,68 @@ def bench_fpset(args):
     }
 
 
+def relaunch(args) -> int:
+    """`python bench.py --gpus N` without a torch.distributed launcher: start
+    N ranks under torch.distributed.run as a CHILD process (nothing here has
+    touched the GPU; no exec) and return its exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def golden_check(workload: str, res: dict) -> str:
+    """Counts of a bench run against the committed fixtures: NP=2 against the
+    oracle's full run (tests/golden/np2_full.json), Model_1 against MC.out
+    (tests/golden/model1_mcout.json) and the oracle's level widths."""
+    g = os.path.join(ROOT, "tests", "golden")
+    if workload == "np2":
+        fx = json.load(open(os.path.join(g, "np2_full.json")))
+        want = (fx["distinct"], fx["generated"], fx["depth"], fx["level_width"])
+        src = "tests/golden/np2_full.json"
+    else:
+        mc = json.load(open(os.path.join(g, "model1_mcout.json")))
+        fx = json.load(open(os.path.join(g, "oracle_fixtures.json")))["model1"]
+        want = (mc["distinct"], mc["generated"], mc["depth"], fx["level_width"])
+        src = "tests/golden/model1_mcout.json (MC.out:1098,1101) + oracle level widths"
+    got = (res["distinct"], res["generated"], res["depth"], list(res["level_width"]))
+    if got != want:
+        raise RuntimeError(f"bench {workload}: counts differ from {src}: "
+                           f"got {got[:3]} want {want[:3]} (widths equal: {got[3] == want[3]})")
+    return src
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
     if args.gpus != world and world != 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.workload == "fpset":
-        out = bench_fpset(args)
+        if args.gpus > 1:
+            from kubecheck.sharded_fpset import bench_sharded_fpset
+
+            out = bench_sharded_fpset(args)
+            if out is None:          # not rank 0
+                return
+        else:
+            out = bench_fpset(args)
     else:
         kw, desc = WORKLOADS[args.workload]
         if args.gpus > 1 or args.sharded:
             from kubecheck import distributed
 
-            out = distributed.bench_sharded(args, kw, desc)
+            out = distributed.bench_sharded(args, kw, desc, golden_check)
             if out is None:          # not rank 0
                 return
         else:

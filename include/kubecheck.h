@@ -86,13 +86,44 @@ uint64_t kc_fpset_capacity(const kc_fpset *s);
  * (sorted), from which TLC derives "based on the actual fingerprints"
  * (MC.out:42).  *prob_out = 1/min_gap (TLC's estimate). */
 int kc_fpset_check_fps(kc_fpset *s, uint64_t *min_gap_out, double *prob_out);
-/* Synthetic stress: insert fingerprints
- * splitmix64(seed + i) for i in [0, n) generated on device, in batches of
- * `batch`; then look up n_lookup fps of which half are present.  Times are
- * device times in seconds. */
+/* Single-fingerprint put/contains, safe from many host threads at once
+ * (TLC's -workers threads each call FPSet.put(long); MC.out:5 "4 workers").
+ * Concurrent calls are flat-combined: one caller launches every pending
+ * request as one batch (arrival order = sequential put order) while the
+ * others wait for their result.  *seen_out = 1 iff already present. */
+int kc_fpset_put(kc_fpset *s, uint64_t fp, int *seen_out);
+int kc_fpset_contains(kc_fpset *s, uint64_t fp, int *seen_out);
+/* Number of combined batches launched by kc_fpset_put/contains so far. */
+uint64_t kc_fpset_combine_rounds(const kc_fpset *s);
+/* Bulk insert / lookup of device-resident fingerprints without per-fp
+ * results (a sharded or streaming caller that only needs the totals):
+ * *n_new_out = fps newly inserted, *found_out = fps present.  Synchronous. */
+int kc_fpset_insert_count_dev(kc_fpset *s, const uint64_t *fps_dev, size_t n, uint64_t *n_new_out,
+                              void *hip_stream);
+int kc_fpset_contains_count_dev(kc_fpset *s, const uint64_t *fps_dev, size_t n, uint64_t *found_out,
+                                void *hip_stream);
+/* Fingerprint-owner routing of a batch (multi-GPU FPSet): stable counting
+ * sort of fps_dev by owner rank floor(fp * world / 2^63) (after the MSB/0
+ * normalisation) into out_dev; counts_out[r] = fps for rank r (host array of
+ * `world` entries, 1 <= world <= 16).  Synchronous. */
+int kc_fpset_partition_dev(kc_fpset *s, const uint64_t *fps_dev, uint64_t n, int world,
+                           uint64_t *out_dev, uint64_t *counts_out, void *hip_stream);
+/* Synthetic stress, fingerprints generated on device:
+ * insert stream i -> perm63(seed + i) for i in [0, n) (perm63 a bijection of
+ * [0, 2^63), so the n fps are distinct and normalised), in batches of
+ * `batch`; then n_lookup lookups, entry j present for even j and absent for
+ * odd j.  So size() grows by exactly n and *found_out = ceil(n_lookup / 2).
+ * Needs 1 <= seed and seed + n + n_lookup < 2^63.  Device times in seconds. */
 int kc_fpset_stress(kc_fpset *s, uint64_t seed, uint64_t n, uint64_t batch,
                     uint64_t n_lookup, double *insert_seconds, double *lookup_seconds,
                     uint64_t *found_out);
+/* The same streams written to device memory: kind 0 = insert stream entries
+ * [start, start + n); kind 1 = lookup stream entries (n_ins = the insert
+ * stream's length).  Asynchronous on hip_stream. */
+int kc_stress_fps_dev(uint64_t seed, int kind, uint64_t n_ins, uint64_t start, uint64_t n,
+                      uint64_t *out_dev, void *hip_stream);
+/* Host copy of one stream entry (tests). */
+uint64_t kc_stress_fp(uint64_t seed, int kind, uint64_t n_ins, uint64_t i);
 
 /* ----------------------------------------------------------- StateQueue */
 typedef struct kc_squeue kc_squeue;
@@ -110,7 +141,10 @@ typedef struct {
   int can_fail;            /* REQUESTS_CAN_FAIL  (MC.tla:5-7) */
   int can_timeout;         /* REQUESTS_CAN_TIMEOUT (MC.tla:10-12) */
   int check_deadlock;      /* launch:16 */
-  int variant;             /* 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace */
+  int variant;             /* 0 = KubeAPI.tla as written; seeded bugs: 1 = Update w/o
+                              HasRead, 2 = Force w/o replace, 3 = C1 ignores the
+                              reply status, 4 = list ignores kind, 5 = Init store
+                              with two Secret versions (kubeapi_spec.h Flags) */
   int device;              /* HIP device ordinal */
   int keep_trace;          /* parent pointers (TLC's trace file); default 1 */
   int max_levels;          /* 0 = to completion */
@@ -119,6 +153,8 @@ typedef struct {
   int verbose;             /* progress lines to stderr */
   int timing;              /* 1 = time every kernel launch with HIP events,
                               2 = only k_claim (the roofline kernel) */
+  int invariants;          /* MC.cfg INVARIANT list: bit 0 TypeOK, bit 1
+                              OnlyOneVersion (default 3; 0 = check none) */
 } kc_model_config;
 
 typedef struct {
@@ -213,6 +249,9 @@ int kc_shard_frontier_tuple(kc_shard *s, uint64_t idx, uint64_t *out);
 /* This rank's counters: act_gen (its parents), act_dist (its new states),
  * generated, distinct (owned), fpset_slots. */
 int kc_shard_result(kc_shard *s, kc_result *res);
+/* k_claim device time in ms (HIP events; needs cfg.timing != 0), launches
+ * and parents expanded since the previous call (counters reset on read). */
+int kc_shard_claim_times(kc_shard *s, double *ms, uint64_t *launches, uint64_t *parents);
 /* owner rank of a fingerprint */
 int kc_shard_owner(uint64_t fp, int world);
 

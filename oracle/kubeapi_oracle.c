@@ -247,10 +247,11 @@ static void a_CStart(const model *m, const kstate *s, int self, emitter *e) {
   }
 }
 static void a_C1(const model *m, const kstate *s, int self, emitter *e) {  /* :551-556 */
-  (void)m;
   if (s->pc[self] != KO_C1) return;
   kstate t = *s;
-  if (s->rq_status[self] != ST_Ok) { br(e, KO_B_C1_START); t.pc[self] = KO_CStart; }
+  /* variant 3 (seeded bug): the Force reply status is ignored, so C2's
+   * Assert(ObjectExists(Secret)) (:598-599) can fail */
+  if (s->rq_status[self] != ST_Ok && m->cfg.variant != 3) { br(e, KO_B_C1_START); t.pc[self] = KO_CStart; }
   else { br(e, KO_B_C1_C10); t.pc[self] = KO_C10; }
   emit(e, &t, 5);
 }
@@ -472,7 +473,9 @@ static void a_APIStart(const model *m, const kstate *s, int self, emitter *e) {
     kstate t = *s;
     int k = s->lr_kind[c];
     uint64_t km = (k == K_Secret) ? m->idmask[ID_SECRET] : (k == K_PVC) ? m->idmask[ID_PVC] : 0;
-    t.lr_objs[c] = s->api & km;
+    /* variant 4 (seeded bug): the reply lists objects of every kind, which
+     * violates IsValidListRequest's o.k = r.kind (:435), i.e. TypeOK */
+    t.lr_objs[c] = m->cfg.variant == 4 ? s->api : (s->api & km);
     t.lr_status[c] = ST_Ok;
     uint64_t nw = s->api & ~km, x = s->api & km;
     while (x) {
@@ -520,6 +523,10 @@ static int init_states(const model *m, kstate *out) {
       t->pc[p] = k == PK_CLIENT ? KO_CStart : k == PK_PVC ? KO_PVCStart : KO_APIStart;
       if (k == PK_CLIENT) t->sr[p] = (mask >> p) & 1;
     }
+    /* variant 5 (seeded bug): apiState starts with two versions of
+     * Secret/foo (vv {} and vv {process 0}), violating OnlyOneVersion */
+    if (m->cfg.variant == 5)
+      t->api = (1ull << u_of(m, ov_make(ID_SECRET, 1, 0, 0))) | (1ull << u_of(m, ov_make(ID_SECRET, 1, 0, 1)));
   }
   return n;
 }
@@ -527,7 +534,22 @@ static int init_states(const model *m, kstate *out) {
 /* TypeOK (KubeAPI.tla:776-781) and OnlyOneVersion (:787-789).
  * Returns -1 if both hold, else the index of the first violated invariant
  * in MC.cfg order (0 TypeOK, 1 OnlyOneVersion). */
+static int check_invariants_all(const model *m, const kstate *s);
+/* the invariants the config lists (MC.cfg:13-15); -1 = all hold */
 static int check_invariants(const model *m, const kstate *s) {
+  int mask = 3 & ~m->cfg.skip_inv;
+  if (!mask) return -1;
+  kstate t = *s;
+  int r = check_invariants_all(m, &t);
+  if (r == 0 && !(mask & 1)) {               /* TypeOK fails but is not checked */
+    for (int id = 0; id < 2; id++)
+      if (popc64(s->api & m->idmask[id]) > 1) return (mask & 2) ? 1 : -1;
+    return -1;
+  }
+  if (r == 1 && !(mask & 2)) return -1;
+  return r;
+}
+static int check_invariants_all(const model *m, const kstate *s) {
   int ok = 1;
   /* \A o \in apiState: IsValidAPIObject(o) — every element of U is a record
    * with n,k,vv[,spec] : holds by construction. */

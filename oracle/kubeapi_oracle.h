@@ -65,10 +65,12 @@ typedef struct {
   int keep_trace;          /* record parent pointers for counterexamples */
   int max_levels;          /* 0 = run to completion */
   uint64_t max_distinct;   /* 0 = unlimited; stop after the level that passes it */
-  int variant;             /* 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace */
+  int variant;             /* 0 = as written; seeded bugs 1-5 (see kubeapi_oracle.c) */
   int fp_bits;             /* 128 (default, 0 means 128) or 64 */
   int fpset_log2;          /* >0: presize the seen-set to 2^k entries (no growth) */
   int progress;            /* print per-level progress to stderr */
+  int skip_inv;            /* invariants NOT in the .cfg's INVARIANT list:
+                              bit 0 TypeOK, bit 1 OnlyOneVersion (0 = check both) */
 } ko_config;
 
 enum { KO_OK = 0, KO_ERR_ASSERT = 1, KO_ERR_INVARIANT = 2, KO_ERR_DEADLOCK = 3,

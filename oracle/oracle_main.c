@@ -13,7 +13,7 @@
 #include <string.h>
 
 int main(int argc, char **argv) {
-  ko_config cfg = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 128, 0, 0};
+  ko_config cfg = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 128, 0, 0, 0};
   int print_trace = 0;
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "-nc") && i + 1 < argc) cfg.nc = atoi(argv[++i]);

@@ -34,7 +34,8 @@ class KoConfig(C.Structure):
     _fields_ = [("nc", C.c_int), ("np", C.c_int), ("ns", C.c_int), ("can_fail", C.c_int),
                 ("can_timeout", C.c_int), ("check_deadlock", C.c_int), ("keep_trace", C.c_int),
                 ("max_levels", C.c_int), ("max_distinct", C.c_uint64), ("variant", C.c_int),
-                ("fp_bits", C.c_int), ("fpset_log2", C.c_int), ("progress", C.c_int)]
+                ("fp_bits", C.c_int), ("fpset_log2", C.c_int), ("progress", C.c_int),
+                ("skip_inv", C.c_int)]
 
 
 class KoResult(C.Structure):
@@ -84,9 +85,10 @@ def lib():
 
 
 def config(nc=1, np_=1, ns=1, can_fail=True, can_timeout=True, check_deadlock=True,
-           keep_trace=True, max_levels=0, variant=0, fp_bits=128) -> KoConfig:
+           keep_trace=True, max_levels=0, variant=0, fp_bits=128, invariants=3) -> KoConfig:
+    """invariants: bit 0 TypeOK, bit 1 OnlyOneVersion (the .cfg INVARIANT list)."""
     return KoConfig(nc, np_, ns, int(can_fail), int(can_timeout), int(check_deadlock),
-                    int(keep_trace), max_levels, 0, variant, fp_bits, 0, 0)
+                    int(keep_trace), max_levels, 0, variant, fp_bits, 0, 0, 3 & ~invariants)
 
 
 def run(cfg: KoConfig) -> dict:

@@ -102,3 +102,18 @@ def test_owner_function_matches_library():
     for fp in rng.integers(1, 2**63, size=2000, dtype="uint64"):
         for w in (2, 3, 8):
             assert owner(int(fp), w) == lib.kc_shard_owner(int(fp), w)
+
+
+@pytest.mark.parametrize("key,kw,kind", [("variant5", dict(variant=5), "invariant"),
+                                         ("ns0", dict(ns=0), "deadlock"),
+                                         ("variant3", dict(variant=3), "assertion")])
+def test_sharded_error_paths(tmp_path, fixtures, key, kw, kind):
+    # variant5: an Init state violates OnlyOneVersion (the sharded Init-state
+    # key 0x12); ns0: deadlock; variant3: C2's Assert
+    fx = fixtures[key]
+    r = run_sharded(tmp_path, 2, **kw)
+    assert r["error"] == kind
+    assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
+    if kind == "assertion":
+        assert r["error_action"] == fx["err_action"]
+    assert r["trace"][0] == fx["trace"][0]

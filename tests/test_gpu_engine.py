@@ -123,3 +123,45 @@ def test_enlarged_full(fixtures):
     assert r.level_width == fx["level_width"]
     assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
     assert r.complete and r.error is None
+
+
+# --- error paths: every kind of violation the checker
+# reports, against the oracle's error, level and trace, state for state
+@pytest.mark.parametrize("key,kw,kind,what", [
+    ("variant3", dict(variant=3), "assertion", "C2"),          # KubeAPI.tla:598-599
+    ("variant4", dict(variant=4), "invariant", "TypeOK"),      # :776-781 (IsValidListRequest)
+    ("variant5", dict(variant=5), "invariant", "OnlyOneVersion"),  # an Init state (:455)
+    ("ns0", dict(ns=0), "deadlock", None),                     # launch:16, no API server
+])
+def test_error_paths(fixtures, key, kw, kind, what):
+    fx = fixtures[key]
+    with ModelChecker(ModelConfig(**kw)) as mc:
+        r = mc.run()
+    assert r.error == kind and not r.complete
+    if kind == "assertion":
+        assert r.error_action == what == fx["err_action"]
+    if kind == "invariant":
+        assert r.error_invariant == what and fx["err_invariant"] == {"TypeOK": 0, "OnlyOneVersion": 1}[what]
+    assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
+    assert [list(map(int, t)) for t in r.trace] == fx["trace"]
+    assert r.level_width == fx["level_width"][:len(r.level_width)]
+
+
+def test_error_without_trace_store():
+    # keep_trace=False (no parent pointers): the violation is still reported
+    with ModelChecker(ModelConfig(variant=3, keep_trace=False)) as mc:
+        r = mc.run()
+    assert r.error == "assertion" and r.error_action == "C2" and r.error_level == 23
+    assert r.trace_len == 0 and r.trace == []
+
+
+@pytest.mark.parametrize("key,kw", [("ns0_nodeadlock", dict(ns=0, check_deadlock=False)),
+                                    ("variant4_oov_only", dict(variant=4, invariants=2)),
+                                    ("variant5_no_invariants", dict(variant=5, invariants=0))])
+def test_config_switches(fixtures, key, kw):
+    # -deadlock and the .cfg INVARIANT list: unlisted checks are not reported
+    fx = fixtures[key]
+    r = run(**kw)
+    assert r.complete and r.error is None
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]

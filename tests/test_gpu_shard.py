@@ -24,13 +24,19 @@ def emulate(R, **kw):
     widths, err = [n], NONE_KEY
     while True:
         sends, counts = [], []
+        init_err = NONE_KEY
         for s in shards:
             c, e = s.expand()
+            if (e & 0xFF) == 0x12 and e != NONE_KEY:
+                init_err = min(init_err, e)       # Init violations precede level-2 errors
             err = min(err, e)
             buf = torch.empty(max(sum(c), 1) * rb // 8, dtype=torch.int64, device="cuda")
             s.pack(buf)
             sends.append(buf)
             counts.append(c)
+        if init_err != NONE_KEY:
+            err = init_err
+            break
         total = 0
         for r, s in enumerate(shards):
             parts, m = [], 0
@@ -68,14 +74,21 @@ def test_model1_any_shard_count(fixtures, R):
     assert r["act_gen"] == fx["act_gen"]
 
 
-@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("R", [2, 3, 9])
 def test_errors_sharded(fixtures, R):
+    # R = 9: error keys of ranks >= 8 are >= 2^63
     r = emulate(R, nc=2)
     assert r["err"] & 0xFF == 1 and len(r["level_width"]) == 10
     assert r["level_width"] == fixtures["nc2"]["level_width"]
     r = emulate(R, variant=2)
     assert r["err"] & 0xFF == 2
     assert len(r["level_width"]) + 1 == fixtures["variant2"]["err_level"]
+    r = emulate(R, variant=3)
+    assert r["err"] & 0xFF == 1 and len(r["level_width"]) == fixtures["variant3"]["err_level"]
+    r = emulate(R, ns=0)
+    assert r["err"] & 0xFF == 3 and len(r["level_width"]) == fixtures["ns0"]["err_level"]
+    r = emulate(R, variant=5)                 # an Init state violates OnlyOneVersion
+    assert r["err"] & 0xFF == 0x12 and len(r["level_width"]) == 1
 
 
 def test_enlarged_prefix_sharded(fixtures):
@@ -132,5 +145,12 @@ def test_driver_world1_rccl(fixtures):
         cfg2 = ModelConfig(nc=2)
         r2 = ShardedModelChecker(cfg2, HipShard(cfg2, 0, 1)).run()
         assert r2["error"] == "assertion" and r2["trace"] == fixtures["nc2"]["trace"]
+        for key, kw, kind in (("variant5", dict(variant=5), "invariant"),
+                              ("ns0", dict(ns=0), "deadlock"),
+                              ("variant4", dict(variant=4), "invariant")):
+            c = ModelConfig(**kw)
+            r3 = ShardedModelChecker(c, HipShard(c, 0, 1)).run()
+            assert r3["error"] == kind and r3["trace_len"] == fixtures[key]["trace_len"]
+            assert r3["error_level"] == fixtures[key]["err_level"]
     finally:
         dist.destroy_process_group()

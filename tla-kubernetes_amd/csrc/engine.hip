@@ -66,13 +66,15 @@ __global__ void k_level_reset(Counters* __restrict__ C) {
 
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
 
+constexpr uint64_t kMaxChunk = (1ull << 27) - 256;
+
 template <class M>
 class EngineT final : public EngineBase {
   using State = typename M::State;
 
  public:
   explicit EngineT(const kc_model_config& cfg) : EngineBase(cfg) {
-    flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
+    flags_ = flags_of(cfg);
     timing_ = cfg.timing == 2 ? 2 : (cfg.timing != 0 ? 1 : 0);
     const char* ab = getenv("KC_ABLATE");
     ablate_ = ab && ab[0] == '1';
@@ -117,7 +119,7 @@ class EngineT final : public EngineBase {
     std::vector<uint64_t> fps(ni);
     uint64_t cand = 0;
     for (int k = 0; k < ni; ++k) {
-      M::init_state(k, init[k]);
+      M::init_state(k, init[k], cfg_.variant);
       fps[k] = M::fingerprint(init[k]);
       cand += (uint64_t)M::plan(init[k], flags_).total;
     }
@@ -168,7 +170,7 @@ class EngineT final : public EngineBase {
     res->nlevels = 1;
     // invariants of the initial states
     for (int k = 0; k < ni; ++k) {
-      const int inv = M::check(init[k]);
+      const int inv = M::check(init[k], flags_.inv_mask);
       if (inv >= 0) {
         res->err_kind = E_INVARIANT;
         res->err_invariant = inv;
@@ -185,7 +187,10 @@ class EngineT final : public EngineBase {
     // so a chunk's winners are final once its own claim pass is done.
     // per-level counter fields: err_key = ~0, the rest 0 (act_* are cumulative)
     hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
-    const uint64_t chunk = ((cfg_.chunk_states ? cfg_.chunk_states : (1ull << 40)) + 255) / 256 * 256;
+    // <= 2^27 parents per chunk: the chunk's scan runs on int counts and its
+    // offsets are u32 (at most 32 new states per parent: < 2^32 per chunk)
+    const uint64_t chunk =
+        (std::min<uint64_t>(cfg_.chunk_states ? cfg_.chunk_states : kMaxChunk, kMaxChunk) + 255) / 256 * 256;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
       if (n >= (1ull << 32)) {
@@ -382,9 +387,15 @@ class EngineT final : public EngineBase {
       return -EIO;
     }
     res->err_kind = kind;
-    // path to the parent through the parent pointers
+    // path to the parent through the parent pointers (TLC's trace file);
+    // without them only the parent itself, still in the current frontier
     std::vector<State> path;
-    KC_TRY(path_to(level_gidx + pidx, path));
+    if (cfg_.keep_trace) {
+      KC_TRY(path_to(level_gidx + pidx, path));
+    } else {
+      path.resize(1);
+      KC_HIP_TRY(hipMemcpy(&path[0], cur_ + pidx, sizeof(State), hipMemcpyDeviceToHost));
+    }
     const State& s = path.back();
     const typename M::Plan pl = M::plan(s, flags_);
     if (kind == E_ASSERT) {
@@ -398,14 +409,16 @@ class EngineT final : public EngineBase {
       M::locate(pl, pos, slot, j);
       State x;
       M::apply(s, slot, j, flags_, x);
-      res->err_invariant = M::check(x);
+      res->err_invariant = M::check(x, flags_.inv_mask);
       path.push_back(x);
       res->err_level = level + 1;
     } else {
       res->err_level = level;
     }
-    trace_ = path;
-    res->trace_len = (int)path.size();
+    if (cfg_.keep_trace) {
+      trace_ = path;
+      res->trace_len = (int)path.size();
+    }
     return 0;
   }
 
@@ -549,6 +562,7 @@ void kc_model_config_default(kc_model_config* c) {
   c->can_fail = c->can_timeout = 1;
   c->check_deadlock = 1;
   c->keep_trace = 1;
+  c->invariants = 3;
 }
 
 int kc_engine_create(const kc_model_config* cfg, kc_engine** out) {

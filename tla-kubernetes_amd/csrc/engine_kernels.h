@@ -471,7 +471,7 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
       parent[next_gidx + o] = level_gidx + pidx;
       ord[next_gidx + o] = (uint8_t)t;
     }
-    if (M::check(x) >= 0)
+    if (M::check(x, f.inv_mask) >= 0)
       atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
     atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
     const typename M::Plan px = M::plan(x, f);

@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/kubecheck.h"
 #include "kc_common.h"
+#include "kubeapi_spec.h"
 
 namespace kc {
 
@@ -24,6 +26,14 @@ int grow_buffer(T*& p, uint64_t& cap, uint64_t need, bool keep, hipStream_t st) 
   p = np;
   cap = nc;
   return 0;
+}
+
+// Run-time switches of a model config (constants, seeded variant,
+// invariants to check: 0 = none, as TLC with no INVARIANT in the .cfg).
+inline Flags flags_of(const kc_model_config& c) {
+  Flags f{c.can_fail, c.can_timeout, c.variant};
+  f.inv_mask = c.invariants & 3;
+  return f;
 }
 
 }  // namespace kc

@@ -5,11 +5,14 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <condition_variable>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/kubecheck.h"
 #include "engine_kernels.h"
+#include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
 
@@ -248,11 +251,32 @@ __global__ void k_contains(const uint64_t* __restrict__ fps, uint64_t n,
   if (i < n) seen[i] = (uint8_t)fpset_contains(slots, nbuckets, fps[i]);
 }
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9e3779b97f4a7c15ull;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
+}
+// Stress fingerprints: fp = perm63(seed + i), a
+// bijection of [0, 2^63) (xor-shifts and odd multiplies mod 2^63), so
+// distinct stream inputs give distinct, already-normalised fingerprints
+// (MSB clear, never 0 for a nonzero input).  The insert stream is inputs
+// seed + [0, n_ins); a lookup j is present for even j (input seed +
+// splitmix64(j) % n_ins) and absent for odd j (input seed + n_ins + j), so
+// a run's size and found counts are known exactly: n_ins and ceil(n_lookup/2).
+__host__ __device__ __forceinline__ uint64_t perm63(uint64_t x) {
+  constexpr uint64_t M = 0x7fffffffffffffffull;
+  x &= M;
+  x ^= x >> 31; x = (x * 0x9e3779b97f4a7c15ull) & M;
+  x ^= x >> 29; x = (x * 0xbf58476d1ce4e5b9ull) & M;
+  x ^= x >> 32; x = (x * 0x94d049bb133111ebull) & M;
+  return x ^ (x >> 30);
+}
+__host__ __device__ __forceinline__ uint64_t stress_insert_fp(uint64_t seed, uint64_t i) {
+  return perm63(seed + i);
+}
+__host__ __device__ __forceinline__ uint64_t stress_lookup_fp(uint64_t seed, uint64_t n_ins, uint64_t j) {
+  return perm63((j & 1) ? seed + n_ins + j : seed + splitmix64(j) % n_ins);
 }
 // Stress insert: fingerprints generated in registers (no input traffic).
 __global__ void __launch_bounds__(256)
@@ -260,25 +284,111 @@ k_stress_insert(uint64_t seed, uint64_t start, uint64_t n, unsigned long long* _
                 uint64_t nbuckets, unsigned long long* __restrict__ stats) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long nw = 0;
-  if (i < n) nw = fpset_insert(slots, nbuckets, normalize_fp(splitmix64(seed + start + i))) == 1;
+  if (i < n) nw = fpset_insert(slots, nbuckets, stress_insert_fp(seed, start + i)) == 1;
   const unsigned long long b = __ballot(nw != 0);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[0], (unsigned long long)__popcll(b));
 }
-// Stress lookup: even i -> an inserted fp, odd i -> one from a second stream.
+// Stress lookup of lookup-stream entries [start, start + n).
 __global__ void __launch_bounds__(256)
-k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t n, const unsigned long long* __restrict__ slots,
-                uint64_t nbuckets, unsigned long long* __restrict__ stats) {
+k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t start, uint64_t n,
+                const unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                unsigned long long* __restrict__ stats) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long f = 0;
-  if (i < n) {
-    const uint64_t z = (i & 1) ? splitmix64(seed ^ 0x5bd1e9955bd1e995ull) + i
-                               : seed + (splitmix64(i) % n_ins);
-    const uint64_t fp = normalize_fp((i & 1) ? splitmix64(z) : splitmix64(z));
-    f = fpset_contains(slots, nbuckets, fp);
-  }
+  if (i < n) f = fpset_contains(slots, nbuckets, stress_lookup_fp(seed, n_ins, start + i));
   const unsigned long long b = __ballot(f != 0);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[2], (unsigned long long)__popcll(b));
 }
+// The same streams written to memory (the sharded stress exchanges them).
+__global__ void k_stress_gen(uint64_t seed, int kind, uint64_t n_ins, uint64_t start, uint64_t n,
+                             uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n)
+    out[i] = kind == 0 ? stress_insert_fp(seed, start + i) : stress_lookup_fp(seed, n_ins, start + i);
+}
+// Bulk insert / lookup of fingerprints in memory, counting new / found.
+__global__ void __launch_bounds__(256)
+k_insert_count(const uint64_t* __restrict__ fps, uint64_t n, unsigned long long* __restrict__ slots,
+               uint64_t nbuckets, unsigned long long* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int r = 0;
+  if (i < n) r = fpset_insert(slots, nbuckets, normalize_fp(fps[i]));
+  const unsigned long long bw = __ballot(r == 1), bf = __ballot(r < 0);
+  if ((threadIdx.x & 63) == 0) {
+    if (bw) atomicAdd(&stat_row(stats)[0], (unsigned long long)__popcll(bw));
+    if (bf) atomicAdd(&stat_row(stats)[1], (unsigned long long)__popcll(bf));
+  }
+}
+__global__ void __launch_bounds__(256)
+k_contains_count(const uint64_t* __restrict__ fps, uint64_t n, const unsigned long long* __restrict__ slots,
+                 uint64_t nbuckets, unsigned long long* __restrict__ stats) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int f = 0;
+  if (i < n) f = fpset_contains(slots, nbuckets, normalize_fp(fps[i]));
+  const unsigned long long b = __ballot(f != 0);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[2], (unsigned long long)__popcll(b));
+}
+
+// ------------------------------------------------------- owner partition
+// Stable counting sort of a batch of fingerprints by owner rank
+// floor(fp * R / 2^63) (the sharded FPSet's routing step, like the BFS
+// records: engine_kernels.h owner_of).  One workgroup = PART_TILE
+// consecutive fps; pass 1 counts per (owner, tile), one exclusive scan over
+// the owner-major matrix gives each tile's base, pass 2 scatters in input
+// order (wave ballots rank the lanes of one owner, LDS carries the running
+// per-owner offset across the tile's rounds).
+constexpr int PART_TILE = 4096;
+constexpr int PART_MAXR = 16;
+__device__ __forceinline__ uint32_t part_owner(uint64_t fp, uint32_t world) {
+  return owner_of(normalize_fp(fp), world);
+}
+__global__ void __launch_bounds__(256)
+k_part_count(const uint64_t* __restrict__ fps, uint64_t n, uint32_t world, uint32_t ntiles,
+             uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[PART_MAXR];
+  if (threadIdx.x < PART_MAXR) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE;
+  for (int k = threadIdx.x; k < PART_TILE; k += 256) {
+    const uint64_t i = t0 + k;
+    if (i < n) atomicAdd(&h[part_owner(fps[i], world)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < world) cnt[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+__global__ void __launch_bounds__(256)
+k_part_scatter(const uint64_t* __restrict__ fps, uint64_t n, uint32_t world, uint32_t ntiles,
+               const uint32_t* __restrict__ off, uint64_t* __restrict__ out) {
+  __shared__ uint32_t run[PART_MAXR];
+  __shared__ uint32_t wcnt[4][PART_MAXR];
+  if (threadIdx.x < world) run[threadIdx.x] = off[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1;
+  const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE;
+  for (int k = 0; k < PART_TILE; k += 256) {
+    const uint64_t i = t0 + k + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t fp = live ? fps[i] : 0;
+    const uint32_t o = live ? part_owner(fp, world) : PART_MAXR;
+    uint32_t r = 0;
+    for (uint32_t q = 0; q < world; ++q) {
+      const uint64_t m = __ballot(o == q);
+      if (o == q) r = (uint32_t)__popcll(m & lt);
+      if (lane == 0) wcnt[wv][q] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (live) {
+      uint32_t pos = run[o] + r;
+      for (int w = 0; w < wv; ++w) pos += wcnt[w][o];
+      out[pos] = fp;
+    }
+    __syncthreads();
+    if (threadIdx.x < world)
+      run[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+    __syncthreads();
+  }
+}
+
 __global__ void k_compact_fps(const unsigned long long* __restrict__ slots, uint64_t nslots,
                               unsigned long long* __restrict__ out, unsigned long long* __restrict__ n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -294,6 +404,18 @@ __global__ void k_min_gap(const unsigned long long* __restrict__ s, uint64_t n,
 
 using namespace kc;
 
+// Flat-combining state of the single-fingerprint put/contains (below).
+struct Combiner {
+  struct Req { uint64_t fp; int op; uint64_t ticket; };
+  struct Res { uint8_t seen; int rc; };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Req> pending;
+  std::unordered_map<uint64_t, Res> done;
+  uint64_t next_ticket = 0, rounds = 0;
+  bool busy = false;
+};
+
 struct kc_fpset {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -303,7 +425,12 @@ struct kc_fpset {
   uint8_t* d_seen = nullptr;
   uint64_t stage_cap = 0;
   unsigned long long* d_stats = nullptr;  // STAT_ROWS rows of [new, full, found, -]
+  uint32_t *part_cnt = nullptr, *part_off = nullptr;   // owner partition scratch
+  uint64_t part_cap = 0, part_off_cap = 0;
+  uint8_t* scan_tmp = nullptr;
+  uint64_t scan_cap = 0;
   std::mutex mu;
+  Combiner comb;
 };
 
 // Sum the striped stats rows (syncs the stream).
@@ -389,6 +516,8 @@ void kc_fpset_destroy(kc_fpset* s) {
   if (s->d_fps) (void)hipFree(s->d_fps);
   if (s->d_seen) (void)hipFree(s->d_seen);
   if (s->d_stats) (void)hipFree(s->d_stats);
+  for (void* p : {(void*)s->part_cnt, (void*)s->part_off, (void*)s->scan_tmp})
+    if (p) (void)hipFree(p);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -495,9 +624,19 @@ int kc_fpset_check_fps(kc_fpset* s, uint64_t* min_gap_out, double* prob_out) {
   return 0;
 }
 
+static bool stress_args_ok(uint64_t seed, uint64_t n, uint64_t n_lookup) {
+  // every stream input seed + x (x < n + n_lookup) must lie in [1, 2^63)
+  const uint64_t M = 0x7fffffffffffffffull;
+  return seed >= 1 && seed <= M && n <= M - seed && n_lookup <= M - seed - n;
+}
+
 int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint64_t n_lookup,
                     double* insert_seconds, double* lookup_seconds, uint64_t* found_out) {
-  if (!s || batch == 0) { set_error("kc_fpset_stress: bad argument"); return -EINVAL; }
+  if (!s || batch == 0 || !stress_args_ok(seed, n, n_lookup) || (n_lookup && !n)) {
+    set_error("kc_fpset_stress: bad argument (batch > 0, 1 <= seed, seed + n + n_lookup < 2^63, "
+              "lookups need inserts)");
+    return -EINVAL;
+  }
   std::lock_guard<std::mutex> g(s->mu);
   KC_HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = s->stream;
@@ -517,7 +656,7 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   for (uint64_t off = 0; off < n_lookup; off += batch) {
     const uint64_t m = std::min(batch, n_lookup - off);
     hipLaunchKernelGGL(k_stress_lookup, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
-                       seed + 0, n, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+                       seed, n, off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
   }
   KC_HIP_TRY(hipEventRecord(e2, st));
   KC_HIP_TRY(hipGetLastError());
@@ -535,5 +674,176 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   if (found_out) *found_out = stats[2];
   return 0;
 }
+
+int kc_stress_fps_dev(uint64_t seed, int kind, uint64_t n_ins, uint64_t start, uint64_t n,
+                      uint64_t* out_dev, void* hs) {
+  if ((n && !out_dev) || (kind != 0 && kind != 1) || (kind == 1 && n_ins == 0) ||
+      !stress_args_ok(seed, kind == 0 ? start + n : n_ins, kind == 0 ? 0 : start + n)) {
+    set_error("kc_stress_fps_dev: bad argument");
+    return -EINVAL;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_stress_gen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)hs,
+                     seed, kind, n_ins, start, n, out_dev);
+  KC_HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+uint64_t kc_stress_fp(uint64_t seed, int kind, uint64_t n_ins, uint64_t i) {
+  return kind == 0 ? stress_insert_fp(seed, i) : stress_lookup_fp(seed, n_ins ? n_ins : 1, i);
+}
+
+int kc_fpset_partition_dev(kc_fpset* s, const uint64_t* fps_dev, uint64_t n, int world,
+                           uint64_t* out_dev, uint64_t* counts_out, void* hs) {
+  if (!s || world < 1 || world > PART_MAXR || !counts_out || (n && (!fps_dev || !out_dev)) ||
+      fps_dev == out_dev) {
+    set_error("kc_fpset_partition_dev: bad argument (1 <= world <= %d, distinct buffers)", PART_MAXR);
+    return -EINVAL;
+  }
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = hs ? (hipStream_t)hs : s->stream;
+  for (int o = 0; o < world; ++o) counts_out[o] = 0;
+  if (n == 0) return 0;
+  const uint64_t ntiles = (n + PART_TILE - 1) / PART_TILE;
+  const uint64_t cells = ntiles * (uint64_t)world;
+  if (cells >= (1ull << 31) || n >= (1ull << 32)) {
+    set_error("kc_fpset_partition_dev: batch too large (< 2^32 fingerprints)");
+    return -EINVAL;
+  }
+  KC_TRY(grow_buffer(s->part_cnt, s->part_cap, cells + 1, false, st));
+  KC_TRY(grow_buffer(s->part_off, s->part_off_cap, cells + 1, false, st));
+  hipLaunchKernelGGL(k_part_count, dim3((unsigned)ntiles), dim3(256), 0, st, fps_dev, n, (uint32_t)world,
+                     (uint32_t)ntiles, s->part_cnt);
+  size_t tmp_bytes = 0;
+  KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s->part_cnt, s->part_off, (int)cells, st));
+  KC_TRY(grow_buffer(s->scan_tmp, s->scan_cap, tmp_bytes + 16, false, st));
+  KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tmp_bytes, s->part_cnt, s->part_off, (int)cells, st));
+  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)ntiles), dim3(256), 0, st, fps_dev, n, (uint32_t)world,
+                     (uint32_t)ntiles, s->part_off, out_dev);
+  KC_HIP_TRY(hipGetLastError());
+  // per-owner totals: the owner-major scan's bases (owner o starts at
+  // off[o * ntiles]); the last owner ends at n
+  std::vector<uint32_t> base(world);
+  for (int o = 0; o < world; ++o)
+    KC_HIP_TRY(hipMemcpyAsync(&base[o], s->part_off + (uint64_t)o * ntiles, 4, hipMemcpyDeviceToHost, st));
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  for (int o = 0; o < world; ++o)
+    counts_out[o] = (o + 1 < world ? (uint64_t)base[o + 1] : n) - base[o];
+  return 0;
+}
+
+static int count_dev(kc_fpset* s, const uint64_t* fps_dev, size_t n, uint64_t* out, void* hs, bool insert) {
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = hs ? (hipStream_t)hs : s->stream;
+  if (insert) KC_TRY(s->fs.reserve(n, st));
+  KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, STAT_BYTES, st));
+  if (n) {
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (insert)
+      hipLaunchKernelGGL(k_insert_count, dim3(grid), dim3(256), 0, st, fps_dev, (uint64_t)n, s->fs.slots,
+                         s->fs.nbuckets, s->d_stats);
+    else
+      hipLaunchKernelGGL(k_contains_count, dim3(grid), dim3(256), 0, st, fps_dev, (uint64_t)n,
+                         s->fs.slots, s->fs.nbuckets, s->d_stats);
+    KC_HIP_TRY(hipGetLastError());
+  }
+  unsigned long long stats[4];
+  KC_TRY(read_stats(s, st, stats));
+  if (stats[1]) {
+    set_error("fpset full");
+    return -ENOMEM;
+  }
+  if (insert) s->fs.count += stats[0];
+  *out = insert ? stats[0] : stats[2];
+  return 0;
+}
+
+int kc_fpset_insert_count_dev(kc_fpset* s, const uint64_t* fps_dev, size_t n, uint64_t* n_new_out, void* hs) {
+  if (!s || !n_new_out || (n && !fps_dev)) { set_error("kc_fpset_insert_count_dev: bad argument"); return -EINVAL; }
+  return count_dev(s, fps_dev, n, n_new_out, hs, true);
+}
+
+int kc_fpset_contains_count_dev(kc_fpset* s, const uint64_t* fps_dev, size_t n, uint64_t* found_out, void* hs) {
+  if (!s || !found_out || (n && !fps_dev)) { set_error("kc_fpset_contains_count_dev: bad argument"); return -EINVAL; }
+  return count_dev(s, fps_dev, n, found_out, hs, false);
+}
+
+// ---- single-fingerprint put/contains from many host threads (flat combining)
+// TLC's workers call FPSet.put(long) concurrently, one fingerprint each
+// (MC.out:5 "4 workers").  A caller enqueues its request; if no batch is in
+// flight it becomes the combiner: it takes every pending request (in arrival
+// order), runs them as ONE put_batch launch (equal fps inside resolve in
+// arrival order, as sequential puts would), publishes the results and
+// repeats while requests are pending.  Other callers just wait for their
+// result, so N concurrent workers cost one kernel launch per round, not N.
+static int combine_one(kc_fpset* s, uint64_t fp, int op, uint8_t* result) {
+  Combiner& c = s->comb;
+  std::unique_lock<std::mutex> lk(c.mu);
+  const uint64_t ticket = c.next_ticket++;
+  c.pending.push_back({fp, op, ticket});
+  for (;;) {
+    auto it = c.done.find(ticket);
+    if (it != c.done.end()) {
+      const int rc = it->second.rc;
+      *result = it->second.seen;
+      c.done.erase(it);
+      return rc;
+    }
+    if (!c.busy) break;
+    c.cv.wait(lk);
+  }
+  // become the combiner
+  c.busy = true;
+  while (!c.pending.empty()) {
+    std::vector<Combiner::Req> batch;
+    batch.swap(c.pending);
+    lk.unlock();
+    // puts and contains keep their relative order: consecutive runs of the
+    // same op go out as one batch each
+    std::vector<uint8_t> seen(batch.size());
+    std::vector<int> rcs(batch.size(), 0);
+    size_t a = 0;
+    while (a < batch.size()) {
+      size_t b = a;
+      std::vector<uint64_t> fps;
+      while (b < batch.size() && batch[b].op == batch[a].op) fps.push_back(batch[b++].fp);
+      const int rc = batch[a].op == 0 ? kc_fpset_put_batch(s, fps.data(), fps.size(), seen.data() + a)
+                                      : kc_fpset_contains_batch(s, fps.data(), fps.size(), seen.data() + a);
+      for (size_t k = a; k < b; ++k) rcs[k] = rc;
+      a = b;
+    }
+    lk.lock();
+    ++c.rounds;
+    for (size_t k = 0; k < batch.size(); ++k) c.done[batch[k].ticket] = {seen[k], rcs[k]};
+    c.cv.notify_all();
+  }
+  c.busy = false;
+  auto it = c.done.find(ticket);
+  const int rc = it->second.rc;
+  *result = it->second.seen;
+  c.done.erase(it);
+  c.cv.notify_all();
+  return rc;
+}
+
+int kc_fpset_put(kc_fpset* s, uint64_t fp, int* seen_out) {
+  if (!s || !seen_out) { set_error("kc_fpset_put: NULL"); return -EINVAL; }
+  uint8_t r = 0;
+  const int rc = combine_one(s, fp, 0, &r);
+  *seen_out = r;
+  return rc;
+}
+
+int kc_fpset_contains(kc_fpset* s, uint64_t fp, int* seen_out) {
+  if (!s || !seen_out) { set_error("kc_fpset_contains: NULL"); return -EINVAL; }
+  uint8_t r = 0;
+  const int rc = combine_one(s, fp, 1, &r);
+  *seen_out = r;
+  return rc;
+}
+
+uint64_t kc_fpset_combine_rounds(const kc_fpset* s) { return s ? s->comb.rounds : 0; }
 
 }  // extern "C"

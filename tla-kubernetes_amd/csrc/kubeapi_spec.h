@@ -65,10 +65,19 @@ enum Ident : int { ID_Secret = 0, ID_PVC = 1 };
 enum ErrKind : int { E_NONE = 0, E_ASSERT = 1, E_INVARIANT = 2, E_DEADLOCK = 3 };
 
 // run-time switches (MC.tla constants and build-authored variants)
+//   variant 0 = KubeAPI.tla as written.  Seeded bugs (build-authored, each
+//   exercising one error path of the checker; the oracle has the same):
+//   1 = Update without the HasRead check (:733)        -> lost updates
+//   2 = Force adds without replacing (:706-715)         -> OnlyOneVersion
+//   3 = C1 ignores the Force reply status (:553)        -> C2 Assert (:598-599)
+//   4 = list replies ignore the kind filter (:747)      -> TypeOK (:433-435)
+//   5 = Init store already holds two Secret versions    -> Init violates
+//       (a pre-corrupted apiState, :456)                   OnlyOneVersion
 struct Flags {
   int can_fail;      // REQUESTS_CAN_FAIL
   int can_timeout;   // REQUESTS_CAN_TIMEOUT
-  int variant;       // 0 = as written; 1 = Update w/o HasRead; 2 = Force w/o replace
+  int variant;
+  int inv_mask = 3;  // invariants checked (MC.cfg INVARIANT): bit 0 TypeOK, bit 1 OnlyOneVersion
 };
 
 KC_HD constexpr int ceil_log2(int x) { return x <= 1 ? 0 : 1 + ceil_log2((x + 1) / 2); }
@@ -116,7 +125,7 @@ struct Model {
   static constexpr int U = 1 << UB;             // object universe size
   static constexpr int NOBJ = 3 + U;            // objcode values
   static constexpr int OBJB = ceil_log2(NOBJ);  // objcode bits
-  static_assert(A >= 1 && A <= 4 && NS >= 1, "KubeAPI model: 1..4 actors, >=1 server");
+  static_assert(A >= 1 && A <= 4 && NS >= 0, "KubeAPI model: 1..4 actors");
   static constexpr int OBJ_PER_WORD = 64 / U;   // listRequests objs masks per word
   static constexpr int OBJ_WORDS = (A + OBJ_PER_WORD - 1) / OBJ_PER_WORD;
   static constexpr int W_RAW = 1 + A + OBJ_WORDS;
@@ -265,9 +274,11 @@ struct Model {
   // Init (KubeAPI.tla:455-469): 2^NC states, shouldReconcile enumerated as a
   // binary counter (client 0 least significant, FALSE first).
   KC_HD static int num_init() { return 1 << NC; }
-  KC_HD static void init_state(int k, State& s) {
+  KC_HD static void init_state(int k, State& s, int variant = 0) {
 #pragma unroll
     for (int i = 0; i < W; ++i) s.w[i] = 0;
+    // variant 5: Secret/foo stored twice (vv {} and vv {actor 0})
+    if (variant == 5) s.w[0] = (1ull << u_make(ID_Secret, 0, 0)) | (1ull << u_make(ID_Secret, 0, 1));
     static_for<A>([&](auto AI) {
       constexpr int a = AI;
       put<a>(s, F_PC, B_PC, is_client(a) ? L_CStart : L_PVCStart);
@@ -488,7 +499,8 @@ struct Model {
             break;
           }
           case L_C1:                                            // :551-556
-            w = sw(w, F_PC, B_PC, g(w, F_RQST, 2) != ST_Ok ? L_CStart : L_C10); break;
+            // variant 3 (seeded bug): the Force reply status is ignored
+            w = sw(w, F_PC, B_PC, (g(w, F_RQST, 2) != ST_Ok && f.variant != 3) ? L_CStart : L_C10); break;
           case L_C10: w = call_w(w, L_C11, OP_Force, oc_bare(ID_PVC)); break;   // :558-568
           case L_C11:                                           // :570-575
             w = sw(w, F_PC, B_PC, g(w, F_RQST, 2) != ST_Ok ? L_CStart : L_c12); break;
@@ -582,7 +594,8 @@ struct Model {
     if (plr) {                                                  // :745-753
       const int c = nth_bit(plr, j - nrq);
       const uint64_t km = kind_mask(g(aw_d(s, c), F_LRK, 2));
-      set_objs_d(t, c, api & km);
+      // variant 4 (seeded bug): the reply lists every object, any kind
+      set_objs_d(t, c, f.variant == 4 ? api : (api & km));
       put_word_d(t, c, sw(aw_d(s, c), F_LRST, 2, ST_Ok));
       t.w[0] = read_map(api, km, c);
       return c;
@@ -604,8 +617,10 @@ struct Model {
 
   // ------------------------------------------------------------ invariants
   // Returns -1 if TypeOK (:776-781) and OnlyOneVersion (:787-789) hold, else
-  // the index of the first violated one in MC.cfg order (0 TypeOK, 1 OOV).
-  KC_HD static int check(const State& s) {
+  // the index of the first violated one in MC.cfg order (0 TypeOK, 1 OOV);
+  // only the invariants in `mask` (Flags::inv_mask) are evaluated.
+  KC_HD static int check(const State& s, int mask = 3) {
+    if (!mask) return -1;
     bool typeok = true;
     static_for<A>([&](auto CI) {
       constexpr int c = CI;
@@ -620,8 +635,8 @@ struct Model {
           typeok = false;
       }
     });
-    if (!typeok) return 0;
-    if (popc(s.w[0] & id_mask(0)) > 1 || popc(s.w[0] & id_mask(1)) > 1) return 1;
+    if (!typeok && (mask & 1)) return 0;
+    if ((mask & 2) && (popc(s.w[0] & id_mask(0)) > 1 || popc(s.w[0] & id_mask(1)) > 1)) return 1;
     return -1;
   }
 
@@ -796,6 +811,7 @@ struct Model {
 
 // Supported instantiations (NC, NP, NS); the engine dispatches on these.
 #define KC_FOR_EACH_MODEL(X) \
-  X(1, 1, 1) X(2, 1, 1) X(1, 2, 1) X(2, 0, 1) X(1, 1, 2) X(1, 3, 1) X(2, 2, 1) X(1, 0, 1) X(0, 1, 1)
+  X(1, 1, 1) X(2, 1, 1) X(1, 2, 1) X(2, 0, 1) X(1, 1, 2) X(1, 3, 1) X(2, 2, 1) X(1, 0, 1) X(0, 1, 1) \
+  X(1, 1, 0)
 
 }  // namespace kc

@@ -229,7 +229,7 @@ k_shard_emit_local(const typename M::State* __restrict__ cur, uint64_t n, Flags 
         const int act = M::slot_action(s, slot);
         const uint64_t key = (rank << 60) | (i << 16) | ((uint64_t)t << 8);
         pkeys[next_gidx + o] = key | (uint64_t)act;
-        if (M::check(x) >= 0) atomicMin(&C->err_key, key | E_INVARIANT);
+        if (M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, key | E_INVARIANT);
         atomicAdd(&sh_act[act], 1u);
         cand += (unsigned long long)M::plan(x, f).total;
         ++o;
@@ -265,7 +265,7 @@ k_shard_emit_rec(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* _
     const uint64_t o = C->chunk_base + ioff[i];
     store_state<M>(next, o, x);
     pkeys[next_gidx + o] = key;
-    if (M::check(x) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
+    if (M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
     atomicAdd(&sh_act[key & 0xff], 1u);
     cand = (unsigned long long)M::plan(x, f).total;
   }
@@ -292,6 +292,7 @@ class ShardBase {
   virtual int parent_key(int level, uint64_t idx, uint64_t* key) = 0;
   virtual int frontier_tuple(uint64_t idx, uint64_t* out) = 0;
   virtual int result(kc_result* r) = 0;
+  virtual void claim_times(double* ms, uint64_t* launches, uint64_t* parents) = 0;
 };
 
 template <class M>
@@ -302,7 +303,7 @@ class ShardT final : public ShardBase {
  public:
   ShardT(const kc_model_config& cfg, int rank, int world)
       : cfg_(cfg), rank_(rank), world_(world) {
-    flags_ = Flags{cfg.can_fail, cfg.can_timeout, cfg.variant};
+    flags_ = flags_of(cfg);
   }
   ~ShardT() override { release(); }
 
@@ -326,7 +327,19 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
+    KC_HIP_TRY(hipEventCreate(&ev_[0]));
+    KC_HIP_TRY(hipEventCreate(&ev_[1]));
     return 0;
+  }
+
+  // k_claim time (HIP events, cfg.timing != 0), launches and parents since
+  // the last call to this function (reset on read).
+  void claim_times(double* ms, uint64_t* launches, uint64_t* parents) override {
+    *ms = claim_ms_;
+    *launches = claim_launches_;
+    *parents = claim_parents_;
+    claim_ms_ = 0;
+    claim_launches_ = claim_parents_ = 0;
   }
 
   int set_stream(hipStream_t st) override {
@@ -351,7 +364,7 @@ class ShardT final : public ShardBase {
     cand_ = 0;
     for (int k = 0; k < M::num_init(); ++k) {
       State s;
-      M::init_state(k, s);
+      M::init_state(k, s, cfg_.variant);
       const uint64_t fp = M::fingerprint(s);
       const uint32_t o = (uint32_t)(((unsigned __int128)(fp << 1) * (uint64_t)world_) >> 64);
       if ((int)o != rank_) continue;
@@ -359,7 +372,7 @@ class ShardT final : public ShardBase {
       keys.push_back(KEY_INIT | (uint64_t)k);
       fps.push_back(fp);
       cand_ += (uint64_t)M::plan(s, flags_).total;
-      if (M::check(s) >= 0 && init_err_ == ~0ull)
+      if (M::check(s, flags_.inv_mask) >= 0 && init_err_ == ~0ull)
         init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
     }
     n_ = mine.size();
@@ -414,13 +427,20 @@ class ShardT final : public ShardBase {
     sh.repmask = repmask_;
     sh.cnt = cnt_;
     const size_t dyn = (size_t)(CLAIM_TILE + ((world_ + 3) / 4) * CLAIM_TILE) * sizeof(unsigned int);
+    if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[0], st_));
     hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
                        cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                        (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                        d_ctr_, sh);
+    if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[1], st_));
     // one exclusive scan over the owner-major matrix = every record's position
     // in the owner-grouped send buffer
     const uint64_t cells = n_ * (uint64_t)world_;
+    if (cells >= (1ull << 31)) {
+      set_error("kc_shard_expand: frontier x world = %llu cells exceeds one scan (2^31)",
+                (unsigned long long)cells);
+      return -ENOMEM;
+    }
     size_t tmp_bytes = 0;
     KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
     KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
@@ -431,6 +451,13 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipMemcpyAsync(h_owner_base_, d_owner_base_, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (cfg_.timing) {
+      float ms = 0;
+      KC_HIP_TRY(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+      claim_ms_ += ms;
+      ++claim_launches_;
+    }
+    claim_parents_ += n_;
     if (h_ctr_->overflow || h_ctr_->batch_used) {
       set_error("kc_shard_expand: successor overflow or full table");
       return -ENOMEM;
@@ -467,6 +494,10 @@ class ShardT final : public ShardBase {
     *err_key = ~0ull;
     next_n_ = 0;
     if (n_ == 0 && n == 0) return 0;
+    if (n >= (1ull << 31) || n_ >= (1ull << 31)) {
+      set_error("kc_shard_insert: more than 2^31 records or parents in one level");
+      return -ENOMEM;
+    }
     KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
     KC_TRY(cs_.reserve(cand_ + n, st_));     // count excludes this level's local inserts (<= cand_)
     const uint32_t succ_level = (uint32_t)level_ + 1;
@@ -601,6 +632,8 @@ class ShardT final : public ShardBase {
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_owner_base_) (void)hipHostFree(h_owner_base_);
+    for (auto& e : ev_)
+      if (e) (void)hipEventDestroy(e);
     if (st_ && own_st_) (void)hipStreamDestroy(st_);
   }
 
@@ -635,6 +668,9 @@ class ShardT final : public ShardBase {
   uint64_t init_err_ = ~0ull;
   int level_ = 0;
   std::vector<uint64_t> level_base_;
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  double claim_ms_ = 0;
+  uint64_t claim_launches_ = 0, claim_parents_ = 0;
 };
 
 std::unique_ptr<ShardBase> make_shard(const kc_model_config& cfg, int rank, int world) {
@@ -706,6 +742,11 @@ int kc_shard_frontier_tuple(kc_shard* s, uint64_t idx, uint64_t* out) {
 int kc_shard_result(kc_shard* s, kc_result* r) {
   if (!s || !r) { set_error("kc_shard_result: NULL"); return -EINVAL; }
   return s->impl->result(r);
+}
+int kc_shard_claim_times(kc_shard* s, double* ms, uint64_t* launches, uint64_t* parents) {
+  if (!s || !ms || !launches || !parents) { set_error("kc_shard_claim_times: NULL"); return -EINVAL; }
+  s->impl->claim_times(ms, launches, parents);
+  return 0;
 }
 int kc_shard_owner(uint64_t fp, int world) {
   if (world < 1) return -EINVAL;

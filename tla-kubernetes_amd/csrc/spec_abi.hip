@@ -11,6 +11,7 @@
 
 #include "../../include/kubecheck.h"
 #include "engine.h"
+#include "engine_util.h"
 #include "kc_common.h"
 #include "kubeapi_spec.h"
 
@@ -187,7 +188,7 @@ int kc_spec_init(const kc_model_config* cfg, uint64_t* out, int cap) {
     const int n = M::num_init();
     for (int k = 0; k < n && k < cap; ++k) {
       typename M::State s;
-      M::init_state(k, s);
+      M::init_state(k, s, cfg->variant);
       if (out) M::to_tuple(s, out + (size_t)k * M::TUPLE_WORDS);
     }
     return n;
@@ -201,7 +202,7 @@ int kc_spec_successors(const kc_model_config* cfg, const uint64_t* tuple, int* a
     using M = decltype(m);
     typename M::State s;
     if (!M::from_tuple(tuple, s)) { set_error("kc_spec_successors: tuple outside the lowered domain"); return -EINVAL; }
-    const Flags f{cfg->can_fail, cfg->can_timeout, cfg->variant};
+    const Flags f = flags_of(*cfg);
     const typename M::Plan pl = M::plan(s, f);
     if (fail_action) *fail_action = pl.fail_pos >= 0 ? M::slot_action(s, pl.fail_slot) : -1;
     for (int t = 0; t < pl.total && t < cap; ++t) {
@@ -222,7 +223,7 @@ int kc_spec_check(const kc_model_config* cfg, const uint64_t* tuple) {
     using M = decltype(m);
     typename M::State s;
     if (!M::from_tuple(tuple, s)) { set_error("kc_spec_check: bad tuple"); return -EINVAL; }
-    return M::check(s);
+    return M::check(s, flags_of(*cfg).inv_mask);
   });
 }
 
@@ -243,7 +244,7 @@ int kc_spec_fp_selfcheck(const kc_model_config* cfg, const uint64_t* tuple) {
     using M = decltype(m);
     typename M::State s;
     if (!M::from_tuple(tuple, s)) { set_error("kc_spec_fp_selfcheck: bad tuple"); return -EINVAL; }
-    const Flags f{cfg->can_fail, cfg->can_timeout, cfg->variant};
+    const Flags f = flags_of(*cfg);
     const typename M::Plan pl = M::plan(s, f);
     const uint64_t fold = M::fp_fold(s);
     int bad = 0;

@@ -27,7 +27,7 @@ from ._lib import (ACTIONS, ERR_KINDS, INVARIANTS, KcModelConfig, KcResult, Kube
                    check, load)
 
 __all__ = ["ModelConfig", "ModelChecker", "CheckResult", "FPSet", "StateQueue", "Spec",
-           "KubecheckError", "ACTIONS", "load", "device_count"]
+           "KubecheckError", "ACTIONS", "load", "device_count", "stress_fps_dev", "stress_fp"]
 
 
 def device_count() -> int:
@@ -43,7 +43,7 @@ class ModelConfig:
     can_fail: bool = True       # REQUESTS_CAN_FAIL    (MC.tla:5-7)
     can_timeout: bool = True    # REQUESTS_CAN_TIMEOUT (MC.tla:10-12)
     check_deadlock: bool = True # KubeAPI___Model_1.launch:16
-    variant: int = 0            # 1 = Update without HasRead (seeded lost-update bug)
+    variant: int = 0            # seeded bugs 1-5 (include/kubecheck.h); 0 = KubeAPI.tla as written
     device: int = 0
     keep_trace: bool = True
     max_levels: int = 0
@@ -51,6 +51,7 @@ class ModelConfig:
     chunk_states: int = 0
     verbose: int = 0
     timing: int = 0             # HIP-event timing (kernel_times()): 1 every kernel, 2 k_claim only
+    invariants: int = 3         # MC.cfg INVARIANT: bit 0 TypeOK, bit 1 OnlyOneVersion (0 = none)
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()
@@ -175,6 +176,21 @@ class ModelChecker:
             pass
 
 
+def _stream(stream):
+    return C.c_void_p(stream.cuda_stream if stream is not None else 0)
+
+
+def stress_fps_dev(seed: int, kind: int, n_ins: int, start: int, n: int, out, stream=None) -> None:
+    """Stress stream entries [start, start+n) into a device tensor
+    (kind 0 = inserts, 1 = lookups; kc_stress_fps_dev)."""
+    check("kc_stress_fps_dev", load().kc_stress_fps_dev(seed, kind, n_ins, start, n,
+                                                         C.c_void_p(out.data_ptr()), _stream(stream)))
+
+
+def stress_fp(seed: int, kind: int, n_ins: int, i: int) -> int:
+    return int(load().kc_stress_fp(seed, kind, n_ins, i))
+
+
 def _u64(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_uint64))
 
@@ -202,10 +218,43 @@ class FPSet:
         return seen.astype(bool)
 
     def put(self, fp: int) -> bool:
-        return bool(self.put_batch([fp])[0])
+        """TLC FPSet.put(long): thread-safe; concurrent callers are
+        flat-combined into one batch launch (kc_fpset_put)."""
+        seen = C.c_int()
+        check("kc_fpset_put", self._lib.kc_fpset_put(self._h, int(fp) & (2**64 - 1), C.byref(seen)))
+        return bool(seen.value)
 
     def contains(self, fp: int) -> bool:
-        return bool(self.contains_batch([fp])[0])
+        seen = C.c_int()
+        check("kc_fpset_contains", self._lib.kc_fpset_contains(self._h, int(fp) & (2**64 - 1), C.byref(seen)))
+        return bool(seen.value)
+
+    def combine_rounds(self) -> int:
+        """Batches launched so far by put()/contains()."""
+        return int(self._lib.kc_fpset_combine_rounds(self._h))
+
+    # -- device-resident batches (torch tensors of int64 on this set's GPU)
+    def insert_count_dev(self, fps, n: int, stream=None) -> int:
+        """Insert the first n fps of a device tensor; returns how many were new."""
+        out = C.c_uint64()
+        check("kc_fpset_insert_count_dev", self._lib.kc_fpset_insert_count_dev(
+            self._h, C.c_void_p(fps.data_ptr()), n, C.byref(out), _stream(stream)))
+        return int(out.value)
+
+    def contains_count_dev(self, fps, n: int, stream=None) -> int:
+        out = C.c_uint64()
+        check("kc_fpset_contains_count_dev", self._lib.kc_fpset_contains_count_dev(
+            self._h, C.c_void_p(fps.data_ptr()), n, C.byref(out), _stream(stream)))
+        return int(out.value)
+
+    def partition_dev(self, fps, n: int, world: int, out, stream=None) -> List[int]:
+        """Stable counting sort of n device fps by owner rank into `out`;
+        returns the per-owner counts."""
+        counts = (C.c_uint64 * world)()
+        check("kc_fpset_partition_dev", self._lib.kc_fpset_partition_dev(
+            self._h, C.c_void_p(fps.data_ptr()), n, world, C.c_void_p(out.data_ptr()), counts,
+            _stream(stream)))
+        return [int(x) for x in counts]
 
     def size(self) -> int:
         return int(self._lib.kc_fpset_size(self._h))

@@ -32,7 +32,7 @@ class KcModelConfig(C.Structure):
         ("can_fail", C.c_int), ("can_timeout", C.c_int), ("check_deadlock", C.c_int),
         ("variant", C.c_int), ("device", C.c_int), ("keep_trace", C.c_int),
         ("max_levels", C.c_int), ("fpset_slots", C.c_uint64), ("chunk_states", C.c_uint64),
-        ("verbose", C.c_int), ("timing", C.c_int),
+        ("verbose", C.c_int), ("timing", C.c_int), ("invariants", C.c_int),
     ]
 
 
@@ -72,6 +72,14 @@ SIGNATURES = [
     ("kc_fpset_check_fps", C.c_int, [_P, _U64P, C.POINTER(C.c_double)]),
     ("kc_fpset_stress", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                   C.POINTER(C.c_double), C.POINTER(C.c_double), _U64P]),
+    ("kc_fpset_put", C.c_int, [_P, C.c_uint64, _IP]),
+    ("kc_fpset_contains", C.c_int, [_P, C.c_uint64, _IP]),
+    ("kc_fpset_combine_rounds", C.c_uint64, [_P]),
+    ("kc_fpset_insert_count_dev", C.c_int, [_P, _P, C.c_size_t, _U64P, _P]),
+    ("kc_fpset_contains_count_dev", C.c_int, [_P, _P, C.c_size_t, _U64P, _P]),
+    ("kc_fpset_partition_dev", C.c_int, [_P, _P, C.c_uint64, C.c_int, _P, _U64P, _P]),
+    ("kc_stress_fps_dev", C.c_int, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P]),
+    ("kc_stress_fp", C.c_uint64, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]),
     ("kc_squeue_create", C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(_P)]),
     ("kc_squeue_destroy", None, [_P]),
     ("kc_squeue_enqueue", C.c_int, [_P, _U64P, C.c_size_t]),
@@ -98,6 +106,7 @@ SIGNATURES = [
     ("kc_shard_parent_key", C.c_int, [_P, C.c_int, C.c_uint64, _U64P]),
     ("kc_shard_frontier_tuple", C.c_int, [_P, C.c_uint64, _U64P]),
     ("kc_shard_result", C.c_int, [_P, C.POINTER(KcResult)]),
+    ("kc_shard_claim_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P, _U64P]),
     ("kc_shard_owner", C.c_int, [C.c_uint64, C.c_int]),
     ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),

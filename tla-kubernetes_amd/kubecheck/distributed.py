@@ -31,8 +31,20 @@ import numpy as np
 from . import ACTIONS, INVARIANTS, ModelConfig, Spec
 from ._lib import KcResult, check, load
 
-NONE_KEY = (1 << 63) - 1       # "no error" in the int64 all-reduce
+NONE_KEY = (1 << 64) - 1       # "no error" (the library's ~0)
 M44 = (1 << 44) - 1
+MAX_WORLD = 15                 # keys carry the rank in 4 bits (shard.hip); 15 = Init-state keys
+
+
+def key_to_i64(key: int) -> int:
+    """Order-preserving map of an unsigned 64-bit key into int64 (for the
+    int64 collectives): key - 2^63, so NONE_KEY becomes INT64_MAX and keys
+    of ranks >= 8 (>= 2^63) stay ordered below it."""
+    return int(key) - (1 << 63)
+
+
+def i64_to_key(v: int) -> int:
+    return int(v) + (1 << 63)
 
 
 def owner(fp: int, world: int) -> int:
@@ -98,6 +110,13 @@ class HipShard:
                 "init": int(r.init), "generated": int(r.generated), "distinct": int(r.distinct),
                 "fpset_slots": int(r.fpset_slots)}
 
+    def claim_times(self):
+        """(k_claim ms, launches, parents) since the last call."""
+        ms, n, p = C.c_double(), C.c_uint64(), C.c_uint64()
+        check("kc_shard_claim_times", self._lib.kc_shard_claim_times(self._h, C.byref(ms), C.byref(n),
+                                                                      C.byref(p)))
+        return ms.value, int(n.value), int(p.value)
+
     def close(self) -> None:
         if self._h:
             self._lib.kc_shard_destroy(self._h)
@@ -115,6 +134,8 @@ class ShardedModelChecker:
         self.cfg, self.be, self.group = cfg, backend, group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        if not 1 <= self.world <= MAX_WORLD:
+            raise ValueError(f"sharded check: world size {self.world} outside 1..{MAX_WORLD}")
         self.dev = torch.device(backend.device_type, torch.cuda.current_device()) \
             if backend.device_type == "cuda" else torch.device("cpu")
         # exchange buffers in 8-byte words (records are whole words): element
@@ -154,11 +175,11 @@ class ShardedModelChecker:
         R = self.world
         if R == 1:
             return [list(counts)], [n_new], [err]
-        cin = self._i64(list(counts) + [n_new, err])
+        cin = self._i64(list(counts) + [n_new, key_to_i64(err)])
         out = self.torch.empty(R * (R + 2), dtype=self.torch.int64, device=self.dev)
         self.dist.all_gather_into_tensor(out, cin, group=self.group)
         rows = out.view(R, R + 2).tolist()
-        return [r[:R] for r in rows], [r[R] for r in rows], [r[R + 1] for r in rows]
+        return [r[:R] for r in rows], [r[R] for r in rows], [i64_to_key(r[R + 1]) for r in rows]
 
     def _exchange(self, send, M: List[List[int]], rw: int):
         """All-to-all of the owner-grouped records given the counts matrix
@@ -221,6 +242,7 @@ class ShardedModelChecker:
 
         status_new, status_err = be.init(), NONE_KEY
         widths, level, err = [], 1, NONE_KEY
+        self.records_sent = 0                             # to other ranks, this check
         rw = rb // 8                                      # record words
         while True:
             t = tick()
@@ -229,6 +251,11 @@ class ShardedModelChecker:
                 counts, e1 = [0] * self.world, NONE_KEY
             else:
                 counts, e1 = be.expand()                  # expand `level`
+                if level == 1 and e1 != NONE_KEY and (e1 & 0xFF) == 0x12:
+                    # an Init state violates an invariant: that is level 1's
+                    # error (TLC checks Init before expanding anything), so it
+                    # goes into this gather, ahead of any level-2 error
+                    status_err, e1 = e1, NONE_KEY
             t = lap("expand", t)
             M, news, errs = self._gather_status(counts, status_new, status_err)
             t = lap("gather", t)
@@ -243,6 +270,7 @@ class ShardedModelChecker:
             widths.append(total)
             if last:
                 break
+            self.records_sent += sum(counts) - counts[self.rank]
             send = self._buffer("_send", max(sum(counts), 1) * rw)
             be.pack(send)
             t = lap("pack", t)
@@ -251,8 +279,7 @@ class ShardedModelChecker:
                 self._sync()
             t = lap("exchange", t)
             n_new, e2 = be.insert(recv, nrecv)
-            e = min(e1, e2)
-            status_new, status_err = n_new, (e if e < NONE_KEY else NONE_KEY)
+            status_new, status_err = n_new, min(e1, e2)
             be.advance()
             t = lap("insert", t)
             level += 1
@@ -301,7 +328,8 @@ class ShardedModelChecker:
             out.update(error="invariant", error_invariant=self.spec.check_invariants(states[-1]),
                        error_level=level + 1)
         elif kind == 0x12:                      # an Init state violates an invariant
-            out.update(error="invariant", error_invariant=self.spec.check_invariants(states[-1]))
+            out.update(error="invariant", error_invariant=self.spec.check_invariants(states[-1]),
+                       error_level=1)
         elif kind == 1:
             _, fail = self.spec.successors(states[-1])
             out.update(error="assertion", error_action=fail)
@@ -312,8 +340,12 @@ class ShardedModelChecker:
         return out
 
 
-def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
-    """bench.py --gpus N: every rank checks its shard; rank 0 reports."""
+def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict]:
+    """bench.py --gpus N: every rank checks its shard; rank 0 reports.  The
+    counts are checked against the golden fixture (bench.golden_check); the
+    roofline is k_claim's, per GPU (HIP events on every rank's k_claim
+    launches, bytes as in bench.roofline_bfs); xGMI bytes are the records
+    sent to other ranks."""
     import torch
     import torch.distributed as dist
 
@@ -321,17 +353,19 @@ def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     rank, world = dist.get_rank(), dist.get_world_size()
-    cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20)
+    cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20, timing=0 if args.no_timing else 2)
     be = HipShard(cfg, rank, world)
     mc = ShardedModelChecker(cfg, be)
     for _ in range(args.warmup):
         mc.run()
+    be.claim_times()                                  # reset
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = None
+    res, sent = None, 0
     for _ in range(args.steps):
         res = mc.run()
+        sent += mc.records_sent
         if not res["complete"] or res["error"]:
             raise RuntimeError(f"sharded check incomplete: error={res['error']} depth={res['depth']}")
     torch.cuda.synchronize()
@@ -339,9 +373,19 @@ def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
+    ms, launches, parents = be.claim_times()
+    mine = be.result()
+    S = 8 * Spec(cfg).state_words
+    gen_local = mine["generated"] * args.steps        # successors of this rank's parents
+    claim_bytes = parents * S + gen_local * 64
+    agg = torch.tensor([claim_bytes, int(ms * 1e6), launches, sent * be.record_bytes],
+                       dtype=torch.int64, device="cuda")
+    dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+    tot_bytes, tot_ns, tot_launch, xgmi = [int(x) for x in agg.tolist()]
     be.close()
     out = None
     if rank == 0:
+        golden = golden_check(args.workload, res) if golden_check else None
         out = {
             "metric": "distinct states/sec (KubeAPI TLC BFS)",
             "value": round(res["distinct"] * args.steps / dt, 1),
@@ -351,9 +395,21 @@ def bench_sharded(args, kw: dict, desc: str) -> Optional[dict]:
             "data": "synthetic (the model's Init states; no external input)",
             "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
                        "distinct": res["distinct"], "generated": res["generated"],
-                       "depth": res["depth"],
+                       "depth": res["depth"], "golden_check": golden,
+                       "path": "sharded (kc_shard_* stages, fingerprint-owner sharding)",
                        "parallelism": f"{world} GPUs, fingerprint-owner sharding, "
-                                      "RCCL all-to-all per BFS level"},
+                                      "RCCL all-to-all per BFS level",
+                       "xgmi_bytes_per_step": xgmi // max(args.steps, 1),
+                       "xgmi_GBps_per_gpu": round(xgmi / max(args.steps, 1) / world
+                                                  / (dt / args.steps) / 1e9, 2)},
         }
+        if tot_ns > 0:
+            achieved = tot_bytes / (tot_ns * 1e-9) / 1e9
+            out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0,
+                               "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                               "kernel": "k_claim", "per": "GPU (all ranks' bytes / all ranks' k_claim time)",
+                               "launches": tot_launch,
+                               "avg_launch_us": round(tot_ns / 1e3 / max(tot_launch, 1), 2),
+                               "bytes_per_launch": tot_bytes // max(tot_launch, 1)}
     dist.destroy_process_group()
     return out

@@ -135,6 +135,20 @@ def oracle_fixtures(with_np2: bool) -> dict:
     fx["variant2"]["err_invariant"] = r["err_invariant"]
     fx["variant2"]["trace"] = [[int(x) for x in t] for t in r["trace"]]
     fx["variant1"] = summary(O.run(O.config(variant=1)))  # Update without HasRead
+    # seeded bugs that exercise the other error paths (kubeapi_spec.h Flags):
+    # 3 = C2 Assert (KubeAPI.tla:598-599), 4 = TypeOK, 5 = Init violates
+    # OnlyOneVersion; ns=0 (no API server) deadlocks (launch:16)
+    for key, cfg in (("variant3", O.config(variant=3)), ("variant4", O.config(variant=4)),
+                     ("variant5", O.config(variant=5)), ("ns0", O.config(ns=0))):
+        r = O.run(cfg)
+        fx[key] = summary(r)
+        fx[key]["err_invariant"] = r["err_invariant"]
+        fx[key]["trace"] = [[int(x) for x in t] for t in r["trace"]]
+    fx["ns0_nodeadlock"] = summary(O.run(O.config(ns=0, check_deadlock=False)))
+    # a .cfg INVARIANT list without one of the two: the seeded violation of
+    # the unlisted invariant is not reported and the check runs to the end
+    fx["variant4_oov_only"] = summary(O.run(O.config(variant=4, invariants=2)))
+    fx["variant5_no_invariants"] = summary(O.run(O.config(variant=5, invariants=0)))
     fx["ns2"] = summary(O.run(O.config(ns=2)))
     fx["nc1_np0"] = summary(O.run(O.config(np_=0)))
     fx["np2_40levels"] = summary(O.run(O.config(np_=2, max_levels=40, keep_trace=False)))
