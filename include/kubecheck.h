@@ -72,7 +72,8 @@ int kc_fpset_put_batch(kc_fpset *s, const uint64_t *fps, size_t n, uint8_t *seen
 /* contains: seen_out[i] = 1 iff present (TLC FPSet.contains). */
 int kc_fpset_contains_batch(kc_fpset *s, const uint64_t *fps, size_t n, uint8_t *seen_out);
 /* Device-pointer variants (HBM in and out, asynchronous on `hip_stream`,
- * which may be NULL for the handle's own stream).  fps_dev may be rewritten
+ * which may be NULL for the handle's own stream; that stream is a blocking
+ * one, ordered with the legacy default stream).  fps_dev may be rewritten
  * (normalised in place). */
 int kc_fpset_put_batch_dev(kc_fpset *s, uint64_t *fps_dev, size_t n, uint8_t *seen_dev,
                            void *hip_stream);

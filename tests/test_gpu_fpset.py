@@ -104,7 +104,9 @@ def test_stress_full_size(load):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from cpu_fpset_shard import stream
 
-    cap = int(N_FULL / load * 3 / 4)            # slots = 4/3 capacity -> final load `load`
+    # slots = 4/3 capacity -> final load `load`, with room for the window
+    # below (a put past the 3/4 growth threshold would double the table)
+    cap = int((N_FULL + 100_000) / load * 3 / 4)
     with FPSet(capacity=cap) as s:
         ti, tl, found = s.stress(SEED, N_FULL, 1 << 24, N_FULL)
         assert s.size() == N_FULL                # no in-stream duplicates by construction

@@ -499,7 +499,10 @@ int kc_fpset_create(uint64_t capacity_fps, int device, kc_fpset** out) {
   auto* s = new kc_fpset();
   s->device = device;
   int rc = 0;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = -EIO;
+  // a BLOCKING stream: it orders with the legacy default stream, which is
+  // where a caller's NULL-stream work (and torch's default stream) runs, so
+  // a *_dev call without a stream sees the caller's earlier writes
+  if (hipStreamCreate(&s->stream) != hipSuccess) rc = -EIO;
   if (!rc) rc = s->fs.init(capacity_fps * 4 / 3 + 8, s->stream);
   if (!rc && hipMalloc(&s->d_stats, STAT_BYTES) != hipSuccess) rc = -ENOMEM;
   if (!rc && hipStreamSynchronize(s->stream) != hipSuccess) rc = -EIO;
