@@ -105,24 +105,33 @@ def roofline_bfs(times, res, S):
     }
 
 
-def pmc_traffic(workload: str, kernel: str):
+def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     summary for this workload (profiles/<round>_<workload>_rocprof_summary.json,
     written by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE
-    passes, gfx950-corrected).  bench.py cannot collect PMC counters itself
-    (they need their own rocprofv3 run), so the figure is the profile's."""
+    passes).  Corrected with our calibration (profiles/r02b_pmc_calibration.json):
+    the random probes are reported at full size, the kernel's coalesced
+    streaming reads (`stream_read_bytes` per launch, algorithmic) at half,
+    writes as the interface carries them.  bench.py cannot collect PMC
+    counters itself (they need their own rocprofv3 run), so the figure is
+    the profile's."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_rocprof_summary.json")))
-    if not files:
-        return None, None
-    try:
-        with open(files[-1]) as fh:
-            k = json.load(fh)["kernels"].get(kernel, {})
-    except (OSError, ValueError):
-        return None, None
-    b = k.get("hbm_bytes_per_launch")
-    return (int(b) if b else None), os.path.relpath(files[-1], ROOT)
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                k = json.load(fh)["kernels"].get(kernel, {})
+        except (OSError, ValueError):
+            continue
+        if "fetch_bytes_per_launch_raw" in k and "write_bytes_per_launch_raw" in k:
+            b = k["fetch_bytes_per_launch_raw"] + stream_read_bytes / 2 + k["write_bytes_per_launch_raw"]
+            return int(b), os.path.relpath(f, ROOT)
+        if "fetch_size_kib_per_launch_raw" in k and "write_size_kib_per_launch_raw" in k:   # r01 files
+            b = 1024 * (k["fetch_size_kib_per_launch_raw"] + k["write_size_kib_per_launch_raw"]) \
+                + stream_read_bytes / 2
+            return int(b), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(kw, seconds):
@@ -187,8 +196,11 @@ def bench_single(args, kw, desc):
                    "chunks": r.levels_chunks},
     }
     if not args.no_timing:
-        name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, state_bytes(kw))
-        roof["traffic"], src = pmc_traffic(args.workload, roof["kernel"])
+        S = state_bytes(kw)
+        name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, S)
+        # k_claim streams its parents (S B each); everything else it reads is a random probe
+        stream = acc["parents"] * S / max(times["expand"][1], 1) if roof["kernel"] == "k_claim" else 0.0
+        roof["traffic"], src = pmc_traffic(args.workload, roof["kernel"], stream)
         if src:
             roof["traffic_unit"] = "HBM bytes per launch (PMC)"
             roof["traffic_source"] = src

@@ -5,13 +5,21 @@ one JSON file under profiles/.
   python tools/pmc_summary.py --trace DIR [--fetch DIR] [--write DIR] --out profiles/X.json
 
 Per kernel (template arguments stripped): calls and total/average duration
-from the kernel trace, and the HBM traffic from the PMC passes, corrected as
-MI355X_MICROARCH.md §HBM prescribes:
-  * FETCH_SIZE and WRITE_SIZE are in KiB (bytes = value * 1024);
-  * on gfx950 FETCH_SIZE reports 1/2 of the bytes actually fetched
-    (TCC_EA0_RDREQ x 64 B tallied for 128-B requests), so it is doubled;
-  * WRITE_SIZE is taken as is.
-The per-launch figures are averages over every dispatch of that kernel.
+from the kernel trace, and the HBM traffic from the PMC passes.  FETCH_SIZE
+and WRITE_SIZE are in KiB (bytes = value * 1024).  The correction follows
+our own calibration (profiles/r02b_pmc_calibration.json, made with
+tools/microbench/pmc_calib.hip as MI355X_MICROARCH.md §HBM asks for
+uncalibrated shapes):
+  * coalesced 16 B/lane streaming reads are reported at 1/2 (the guide's
+    figure; 128-B requests tallied at 64 B);
+  * random 16-B / 8-B loads are reported at their full 64-B request size;
+  * atomics and random stores are reported as 64-B (CAS) or 32-B (max,
+    8-B stores) write requests, streaming stores exactly.
+So the raw FETCH_SIZE is exact for the random-probe part of a kernel and
+half of its streaming part: hbm_read = raw + streaming_read_bytes / 2, where
+the streaming bytes come from the caller's algorithmic count (bench.py
+pmc_traffic); `hbm_bytes_per_launch_raw` = FETCH + WRITE as reported.  The
+per-launch figures are averages over every dispatch of that kernel.
 """
 from __future__ import annotations
 
@@ -76,25 +84,26 @@ def main():
         if k in fetch:
             n, kib = fetch[k]
             e["fetch_size_kib_per_launch_raw"] = kib / n
-            e["hbm_read_bytes_per_launch"] = 2 * kib * 1024 / n       # gfx950: FETCH_SIZE x2
+            e["fetch_bytes_per_launch_raw"] = kib * 1024 / n
         if k in write:
             n, kib = write[k]
             e["write_size_kib_per_launch_raw"] = kib / n
-            e["hbm_write_bytes_per_launch"] = kib * 1024 / n
-        if "hbm_read_bytes_per_launch" in e and "hbm_write_bytes_per_launch" in e:
-            e["hbm_bytes_per_launch"] = e["hbm_read_bytes_per_launch"] + e["hbm_write_bytes_per_launch"]
-            e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3), 2)
+            e["write_bytes_per_launch_raw"] = kib * 1024 / n
+        if "fetch_bytes_per_launch_raw" in e and "write_bytes_per_launch_raw" in e:
+            e["hbm_bytes_per_launch_raw"] = e["fetch_bytes_per_launch_raw"] + e["write_bytes_per_launch_raw"]
+            e["hbm_GBps_raw"] = round(e["hbm_bytes_per_launch_raw"] / (e["avg_us"] * 1e3), 2)
         kernels[k] = e
     out = {"command": a.command,
-           "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM)",
+           "correction": "raw bytes = FETCH_SIZE*1024 + WRITE_SIZE*1024; hbm_read = raw fetch + "
+                         "streaming_read/2 (profiles/r02b_pmc_calibration.json)",
            "kernels": kernels}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     for k, e in list(kernels.items())[:14]:
         print(f"{k:34s} calls {e['calls']:6d} total {e['total_ms']:9.3f} ms avg {e['avg_us']:9.2f} us"
-              + (f"  hbm {e['hbm_bytes_per_launch'] / 1e6:10.3f} MB/launch {e['hbm_GBps']:8.1f} GB/s"
-                 if "hbm_bytes_per_launch" in e else ""))
+              + (f"  raw {e['hbm_bytes_per_launch_raw'] / 1e6:10.3f} MB/launch {e['hbm_GBps_raw']:8.1f} GB/s"
+                 if "hbm_bytes_per_launch_raw" in e else ""))
 
 
 if __name__ == "__main__":
