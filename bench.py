@@ -89,9 +89,12 @@ def roofline_bfs(times, res, S):
         "resolve": res["settles"] * (12 + 64) + parents * 8,
         "emit": parents * 8 + res["new"] * (2 * S + 9),
         "scan": parents * 8,
+        # k_narrow runs whole levels (expand + probe + emit); its bytes are
+        # only attributable when it ran every level of the check
+        "narrow": parents * S + res["succ"] * 64 + res["new"] * (2 * S + 9),
     }
     kernel_names = {"expand": "k_claim", "resolve": "k_settle_rec", "emit": "k_emit",
-                    "scan": "rocprim scan"}
+                    "scan": "rocprim scan", "narrow": "k_narrow"}
     name = max(times, key=lambda k: times[k][0])
     ms, launches = times[name]
     byts = per_kernel[name]
@@ -158,6 +161,7 @@ def bench_single(args, kw, desc):
     torch.cuda.synchronize()
     times = {"expand": [0.0, 0], "resolve": [0.0, 0], "scan": [0.0, 0], "emit": [0.0, 0]}
     acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0, "settles": 0}
+    narrow = [0.0, 0, 0]          # narrow-level kernel: ms, launches, levels
     t0 = time.perf_counter()
     results = []
     for _ in range(args.steps):
@@ -167,6 +171,8 @@ def bench_single(args, kw, desc):
         for k in times:
             times[k][0] += kt[k][0]
             times[k][1] += kt[k][1]
+        nt = mc.narrow_times()
+        narrow = [narrow[0] + nt[0], narrow[1] + nt[1], narrow[2] + nt[2]]
         acc["parents"] += r.distinct - r.queue_left
         acc["probes"] += r.fpset_probes
         acc["settles"] += r.batch_inserts
@@ -197,7 +203,10 @@ def bench_single(args, kw, desc):
     }
     if not args.no_timing:
         S = state_bytes(kw)
-        name, roof = roofline_bfs({k: tuple(v) for k, v in times.items()}, acc, S)
+        tt = {k: tuple(v) for k, v in times.items()}
+        if narrow[1] and narrow[2] // args.steps == r.depth - 1:     # every level ran narrow
+            tt["narrow"] = (narrow[0], narrow[1])
+        name, roof = roofline_bfs(tt, acc, S)
         # k_claim streams its parents (S B each); everything else it reads is a random probe
         stream = acc["parents"] * S / max(times["expand"][1], 1) if roof["kernel"] == "k_claim" else 0.0
         roof["traffic"], src = pmc_traffic(args.workload, roof["kernel"], stream)
@@ -206,6 +215,9 @@ def bench_single(args, kw, desc):
             roof["traffic_source"] = src
         out["roofline"] = roof
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items() if v[0] > 0}
+        if narrow[1]:
+            out["kernel_ms_per_step"]["narrow"] = round(narrow[0] / args.steps, 3)
+            out["config"]["narrow_levels_per_step"] = narrow[2] // args.steps
     mc.close()
     return out
 

@@ -202,6 +202,10 @@ int kc_engine_capture_level(kc_engine *e, int level);
  * for expand alone):
  * expand, resolve, scan, emit; and the number of launches of each. */
 int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
+/* The narrow-level kernel of the last run (frontiers <= 8192 states run as
+ * whole levels inside one single-workgroup launch): its device time in ms
+ * (with cfg.timing), launches, and the BFS levels it expanded. */
+int kc_engine_narrow_times(kc_engine *e, double *ms, uint64_t *launches, uint64_t *levels);
 
 /* --------------------------------------------------- Sharded (multi-GPU) */
 /* Fingerprint-owner-sharded BFS, one process per GPU (replaces TLC's

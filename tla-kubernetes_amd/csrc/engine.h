@@ -14,6 +14,9 @@ enum KernelKind { KK_EXPAND = 0, KK_RESOLVE = 1, KK_SCAN = 2, KK_EMIT = 3, KK_CO
 // diagnostic-only ablation timings (KC_ABLATE=1 in the environment): extra
 // launches of cut-down k_claim variants on scratch buffers, printed to stderr
 enum AblateKind { KA_LDS = KK_COUNT, KA_COMPUTE = KK_COUNT + 1, KA_PLAN = KK_COUNT + 2, KA_TOTAL = KK_COUNT + 3 };
+// the narrow-level kernel (engine_narrow.h): levels it ran, launches, time
+constexpr int KK_NARROW = KA_TOTAL;
+constexpr int KK_ALL = KA_TOTAL + 1;
 
 class EngineBase {
  public:
@@ -34,13 +37,19 @@ class EngineBase {
       if (launches) launches[k] = klaunch_[k];
     }
   }
+  void narrow_times(double* ms, uint64_t* launches, uint64_t* levels) const {
+    *ms = ktime_ms_[KK_NARROW];
+    *launches = klaunch_[KK_NARROW];
+    *levels = narrow_levels_;
+  }
 
  protected:
   kc_model_config cfg_;
   int capture_level_ = 0;
   int timing_ = 0;   // 1: HIP events on every kernel; 2: on k_claim only
-  double ktime_ms_[KA_TOTAL] = {};
-  uint64_t klaunch_[KA_TOTAL] = {};
+  double ktime_ms_[KK_ALL] = {};
+  uint64_t klaunch_[KK_ALL] = {};
+  uint64_t narrow_levels_ = 0;
   bool ablate_ = false;
 };
 

@@ -22,6 +22,7 @@
 #include "../../include/kubecheck.h"
 #include "engine.h"
 #include "engine_kernels.h"
+#include "engine_narrow.h"
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
@@ -79,6 +80,11 @@ class EngineT final : public EngineBase {
     const char* ab = getenv("KC_ABLATE");
     ablate_ = ab && ab[0] == '1';
     if (ablate_) timing_ = 1;
+    // the narrow-level kernel: on by default; off when the caller asks for
+    // explicit chunks (the chunked wide path is what they exercise) or with
+    // KC_NARROW=0
+    const char* nw = getenv("KC_NARROW");
+    narrow_on_ = cfg.chunk_states == 0 && !(nw && nw[0] == '0') && !ablate_;
   }
   ~EngineT() override { release(); }
 
@@ -99,6 +105,15 @@ class EngineT final : public EngineBase {
     KC_HIP_TRY(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
+    KC_HIP_TRY(hipMalloc(&d_ns_, sizeof(NarrowCtl)));
+    KC_HIP_TRY(hipHostMalloc(&h_ns_, sizeof(NarrowCtl)));
+    if (narrow_on_) {
+      KC_HIP_TRY(hipMalloc(&d_nsc_, sizeof(NarrowScratch)));
+      hipLaunchKernelGGL(k_narrow_scratch_init, dim3((unsigned)((NARROW_LT + 255) / 256)), dim3(256), 0, st_,
+                         d_nsc_);
+      KC_HIP_TRY(hipGetLastError());
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+    }
     return 0;
   }
 
@@ -107,10 +122,12 @@ class EngineT final : public EngineBase {
     memset(res, 0, sizeof *res);
     res->err_action = res->err_self = res->err_invariant = -1;
     trace_.clear();
+    narrow_probes_ = 0;
     for (auto& t : ktime_ms_) t = 0;
     ev_kind_.clear();
     ev_used_ = 0;
     for (auto& c : klaunch_) c = 0;
+    narrow_levels_ = 0;
     const auto t0 = std::chrono::steady_clock::now();
 
     // ---- Init (KubeAPI.tla:455-469), on the host: 2^NC states
@@ -193,6 +210,36 @@ class EngineT final : public EngineBase {
         (std::min<uint64_t>(cfg_.chunk_states ? cfg_.chunk_states : kMaxChunk, kMaxChunk) + 255) / 256 * 256;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
+      if (narrow_on_ && n <= (uint64_t)NARROW_MAX) {
+        // ---- narrow levels: one single-workgroup launch runs as many
+        // levels as fit (engine_narrow.h); the host takes over at the first
+        // level it cannot run
+        int stop = cfg_.max_levels;
+        if (capture_level_ >= level + 1 && (stop == 0 || capture_level_ - 1 < stop)) stop = capture_level_ - 1;
+        NarrowRun nr;
+        KC_TRY(run_narrow(n, level, level_gidx, cand, stop, nr));
+        res->distinct += nr.new_total;
+        for (int L = level; L < nr.level; ++L) {
+          if (L >= KC_MAX_LEVELS) {
+            set_error("kubecheck: more than %d levels", KC_MAX_LEVELS);
+            return -ENOMEM;
+          }
+          res->level_width[L] = h_ns_->widths[L];
+        }
+        if (nr.levels) res->peak_frontier = std::max<uint64_t>(res->peak_frontier, std::max(n, nr.peak));
+        level = nr.level;
+        level_gidx = nr.level_gidx;
+        n = nr.n;
+        cand = nr.cand;
+        if (nr.levels) res->nlevels = n ? level : level - 1;
+        if (nr.reason == NX_ERROR) {
+          KC_TRY(report_error(res, h_ns_->err_key, level, level_gidx, n));
+          finish(res, t0, 0);
+          return 0;
+        }
+        if (nr.levels > 0 || n == 0) continue;
+        // not even one level fitted (buffer room): this level goes wide
+      }
       if (n >= (1ull << 32)) {
         set_error("kubecheck: level wider than 2^32 states");
         return -ENOMEM;
@@ -348,7 +395,7 @@ class EngineT final : public EngineBase {
   void timed(int k, F&& f) {
     // (timing 2: events bracket the roofline kernel only; ten events per
     // level cost the NP=2 check 6 ms and Model_1 4 ms of host/queue time)
-    if (timing_ == 1 || (timing_ == 2 && k == KK_EXPAND)) {
+    if (timing_ == 1 || (timing_ == 2 && (k == KK_EXPAND || k == KK_NARROW))) {
       if (ev_used_ + 2 > ev_pool_.size()) {
         hipEvent_t a, b;
         (void)hipEventCreate(&a);
@@ -475,7 +522,7 @@ class EngineT final : public EngineBase {
     const double d = (double)res->distinct, gg = (double)res->generated;
     res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
     res->fpset_slots = cs_.capacity();
-    res->fpset_probes = h_ctr_->probes();
+    res->fpset_probes = h_ctr_->probes() + narrow_probes_;
     res->batch_inserts = h_ctr_->settles();
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -487,12 +534,108 @@ class EngineT final : public EngineBase {
                     (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (d_ns_) (void)hipFree(d_ns_);
+    if (d_nsc_) (void)hipFree(d_nsc_);
+    if (h_ns_) (void)hipHostFree(h_ns_);
     for (auto& e : ev_pool_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
+  // One launch of k_narrow from the host loop's state; on return the
+  // engine's cur_ holds the frontier of level nr.level.
+  struct NarrowRun {
+    uint64_t n = 0, level_gidx = 0, cand = 0, new_total = 0, peak = 0;
+    int level = 0, levels = 0, reason = 0;
+  };
+  int run_narrow(uint64_t n, int level, uint64_t level_gidx, uint64_t cand, int stop, NarrowRun& nr) {
+    constexpr uint64_t kBuf = 1ull << 16;            // frontier room (states) of a narrow run
+    constexpr uint64_t kNew = 1ull << 20;            // new states one run may add
+    const uint64_t bufs = std::max(cand, kBuf);
+    KC_TRY(grow_buffer(cur_, cur_cap_, bufs, true, st_));
+    KC_TRY(grow_buffer(next_, next_cap_, bufs, false, st_));
+    const uint64_t need_par = level_gidx + n + std::max(cand, kNew) + 1;
+    if (cfg_.keep_trace) {
+      KC_TRY(grow_buffer(parent_, par_cap_, need_par, true, st_));
+      KC_TRY(grow_buffer(ord_, ord_cap_, need_par, true, st_));
+    }
+    KC_TRY(cs_.reserve(std::max(cand, kNew), st_));
+    NarrowCtl& h = *h_ns_;
+    memset(&h, 0, offsetof(NarrowCtl, widths));
+    h.n = n;
+    h.level_gidx = level_gidx;
+    h.cand = cand;
+    h.level = (uint32_t)level;
+    h.cur_is_b = 0;
+    h.buf_cap = std::min(cur_cap_, next_cap_);
+    h.par_cap = cfg_.keep_trace ? std::min(par_cap_, ord_cap_) : ~0ull;
+    h.room = cs_.capacity() / 2 > cs_.count ? cs_.capacity() / 2 - cs_.count : 0;
+    h.stop_level = (uint32_t)stop;
+    h.err = ~0ull;
+    h.epoch = ++narrow_epoch_;
+    h.reason = narrow_exit_reason(h);
+    h.active = h.reason == 0;
+    nr = NarrowRun{};
+    if (!h.active) {                             // this level cannot run narrow
+      nr.n = n, nr.level_gidx = level_gidx, nr.cand = cand, nr.level = level, nr.reason = h.reason;
+      return 0;
+    }
+    KC_HIP_TRY(hipMemcpyAsync(d_ns_, h_ns_, offsetof(NarrowCtl, widths), hipMemcpyHostToDevice, st_));
+    // NARROW_BATCH levels' launches per host sync; they all read the control
+    // block, so the ones after the run has ended return at once
+    State *a = cur_, *b = next_;
+    for (;;) {
+      timed(KK_NARROW, [&] {
+        for (int k = 0; k < NARROW_BATCH; ++k) {
+          hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
+                             cfg_.check_deadlock, d_ns_, d_nsc_, d_ctr_);
+          hipLaunchKernelGGL(k_ninsert, dim3((unsigned)(NARROW_LT / NARROW_THREADS)), dim3(NARROW_THREADS), 0,
+                             st_, d_ns_, d_nsc_, cs_.t, cs_.nslots);
+          hipLaunchKernelGGL(k_nemit<M>, dim3(NARROW_WG), dim3(NARROW_THREADS), 0, st_, a, b, flags_, parent_,
+                             ord_, cfg_.keep_trace, d_ns_, d_nsc_, d_ctr_);
+          hipLaunchKernelGGL(k_nstep, dim3(1), dim3(64), 0, st_, d_ns_, d_ctr_);
+        }
+      });
+      KC_HIP_TRY(hipGetLastError());
+      KC_HIP_TRY(hipMemcpyAsync(h_ns_, d_ns_, offsetof(NarrowCtl, cand_acc), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      if (h_ctr_->overflow) {
+        set_error("kubecheck: state with more than %d successors", M::MAXSUCC);
+        return -ENOMEM;
+      }
+      if (!h.active) break;
+    }
+    collect_times();
+    KC_HIP_TRY(hipMemcpy(h_ns_->widths + level, d_ns_->widths + level,
+                         sizeof(uint64_t) * std::min<uint64_t>(h.levels + 1, KC_MAX_LEVELS - level),
+                         hipMemcpyDeviceToHost));
+    nr.n = h.n;
+    nr.level_gidx = h.level_gidx;
+    nr.cand = h.cand;
+    nr.level = (int)h.level;
+    nr.levels = (int)h.levels;
+    nr.reason = h.reason;
+    nr.new_total = h.new_total;
+    nr.peak = 0;
+    for (int L = level; L < nr.level && L < KC_MAX_LEVELS; ++L) nr.peak = std::max<uint64_t>(nr.peak, h.widths[L]);
+    if (nr.reason == NX_ERROR) h_ctr_->err_key = h.err_key;
+    cs_.count += h.new_total;
+    narrow_levels_ += h.levels;
+    narrow_probes_ += h.probes;
+    if (h.cur_is_b) {
+      std::swap(cur_, next_);
+      std::swap(cur_cap_, next_cap_);
+    }
+    return 0;
+  }
+
   Flags flags_{};
   hipStream_t st_ = nullptr;
+  NarrowCtl *d_ns_ = nullptr, *h_ns_ = nullptr;
+  NarrowScratch* d_nsc_ = nullptr;
+  bool narrow_on_ = true;
+  uint64_t narrow_probes_ = 0;
+  uint32_t narrow_epoch_ = 0;
   DevClaimSet cs_;
   State *cur_ = nullptr, *next_ = nullptr;
   uint64_t cur_cap_ = 0, next_cap_ = 0;
@@ -602,6 +745,12 @@ int64_t kc_engine_level_tuples(kc_engine* e, int level, uint64_t* out, uint64_t 
 int kc_engine_capture_level(kc_engine* e, int level) {
   if (!e) { set_error("kc_engine_capture_level: NULL"); return -EINVAL; }
   e->impl->set_capture(level);
+  return 0;
+}
+
+int kc_engine_narrow_times(kc_engine* e, double* ms, uint64_t* launches, uint64_t* levels) {
+  if (!e || !ms || !launches || !levels) { set_error("kc_engine_narrow_times: NULL"); return -EINVAL; }
+  e->impl->narrow_times(ms, launches, levels);
   return 0;
 }
 

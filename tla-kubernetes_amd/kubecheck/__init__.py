@@ -158,6 +158,13 @@ class ModelChecker:
         names = ["expand", "resolve", "scan", "emit"]
         return {k: (ms[i], int(cnt[i])) for i, k in enumerate(names)}
 
+    def narrow_times(self):
+        """(ms, launches, levels) of the narrow-level kernel in the last run."""
+        ms, n, lv = C.c_double(), C.c_uint64(), C.c_uint64()
+        check("kc_engine_narrow_times", self._lib.kc_engine_narrow_times(self._h, C.byref(ms), C.byref(n),
+                                                                          C.byref(lv)))
+        return ms.value, int(n.value), int(lv.value)
+
     def close(self) -> None:
         if self._h:
             self._lib.kc_engine_destroy(self._h)

@@ -94,6 +94,7 @@ SIGNATURES = [
     ("kc_engine_level_tuples", C.c_int64, [_P, C.c_int, _U64P, C.c_uint64]),
     ("kc_engine_capture_level", C.c_int, [_P, C.c_int]),
     ("kc_engine_kernel_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
+    ("kc_engine_narrow_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P, _U64P]),
     ("kc_shard_create", C.c_int, [C.POINTER(KcModelConfig), C.c_int, C.c_int, C.POINTER(_P)]),
     ("kc_shard_destroy", None, [_P]),
     ("kc_shard_init", C.c_int, [_P, _U64P]),
