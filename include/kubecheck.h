@@ -260,6 +260,30 @@ int kc_shard_claim_times(kc_shard *s, double *ms, uint64_t *launches, uint64_t *
 /* owner rank of a fingerprint */
 int kc_shard_owner(uint64_t fp, int world);
 
+/* ------------------------------------------- Native sharded level loop */
+/* The whole level-synchronous sharded BFS in C++ (the protocol above, with
+ * one all-gather and one all-to-all per level and no caller in the loop).
+ * A group is the set of shards one process drives plus their collectives:
+ *   - kc_group_create_rccl: one shard per process (one process per GPU) and
+ *     an RCCL communicator; every rank passes the same 128-byte id, made by
+ *     kc_rccl_unique_id on one rank and sent to the others by the caller
+ *     (e.g. a torch.distributed broadcast).  RCCL is loaded at run time.
+ *   - kc_group_create_local: ranks 0..n-1 of one process on one GPU, the
+ *     collectives done by device copies (multi-rank emulation, tests).
+ * kc_group_run fills the GLOBAL result (the same on every rank): totals,
+ * per-action counts, level widths, depth, and any error with its trace. */
+#define KC_RCCL_ID_BYTES 128
+typedef struct kc_group kc_group;
+int kc_rccl_unique_id(uint8_t *id_out /* KC_RCCL_ID_BYTES */);
+int kc_group_create_rccl(kc_shard *s, const uint8_t *id, kc_group **out);
+int kc_group_create_local(kc_shard **shards, int nshards, kc_group **out);
+void kc_group_destroy(kc_group *g);
+int kc_group_run(kc_group *g, kc_result *res);
+/* Canonical tuple of trace state i of the last run's error; returns words. */
+int kc_group_trace_tuple(kc_group *g, int i, uint64_t *out);
+/* Records this group's ranks sent to other ranks in the last run (global). */
+uint64_t kc_group_records_sent(const kc_group *g);
+
 /* ---------------------------------------------------------- Spec (host) */
 /* Words of the canonical tuple for a model: 1 + 19 * (nc + np + ns). */
 int kc_spec_tuple_words(int nc, int np, int ns);

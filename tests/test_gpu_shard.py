@@ -154,3 +154,75 @@ def test_driver_world1_rccl(fixtures):
             assert r3["error_level"] == fixtures[key]["err_level"]
     finally:
         dist.destroy_process_group()
+
+
+# --- the native level loop (kc_group_*): the same protocol in C++ --------
+from kubecheck.distributed import NativeShardedChecker
+
+
+def native(R, **kw):
+    mc = NativeShardedChecker(ModelConfig(**kw), emulate=R)
+    try:
+        return mc.run()
+    finally:
+        mc.close()
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 8, 9])
+def test_native_model1_any_rank_count(fixtures, R):
+    fx = fixtures["model1"]
+    r = native(R)
+    assert r["complete"] and r["error"] is None
+    assert r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["act_gen"] == fx["act_gen"]
+    assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+
+
+@pytest.mark.parametrize("R", [2, 9])
+@pytest.mark.parametrize("key,kw,kind", [("nc2", dict(nc=2), "assertion"),
+                                         ("variant2", dict(variant=2), "invariant"),
+                                         ("variant3", dict(variant=3), "assertion"),
+                                         ("variant5", dict(variant=5), "invariant"),
+                                         ("ns0", dict(ns=0), "deadlock")])
+def test_native_error_paths(fixtures, oracle, R, key, kw, kind):
+    fx = fixtures[key]
+    r = native(R, **kw)
+    assert r["error"] == kind
+    assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
+    if kind == "assertion":
+        assert r["error_action"] == fx["err_action"]
+    # the trace is a real behaviour from an Init state, ending in the error
+    # (with R > 1 ranks the frontier order differs, so when a level holds
+    # several errors an equally short one may be reported)
+    cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1), variant=kw.get("variant", 0))
+    for a, b in zip(r["trace"], r["trace"][1:]):
+        succ, _ = oracle.successors(cfg, a)
+        assert any(list(map(int, x)) == b for _, x in succ)
+
+
+def test_native_enlarged_prefix(fixtures):
+    fx = fixtures["np2_40levels"]
+    r = native(4, np=2, max_levels=40)
+    assert r["level_width"] == fx["level_width"] and not r["complete"]
+    assert r["act_gen"] == fx["act_gen"]
+
+
+def test_native_rccl_world1(fixtures, monkeypatch):
+    # the RCCL communicator path (one rank: every collective runs, nothing
+    # moves; KC_RCCL_FORCE=1 keeps the world-1 collectives on RCCL)
+    monkeypatch.setenv("KC_RCCL_FORCE", "1")
+    mc = NativeShardedChecker(ModelConfig(), 0, 1)
+    try:
+        r = mc.run()
+        fx = fixtures["model1"]
+        assert r["level_width"] == fx["level_width"]
+        assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+    finally:
+        mc.close()
+    mc = NativeShardedChecker(ModelConfig(nc=2), 0, 1)
+    try:
+        r = mc.run()
+        assert r["error"] == "assertion" and r["trace"] == fixtures["nc2"]["trace"]
+    finally:
+        mc.close()

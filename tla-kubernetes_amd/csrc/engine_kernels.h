@@ -134,10 +134,19 @@ __device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t til
   rec_lk[tile * CLAIM_RCAP + k] = lk;
 }
 
+// The LDS table of the sharded variant is smaller (CLAIM_LDS_SH entries):
+// its per-parent owner counts take LDS too, and 2048 entries would leave
+// room for 5 workgroups per CU instead of 6 (measured: k_claim 686 vs 564 us
+// per launch at RCCL world 1, r02i).
+constexpr int CLAIM_LDS_SH = 1792;
+static_assert(CLAIM_LDS_SH % CLAIM_TILE == 0, "whole entries per lane in the compaction");
+template <int NT = CLAIM_LDS>
 __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int* sh_key,
                                          uint64_t fp, unsigned int lk) {
-  unsigned int h = (unsigned int)((fp * 0xd6e8feb86659fd93ull) >> (64 - CLAIM_LDS_BITS));
-  for (int p = 0; p < CLAIM_LDS; ++p) {
+  unsigned int h = NT == CLAIM_LDS
+                       ? (unsigned int)((fp * 0xd6e8feb86659fd93ull) >> (64 - CLAIM_LDS_BITS))
+                       : (unsigned int)(((fp * 0xd6e8feb86659fd93ull) >> 32) * (uint64_t)NT >> 32);
+  for (int p = 0; p < NT; ++p) {
     unsigned long long e = __hip_atomic_load(&sh_fp[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (e == 0ull) {
       e = atomicCAS(&sh_fp[h], 0ull, (unsigned long long)fp);
@@ -147,7 +156,7 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
       atomicMin(&sh_key[h], lk);
       return (int)h;
     }
-    h = (h + 1) & (CLAIM_LDS - 1);
+    h = (h + 1 == (unsigned int)NT) ? 0u : h + 1;
   }
   return -1;
 }
@@ -179,8 +188,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh) {
-  __shared__ unsigned long long sh_fp[CLAIM_LDS];
-  __shared__ unsigned int sh_key[CLAIM_LDS];
+  constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
+  __shared__ unsigned long long sh_fp[NT];
+  __shared__ unsigned int sh_key[NT];
   __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_rc;
@@ -194,7 +204,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     sh_rc = 0;
     sh_nrep = 0;
   }
-  for (int k = threadIdx.x; k < CLAIM_LDS; k += CLAIM_TILE) {
+  for (int k = threadIdx.x; k < NT; k += CLAIM_TILE) {
     sh_fp[k] = 0ull;
     sh_key[k] = ~0u;
   }
@@ -244,7 +254,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         acc ^= fp;
         continue;
       }
-      if (lds_claim(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
+      if (lds_claim<NT>(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
         // LDS table full: claim (or send) this copy directly
         if (SH) {
           const uint32_t o = owner_of(fp, sh.world);
@@ -275,7 +285,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   // lane claims ~3 dense entries in a row instead of scanning 8 sparse ones
   // (each scan step costs its wave one probe round trip)
   {
-    constexpr int PER = CLAIM_LDS / CLAIM_TILE;
+    constexpr int PER = NT / CLAIM_TILE;
     unsigned long long efp[PER];
     unsigned int ekey[PER];
     unsigned int mine = 0;

@@ -1,0 +1,47 @@
+// shard.h — type-erased interface of one fingerprint-owner shard (shard.hip)
+// and the kc_shard handle, shared with the native level loop
+// (shard_driver.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <memory>
+#include <vector>
+
+#include "../../include/kubecheck.h"
+
+namespace kc {
+
+class ShardBase {
+ public:
+  virtual ~ShardBase() = default;
+  virtual int setup() = 0;
+  virtual int set_stream(hipStream_t st) = 0;
+  virtual int init(uint64_t* n_local) = 0;
+  virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
+  virtual uint64_t record_bytes() const = 0;
+  virtual int pack(void* send) = 0;
+  virtual int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) = 0;
+  virtual int advance() = 0;
+  virtual int parent_key(int level, uint64_t idx, uint64_t* key) = 0;
+  virtual int frontier_tuple(uint64_t idx, uint64_t* out) = 0;
+  virtual int result(kc_result* r) = 0;
+  virtual void claim_times(double* ms, uint64_t* launches, uint64_t* parents) = 0;
+  virtual hipStream_t stream() const = 0;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  virtual int device() const = 0;
+  virtual int tuple_words() const = 0;
+  virtual const kc_model_config& config() const = 0;
+  // pack() without its own host sync (the caller orders the records' use)
+  virtual void set_async_pack(bool on) = 0;
+  virtual int replay(int init_idx, const std::vector<int>& ords, int kind, int pos,
+                     std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
+                     int* err_inv) = 0;
+};
+
+}  // namespace kc
+
+struct kc_shard {
+  std::unique_ptr<kc::ShardBase> impl;
+};

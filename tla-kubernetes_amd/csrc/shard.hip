@@ -38,6 +38,7 @@
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
+#include "shard.h"
 
 namespace kc {
 
@@ -278,23 +279,6 @@ k_shard_emit_rec(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* _
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
 
-class ShardBase {
- public:
-  virtual ~ShardBase() = default;
-  virtual int setup() = 0;
-  virtual int set_stream(hipStream_t st) = 0;
-  virtual int init(uint64_t* n_local) = 0;
-  virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
-  virtual uint64_t record_bytes() const = 0;
-  virtual int pack(void* send) = 0;
-  virtual int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) = 0;
-  virtual int advance() = 0;
-  virtual int parent_key(int level, uint64_t idx, uint64_t* key) = 0;
-  virtual int frontier_tuple(uint64_t idx, uint64_t* out) = 0;
-  virtual int result(kc_result* r) = 0;
-  virtual void claim_times(double* ms, uint64_t* launches, uint64_t* parents) = 0;
-};
-
 template <class M>
 class ShardT final : public ShardBase {
   using State = typename M::State;
@@ -428,25 +412,38 @@ class ShardT final : public ShardBase {
     sh.cnt = cnt_;
     const size_t dyn = (size_t)(CLAIM_TILE + ((world_ + 3) / 4) * CLAIM_TILE) * sizeof(unsigned int);
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[0], st_));
-    hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
-                       cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                       (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
-                       d_ctr_, sh);
+    if (world_ == 1) {
+      // one rank owns everything: the single-GPU engine's claim kernel (no
+      // owner counting; claim keys then carry rank 0, which they do anyway)
+      hipLaunchKernelGGL((k_claim<M, 0, false>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+                         cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                         (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                         d_ctr_, ShardArgs{});
+    } else {
+      hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
+                         cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                         (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                         d_ctr_, sh);
+    }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[1], st_));
     // one exclusive scan over the owner-major matrix = every record's position
-    // in the owner-grouped send buffer
+    // in the owner-grouped send buffer (nothing to send at world 1)
     const uint64_t cells = n_ * (uint64_t)world_;
     if (cells >= (1ull << 31)) {
       set_error("kc_shard_expand: frontier x world = %llu cells exceeds one scan (2^31)",
                 (unsigned long long)cells);
       return -ENOMEM;
     }
-    size_t tmp_bytes = 0;
-    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
-    KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
-    hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
-                       d_owner_base_);
+    if (world_ > 1) {
+      size_t tmp_bytes = 0;
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
+      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
+      hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
+                         d_owner_base_);
+    } else {
+      KC_HIP_TRY(hipMemsetAsync(d_owner_base_, 0, 16 * sizeof(uint64_t), st_));
+    }
     KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipMemcpyAsync(h_owner_base_, d_owner_base_, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
@@ -472,6 +469,62 @@ class ShardT final : public ShardBase {
   }
 
   uint64_t record_bytes() const override { return sizeof(Rec); }
+  hipStream_t stream() const override { return st_; }
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  int device() const override { return cfg_.device; }
+  int tuple_words() const override { return M::TUPLE_WORDS; }
+  const kc_model_config& config() const override { return cfg_; }
+  void set_async_pack(bool on) override { async_pack_ = on; }
+
+  // Rebuild a counterexample on the host (TLC's trace file walk): from Init
+  // state `init_idx` follow the successor ordinals, then add the violating
+  // successor `pos` (invariant errors).  The same plan/apply code the
+  // kernels run, compiled for the host.
+  int replay(int init_idx, const std::vector<int>& ords, int kind, int pos,
+             std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
+             int* err_inv) override {
+    if (init_idx < 0 || init_idx >= M::num_init()) {
+      set_error("kc_shard replay: bad Init index %d", init_idx);
+      return -EIO;
+    }
+    std::vector<State> path(1);
+    M::init_state(init_idx, path[0], cfg_.variant);
+    for (int t : ords) {
+      const State& s = path.back();
+      const typename M::Plan pl = M::plan(s, flags_);
+      if (t < 0 || t >= pl.total) {
+        set_error("kc_shard replay: ordinal %d out of %d", t, pl.total);
+        return -EIO;
+      }
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      State x;
+      M::apply(s, slot, j, flags_, x);
+      path.push_back(x);
+    }
+    *err_action = *err_self = *err_inv = -1;
+    const State& s = path.back();
+    const typename M::Plan pl = M::plan(s, flags_);
+    if (kind == E_INVARIANT) {
+      int slot, j;
+      M::locate(pl, pos, slot, j);
+      State x;
+      M::apply(s, slot, j, flags_, x);
+      path.push_back(x);
+      *err_inv = M::check(x, flags_.inv_mask);
+    } else if (kind == 0x12) {
+      *err_inv = M::check(s, flags_.inv_mask);
+    } else if (kind == E_ASSERT && pl.fail_slot >= 0) {
+      *err_action = M::slot_action(s, pl.fail_slot);
+      *err_self = pl.fail_slot < M::A ? pl.fail_slot
+                  : pl.fail_slot < 2 * M::A ? pl.fail_slot - M::A
+                                           : M::A + (pl.fail_slot - 2 * M::A);
+    }
+    tuples.assign(path.size(), std::vector<uint64_t>(M::TUPLE_WORDS));
+    for (size_t k = 0; k < path.size(); ++k) M::to_tuple(path[k], tuples[k].data());
+    return 0;
+  }
 
   int pack(void* send) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
@@ -481,7 +534,9 @@ class ShardT final : public ShardBase {
                          (Rec*)send);
       KC_HIP_TRY(hipGetLastError());
     }
-    if (own_st_) KC_HIP_TRY(hipStreamSynchronize(st_));   // else stream-ordered with the caller
+    // else stream-ordered with the caller (set_stream, or the native level
+    // loop, which synchronises before it moves the records itself)
+    if (own_st_ && !async_pack_) KC_HIP_TRY(hipStreamSynchronize(st_));
     return 0;
   }
 
@@ -669,6 +724,7 @@ class ShardT final : public ShardBase {
   int level_ = 0;
   std::vector<uint64_t> level_base_;
   hipEvent_t ev_[2] = {nullptr, nullptr};
+  bool async_pack_ = false;
   double claim_ms_ = 0;
   uint64_t claim_launches_ = 0, claim_parents_ = 0;
 };
@@ -685,10 +741,6 @@ std::unique_ptr<ShardBase> make_shard(const kc_model_config& cfg, int rank, int 
 }  // namespace kc
 
 using namespace kc;
-
-struct kc_shard {
-  std::unique_ptr<ShardBase> impl;
-};
 
 extern "C" {
 

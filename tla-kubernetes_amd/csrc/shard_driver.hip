@@ -1,0 +1,541 @@
+// shard_driver.hip — the native level loop of the fingerprint-owner-sharded
+// BFS (kc_group_*): the per-level protocol of kubecheck/distributed.py's
+// ShardedModelChecker, in C++ and over RCCL directly, so a level costs the
+// kernels, one all-gather, one all-to-all and three host synchronisations
+// (expand's counts, the all-gather, insert's new-state count), without a
+// Python interpreter in the loop.
+//
+// Replaces TLC's single-host worker pool for this spec (TLC's own
+// distributed mode, RMI TLCServer/TLCWorker, is off in Model_1:
+// KubeAPI___Model_1.launch:4-7).  Per BFS level, on every rank:
+//
+//   expand (claim own successors, count the rest per owner)
+//   all-gather of [counts per owner | new states and error key of the level
+//                  finished last]            -> error? done? widths, a2a sizes
+//   pack records per owner -> all-to-all (grouped ncclSend/ncclRecv, in
+//   pieces of <= 256 MiB) -> insert (dedup by min key, emit)  -> advance
+//
+// The collectives sit behind a small Comm interface with two
+// implementations: RcclComm (one shard per process, one process per GPU;
+// RCCL resolved at run time with dlopen, so the library loads on hosts
+// without it) and LocalComm (R shards of ONE process on one GPU, the
+// collectives done by device copies).  The level loop is the same code for
+// both, so the multi-rank protocol is exercised on one GPU with R = 2..15
+// emulated ranks, and RCCL itself at world 1.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/kubecheck.h"
+#include "engine.h"
+#include "engine_util.h"
+#include "kc_common.h"
+#include "shard.h"
+
+namespace kc {
+
+namespace {
+
+constexpr uint64_t NONE = ~0ull;
+constexpr uint64_t KEY44 = (1ull << 44) - 1;
+constexpr uint64_t PIECE_BYTES = 256ull << 20;   // largest single send/recv of the exchange
+
+// ---------------------------------------------------------------- RCCL
+// Resolved at run time: torch ships its own librccl.so.1; when it is loaded
+// already, dlopen returns that copy (one RCCL per process).
+struct RcclApi {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  bool ok = false;
+};
+
+const RcclApi* rccl() {
+  static RcclApi api;
+  static bool tried = false;
+  if (tried) return api.ok ? &api : nullptr;
+  tried = true;
+  void* h = nullptr;
+  for (const char* name : {"librccl.so.1", "librccl.so"}) {
+    h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    if (h) break;
+  }
+  for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+    if (h) break;
+    h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+  }
+  if (!h) return nullptr;
+#define KC_SYM(field, sym) api.field = (decltype(api.field))dlsym(h, #sym); if (!api.field) return nullptr;
+  KC_SYM(get_unique_id, ncclGetUniqueId)
+  KC_SYM(comm_init_rank, ncclCommInitRank)
+  KC_SYM(comm_destroy, ncclCommDestroy)
+  KC_SYM(all_gather, ncclAllGather)
+  KC_SYM(all_reduce, ncclAllReduce)
+  KC_SYM(broadcast, ncclBroadcast)
+  KC_SYM(send, ncclSend)
+  KC_SYM(recv, ncclRecv)
+  KC_SYM(group_start, ncclGroupStart)
+  KC_SYM(group_end, ncclGroupEnd)
+  KC_SYM(error_string, ncclGetErrorString)
+#undef KC_SYM
+  api.ok = true;
+  return &api;
+}
+
+#define KC_NCCL_TRY(expr)                                                                 \
+  do {                                                                                    \
+    const ncclResult_t kc_n_ = (expr);                                                    \
+    if (kc_n_ != ncclSuccess) {                                                           \
+      set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr, rccl()->error_string(kc_n_)); \
+      return -EIO;                                                                        \
+    }                                                                                     \
+  } while (0)
+
+// ---------------------------------------------------------------- Comm
+// Collectives over the ranks; every call is made by the driver on behalf of
+// all the shards this process holds (LocalComm: every rank; RcclComm: one).
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  // rows[i] = the row of local shard i (all rows the same length L);
+  // out = rank-major rows of every rank (world * L)
+  virtual int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) = 0;
+  // per local shard: send buffer grouped by destination; Mx[src][dst] record
+  // counts of every rank; recv buffers grouped by source
+  virtual int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx,
+                         uint64_t rec_bytes, const std::vector<void*>& recv) = 0;
+  // *v: in on the local shard of rank `root` (if any), out everywhere
+  virtual int broadcast(int root, uint64_t* v) = 0;
+  // v[i] = the vector of local shard i; out = the element-wise sum over ranks
+  virtual int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) = 0;
+};
+
+class LocalComm final : public Comm {
+ public:
+  explicit LocalComm(std::vector<ShardBase*> shards) : s_(std::move(shards)) {}
+  int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
+    out.clear();
+    for (const auto& r : rows) out.insert(out.end(), r.begin(), r.end());
+    return 0;
+  }
+  int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx,
+                 uint64_t rb, const std::vector<void*>& recv) override {
+    const int R = (int)s_.size();
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every pack is done
+    for (int dst = 0; dst < R; ++dst) {
+      uint64_t roff = 0;
+      for (int src = 0; src < R; ++src) {
+        uint64_t soff = 0;
+        for (int d = 0; d < dst; ++d) soff += Mx[src][d];
+        const uint64_t n = Mx[src][dst];
+        if (n)
+          KC_HIP_TRY(hipMemcpyAsync((char*)recv[dst] + roff * rb, (const char*)send[src] + soff * rb, n * rb,
+                                    hipMemcpyDeviceToDevice, s_[dst]->stream()));
+        roff += n;
+      }
+    }
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
+    return 0;
+  }
+  int broadcast(int, uint64_t*) override { return 0; }   // the driver read it from the local root
+  int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
+    out.assign(v[0].size(), 0);
+    for (const auto& x : v)
+      for (size_t k = 0; k < x.size(); ++k) out[k] += x[k];
+    return 0;
+  }
+
+ private:
+  std::vector<ShardBase*> s_;
+};
+
+class RcclComm final : public Comm {
+ public:
+  // At world 1 every collective is the identity, done on the host; with
+  // KC_RCCL_FORCE=1 they still go through RCCL (tests of the RCCL path).
+  RcclComm(ShardBase* s, ncclComm_t c) : s_(s), comm_(c) {
+    const char* f = getenv("KC_RCCL_FORCE");
+    trivial_ = s->world() == 1 && !(f && f[0] == '1');
+  }
+  ~RcclComm() override {
+    if (buf_) (void)hipFree(buf_);
+    if (comm_ && rccl()) (void)rccl()->comm_destroy(comm_);
+  }
+  int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
+    if (trivial_) {
+      out = rows[0];
+      return 0;
+    }
+    const size_t L = rows[0].size(), R = (size_t)s_->world();
+    KC_TRY(scratch(L * (R + 1)));
+    hipStream_t st = s_->stream();
+    KC_HIP_TRY(hipMemcpyAsync(buf_, rows[0].data(), L * 8, hipMemcpyHostToDevice, st));
+    KC_NCCL_TRY(rccl()->all_gather(buf_, buf_ + L, L, ncclUint64, comm_, st));
+    out.resize(L * R);
+    KC_HIP_TRY(hipMemcpyAsync(out.data(), buf_ + L, L * R * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+  int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
+                 const std::vector<void*>& recv) override {
+    const int R = s_->world(), me = s_->rank();
+    const uint64_t rw = rb / 8;                       // records are whole 8-byte words
+    const uint64_t piece = std::max<uint64_t>(1, PIECE_BYTES / rb);   // records per piece
+    hipStream_t st = s_->stream();
+    KC_NCCL_TRY(rccl()->group_start());
+    uint64_t soff = 0, roff = 0;
+    for (int peer = 0; peer < R; ++peer) {
+      const uint64_t ns = Mx[me][peer], nr = Mx[peer][me];
+      for (uint64_t k = 0; k < ns; k += piece)
+        KC_NCCL_TRY(rccl()->send((const uint64_t*)send[0] + (soff + k) * rw, std::min(piece, ns - k) * rw,
+                                 ncclUint64, peer, comm_, st));
+      for (uint64_t k = 0; k < nr; k += piece)
+        KC_NCCL_TRY(rccl()->recv((uint64_t*)recv[0] + (roff + k) * rw, std::min(piece, nr - k) * rw,
+                                 ncclUint64, peer, comm_, st));
+      soff += ns;
+      roff += nr;
+    }
+    KC_NCCL_TRY(rccl()->group_end());
+    return 0;                                          // stream-ordered before insert
+  }
+  int broadcast(int root, uint64_t* v) override {
+    if (trivial_) return 0;
+    KC_TRY(scratch(1));
+    hipStream_t st = s_->stream();
+    KC_HIP_TRY(hipMemcpyAsync(buf_, v, 8, hipMemcpyHostToDevice, st));
+    KC_NCCL_TRY(rccl()->broadcast(buf_, buf_, 1, ncclUint64, root, comm_, st));
+    KC_HIP_TRY(hipMemcpyAsync(v, buf_, 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+  int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
+    if (trivial_) {
+      out = v[0];
+      return 0;
+    }
+    const size_t L = v[0].size();
+    KC_TRY(scratch(L));
+    hipStream_t st = s_->stream();
+    KC_HIP_TRY(hipMemcpyAsync(buf_, v[0].data(), L * 8, hipMemcpyHostToDevice, st));
+    KC_NCCL_TRY(rccl()->all_reduce(buf_, buf_, L, ncclUint64, ncclSum, comm_, st));
+    out.resize(L);
+    KC_HIP_TRY(hipMemcpyAsync(out.data(), buf_, L * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+
+ private:
+  int scratch(size_t words) {
+    if (words <= cap_) return 0;
+    if (buf_) KC_HIP_TRY(hipFree(buf_));
+    buf_ = nullptr;
+    cap_ = std::max<size_t>(words, 256);
+    KC_HIP_TRY(hipMalloc(&buf_, cap_ * 8));
+    return 0;
+  }
+  ShardBase* s_;
+  bool trivial_ = false;
+  ncclComm_t comm_ = nullptr;
+  uint64_t* buf_ = nullptr;
+  size_t cap_ = 0;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------- driver
+class Group {
+ public:
+  Group(std::vector<ShardBase*> local, std::unique_ptr<Comm> comm, const kc_model_config& cfg)
+      : local_(std::move(local)), comm_(std::move(comm)), cfg_(cfg) {
+    world_ = local_[0]->world();
+    for (auto* s : local_) s->set_async_pack(true);
+    send_.assign(local_.size(), nullptr);
+    recv_.assign(local_.size(), nullptr);
+    send_cap_.assign(local_.size(), 0);
+    recv_cap_.assign(local_.size(), 0);
+  }
+  ~Group() {
+    for (size_t i = 0; i < local_.size(); ++i) {
+      (void)hipSetDevice(local_[i]->device());
+      if (send_[i]) (void)hipFree(send_[i]);
+      if (recv_[i]) (void)hipFree(recv_[i]);
+    }
+  }
+  int run(kc_result* res);
+  const std::vector<std::vector<uint64_t>>& trace() const { return trace_; }
+  uint64_t records_sent() const { return sent_; }
+
+ private:
+  ShardBase* owner_local(int rank) {
+    for (auto* s : local_)
+      if (s->rank() == rank) return s;
+    return nullptr;
+  }
+  int query_parent(int rank, int level, uint64_t idx, uint64_t* key) {
+    uint64_t v = 0;
+    if (ShardBase* s = owner_local(rank)) KC_TRY(s->parent_key(level, idx, &v));
+    KC_TRY(comm_->broadcast(rank, &v));
+    *key = v;
+    return 0;
+  }
+  int buffer(std::vector<uint64_t*>& bufs, std::vector<uint64_t>& caps, size_t i, uint64_t bytes) {
+    if (bytes <= caps[i]) return 0;
+    KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+    KC_HIP_TRY(hipStreamSynchronize(local_[i]->stream()));
+    if (bufs[i]) KC_HIP_TRY(hipFree(bufs[i]));
+    bufs[i] = nullptr;
+    const uint64_t nb = std::max<uint64_t>(bytes, 2 * caps[i]);
+    KC_HIP_TRY(hipMalloc(&bufs[i], nb));
+    caps[i] = nb;
+    return 0;
+  }
+  int error_trace(uint64_t err, int level, kc_result* res);
+
+  std::vector<ShardBase*> local_;
+  std::unique_ptr<Comm> comm_;
+  kc_model_config cfg_;
+  int world_ = 1;
+  std::vector<uint64_t*> send_, recv_;
+  std::vector<uint64_t> send_cap_, recv_cap_;
+  std::vector<std::vector<uint64_t>> trace_;
+  std::vector<uint64_t> sent_local_;   // records each local shard sent to other ranks
+  uint64_t sent_ = 0;                  // all ranks (after run)
+};
+
+int Group::run(kc_result* res) {
+  memset(res, 0, sizeof *res);
+  res->err_action = res->err_self = res->err_invariant = -1;
+  trace_.clear();
+  sent_ = 0;
+  sent_local_.assign(local_.size(), 0);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t nl = local_.size();
+  const int R = world_;
+  std::vector<uint64_t> status_new(nl), status_err(nl, NONE), e1(nl, NONE);
+  for (size_t i = 0; i < nl; ++i) {
+    KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+    KC_TRY(local_[i]->init(&status_new[i]));
+  }
+  std::vector<uint64_t> widths;
+  int level = 1;
+  uint64_t err = NONE;
+  std::vector<std::vector<uint64_t>> counts(nl, std::vector<uint64_t>(R, 0)), rows(nl);
+  std::vector<uint64_t> all;
+  std::vector<std::vector<uint64_t>> Mx(R, std::vector<uint64_t>(R, 0));
+  for (;;) {
+    const bool last = cfg_.max_levels && level >= cfg_.max_levels;
+    for (size_t i = 0; i < nl; ++i) {
+      std::fill(counts[i].begin(), counts[i].end(), 0);
+      e1[i] = NONE;
+      if (!last) {
+        KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+        KC_TRY(local_[i]->expand(counts[i].data(), &e1[i]));
+        if (level == 1 && e1[i] != NONE && (e1[i] & 0xFF) == 0x12) {
+          // an Init state violates an invariant: level 1's error, ahead of
+          // any level-2 error (distributed.py does the same)
+          status_err[i] = e1[i];
+          e1[i] = NONE;
+        }
+      }
+      rows[i] = counts[i];
+      rows[i].push_back(status_new[i]);
+      rows[i].push_back(status_err[i]);
+    }
+    KC_TRY(comm_->all_gather(rows, all));
+    uint64_t total = 0;
+    err = NONE;
+    for (int r = 0; r < R; ++r) {
+      const uint64_t* row = all.data() + (size_t)r * (R + 2);
+      for (int d = 0; d < R; ++d) Mx[r][d] = row[d];
+      total += row[R];
+      err = std::min(err, row[R + 1]);
+    }
+    if (err != NONE || total == 0) {
+      --level;
+      break;
+    }
+    widths.push_back(total);
+    if (last) break;
+    for (size_t i = 0; i < nl; ++i) {
+      const int me = local_[i]->rank();
+      uint64_t ns = 0, nr = 0;
+      for (int d = 0; d < R; ++d) {
+        ns += Mx[me][d];
+        nr += Mx[d][me];
+      }
+      sent_local_[i] += ns - Mx[me][me];
+      const uint64_t rb = local_[i]->record_bytes();
+      KC_TRY(buffer(send_, send_cap_, i, std::max<uint64_t>(ns, 1) * rb));
+      KC_TRY(buffer(recv_, recv_cap_, i, std::max<uint64_t>(nr, 1) * rb));
+      KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+      KC_TRY(local_[i]->pack(send_[i]));
+    }
+    std::vector<void*> sv(send_.begin(), send_.end()), rv(recv_.begin(), recv_.end());
+    KC_TRY(comm_->all_to_all(sv, Mx, local_[0]->record_bytes(), rv));
+    for (size_t i = 0; i < nl; ++i) {
+      const int me = local_[i]->rank();
+      uint64_t nr = 0;
+      for (int s = 0; s < R; ++s) nr += Mx[s][me];
+      uint64_t n_new = 0, e2 = NONE;
+      KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+      KC_TRY(local_[i]->insert(recv_[i], nr, &n_new, &e2));
+      status_new[i] = n_new;
+      status_err[i] = std::min(e1[i], e2);
+      KC_TRY(local_[i]->advance());
+    }
+    ++level;
+    if ((int)widths.size() >= KC_MAX_LEVELS) {
+      set_error("kc_group_run: more than %d levels", KC_MAX_LEVELS);
+      return -ENOMEM;
+    }
+  }
+  // global totals (the same on every rank)
+  std::vector<std::vector<uint64_t>> mine(nl);
+  for (size_t i = 0; i < nl; ++i) {
+    kc_result r;
+    KC_TRY(local_[i]->result(&r));
+    for (int a = 0; a < KC_NACTIONS; ++a) mine[i].push_back(r.act_gen[a]);
+    for (int a = 0; a < KC_NACTIONS; ++a) mine[i].push_back(r.act_dist[a]);
+    mine[i].push_back(r.init);
+    mine[i].push_back(r.generated);
+    mine[i].push_back(r.distinct);
+    mine[i].push_back(sent_local_[i]);
+  }
+  std::vector<uint64_t> tot;
+  KC_TRY(comm_->all_reduce_sum(mine, tot));
+  for (int a = 0; a < KC_NACTIONS; ++a) {
+    res->act_gen[a] = tot[a];
+    res->act_dist[a] = tot[KC_NACTIONS + a];
+  }
+  res->init = tot[2 * KC_NACTIONS];
+  res->generated = tot[2 * KC_NACTIONS] + tot[2 * KC_NACTIONS + 1];
+  res->distinct = tot[2 * KC_NACTIONS + 2];
+  sent_ = tot[2 * KC_NACTIONS + 3];
+  res->nlevels = (int)widths.size();
+  res->depth = res->nlevels;
+  for (size_t k = 0; k < widths.size(); ++k) res->level_width[k] = widths[k];
+  res->complete = err == NONE && !(cfg_.max_levels && level >= cfg_.max_levels);
+  if (err != NONE) KC_TRY(error_trace(err, level, res));
+  const double d = (double)res->distinct, g = (double)res->generated;
+  res->collision_optimistic = d * (g - d) / 18446744073709551616.0;
+  res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+// Walk the parent keys back across ranks (TLC's trace file), then replay
+// the path on the host: the same protocol as distributed.py's _error.
+int Group::error_trace(uint64_t err, int level, kc_result* res) {
+  const int kind = (int)(err & 0xFF);
+  const int pos = (int)((err >> 8) & 0xFF);
+  std::vector<int> path;
+  int r = (int)(err >> 60), lvl = level;
+  uint64_t idx = (err >> 16) & KEY44;
+  while (lvl > 1) {
+    uint64_t key = 0;
+    KC_TRY(query_parent(r, lvl, idx, &key));
+    path.push_back((int)((key >> 8) & 0xFF));
+    r = (int)(key >> 60);
+    idx = (key >> 16) & KEY44;
+    --lvl;
+  }
+  uint64_t init_key = 0;
+  KC_TRY(query_parent(r, 1, idx, &init_key));
+  std::reverse(path.begin(), path.end());
+  int act = -1, self = -1, inv = -1;
+  KC_TRY(local_[0]->replay((int)(init_key & 0xFFFF), path, kind, pos, trace_, &act, &self, &inv));
+  res->err_kind = kind == 0x12 ? E_INVARIANT : kind;
+  res->err_action = act;
+  res->err_self = self;
+  res->err_invariant = inv;
+  res->err_level = kind == E_INVARIANT ? level + 1 : (kind == 0x12 ? 1 : level);
+  res->trace_len = (int)trace_.size();
+  return 0;
+}
+
+}  // namespace kc
+
+using namespace kc;
+
+struct kc_group {
+  std::unique_ptr<Group> impl;
+};
+
+extern "C" {
+
+int kc_rccl_unique_id(uint8_t* id_out) {
+  if (!id_out) { set_error("kc_rccl_unique_id: NULL"); return -EINVAL; }
+  const RcclApi* api = rccl();
+  if (!api) { set_error("kc_rccl_unique_id: RCCL (librccl.so.1) not loadable"); return -ENODEV; }
+  ncclUniqueId id;
+  KC_NCCL_TRY(api->get_unique_id(&id));
+  static_assert(sizeof(ncclUniqueId) == KC_RCCL_ID_BYTES, "ncclUniqueId size");
+  memcpy(id_out, &id, sizeof id);
+  return 0;
+}
+
+int kc_group_create_rccl(kc_shard* s, const uint8_t* id, kc_group** out) {
+  if (!s || !id || !out) { set_error("kc_group_create_rccl: NULL"); return -EINVAL; }
+  *out = nullptr;
+  const RcclApi* api = rccl();
+  if (!api) { set_error("kc_group_create_rccl: RCCL (librccl.so.1) not loadable"); return -ENODEV; }
+  ShardBase* sh = s->impl.get();
+  KC_HIP_TRY(hipSetDevice(sh->device()));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  ncclComm_t comm = nullptr;
+  KC_NCCL_TRY(api->comm_init_rank(&comm, sh->world(), uid, sh->rank()));
+  *out = new kc_group{std::unique_ptr<Group>(
+      new Group({sh}, std::unique_ptr<Comm>(new RcclComm(sh, comm)), sh->config()))};
+  return 0;
+}
+
+int kc_group_create_local(kc_shard** shards, int nshards, kc_group** out) {
+  if (!shards || nshards < 1 || !out) { set_error("kc_group_create_local: bad argument"); return -EINVAL; }
+  *out = nullptr;
+  std::vector<ShardBase*> v;
+  for (int i = 0; i < nshards; ++i) {
+    if (!shards[i]) { set_error("kc_group_create_local: NULL shard"); return -EINVAL; }
+    ShardBase* sh = shards[i]->impl.get();
+    if (sh->world() != nshards || sh->rank() != i || sh->device() != shards[0]->impl->device()) {
+      set_error("kc_group_create_local: shard %d must be rank %d of %d on one device", i, i, nshards);
+      return -EINVAL;
+    }
+    v.push_back(sh);
+  }
+  *out = new kc_group{std::unique_ptr<Group>(
+      new Group(v, std::unique_ptr<Comm>(new LocalComm(v)), v[0]->config()))};
+  return 0;
+}
+
+void kc_group_destroy(kc_group* g) { delete g; }
+
+int kc_group_run(kc_group* g, kc_result* res) {
+  if (!g || !res) { set_error("kc_group_run: NULL"); return -EINVAL; }
+  return g->impl->run(res);
+}
+
+int kc_group_trace_tuple(kc_group* g, int i, uint64_t* out) {
+  if (!g || !out) { set_error("kc_group_trace_tuple: NULL"); return -EINVAL; }
+  const auto& t = g->impl->trace();
+  if (i < 0 || i >= (int)t.size()) { set_error("kc_group_trace_tuple: index"); return -EINVAL; }
+  std::copy(t[i].begin(), t[i].end(), out);
+  return (int)t[i].size();
+}
+
+uint64_t kc_group_records_sent(const kc_group* g) { return g ? g->impl->records_sent() : 0; }
+
+}  // extern "C"

@@ -109,6 +109,13 @@ SIGNATURES = [
     ("kc_shard_result", C.c_int, [_P, C.POINTER(KcResult)]),
     ("kc_shard_claim_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P, _U64P]),
     ("kc_shard_owner", C.c_int, [C.c_uint64, C.c_int]),
+    ("kc_rccl_unique_id", C.c_int, [C.c_char_p]),
+    ("kc_group_create_rccl", C.c_int, [_P, C.c_char_p, C.POINTER(_P)]),
+    ("kc_group_create_local", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(_P)]),
+    ("kc_group_destroy", None, [_P]),
+    ("kc_group_run", C.c_int, [_P, C.POINTER(KcResult)]),
+    ("kc_group_trace_tuple", C.c_int, [_P, C.c_int, _U64P]),
+    ("kc_group_records_sent", C.c_uint64, [_P]),
     ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_init", C.c_int, [C.POINTER(KcModelConfig), _U64P, C.c_int]),

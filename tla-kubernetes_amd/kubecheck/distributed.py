@@ -123,6 +123,110 @@ class HipShard:
             self._h = C.c_void_p()
 
 
+class NativeShardedChecker:
+    """The sharded BFS with the native level loop (libkubecheck kc_group_*):
+    the same protocol and result dict as :class:`ShardedModelChecker`, with
+    the levels driven in C++ over RCCL instead of from Python.
+
+    * ``NativeShardedChecker(cfg, rank, world)`` inside a torch.distributed
+      job (one process per GPU): rank 0 makes the RCCL id, torch broadcasts
+      it, every rank joins one RCCL communicator.
+    * ``NativeShardedChecker(cfg, emulate=R)``: ranks 0..R-1 in this process
+      on one GPU, collectives by device copies (the multi-rank protocol on
+      one GPU)."""
+
+    def __init__(self, cfg: ModelConfig, rank: int = 0, world: int = 1, emulate: int = 0, group=None):
+        self._lib = load()
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        self.spec = Spec(cfg)
+        self._shards = []
+        self._g = C.c_void_p()
+        if emulate:
+            for r in range(emulate):
+                h = C.c_void_p()
+                check("kc_shard_create", self._lib.kc_shard_create(C.byref(self._c), r, emulate, C.byref(h)))
+                self._shards.append(h)
+            arr = (C.c_void_p * emulate)(*[h.value for h in self._shards])
+            check("kc_group_create_local", self._lib.kc_group_create_local(arr, emulate, C.byref(self._g)))
+            self.world = emulate
+        else:
+            import torch
+            import torch.distributed as dist
+
+            h = C.c_void_p()
+            check("kc_shard_create", self._lib.kc_shard_create(C.byref(self._c), rank, world, C.byref(h)))
+            self._shards.append(h)
+            uid = C.create_string_buffer(128)
+            if rank == 0:
+                check("kc_rccl_unique_id", self._lib.kc_rccl_unique_id(uid))
+            if world > 1:
+                t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).to(
+                    "cuda" if dist.get_backend(group) == "nccl" else "cpu")
+                dist.broadcast(t, src=0, group=group)
+                uid = C.create_string_buffer(bytes(t.cpu().tolist()), 128)
+            check("kc_group_create_rccl", self._lib.kc_group_create_rccl(h, uid, C.byref(self._g)))
+            self.world = world
+        self.records_sent = 0
+        self.record_bytes = int(self._lib.kc_shard_record_bytes(self._shards[0]))
+
+    def run(self) -> dict:
+        r = KcResult()
+        check("kc_group_run", self._lib.kc_group_run(self._g, C.byref(r)))
+        self.records_sent = int(self._lib.kc_group_records_sent(self._g))
+        na = len(ACTIONS)
+        out = {
+            "init": int(r.init), "generated": int(r.generated), "distinct": int(r.distinct),
+            "depth": int(r.depth), "level_width": [int(r.level_width[i]) for i in range(r.nlevels)],
+            "act_gen": {a: int(r.act_gen[i]) for i, a in enumerate(ACTIONS)},
+            "act_dist": {a: int(r.act_dist[i]) for i, a in enumerate(ACTIONS)},
+            "seconds": float(r.seconds), "error": None, "complete": bool(r.complete),
+        }
+        assert len(out["act_gen"]) == na
+        if r.err_kind:
+            tw = self.spec.tuple_words
+            trace = []
+            for i in range(r.trace_len):
+                buf = (C.c_uint64 * tw)()
+                check("kc_group_trace_tuple", self._lib.kc_group_trace_tuple(self._g, i, buf))
+                trace.append([int(x) for x in buf])
+            out.update(error={1: "assertion", 2: "invariant", 3: "deadlock"}[r.err_kind],
+                       error_level=int(r.err_level), trace=trace, trace_len=int(r.trace_len))
+            if r.err_kind == 1:
+                out["error_action"] = ACTIONS[r.err_action]
+            if r.err_kind == 2:
+                out["error_invariant"] = INVARIANTS.get(r.err_invariant)
+        return out
+
+    def claim_times(self):
+        """(k_claim ms, launches, parents) of this process's shards since the last call."""
+        ms, n, p = C.c_double(), C.c_uint64(), C.c_uint64()
+        tot = [0.0, 0, 0]
+        for h in self._shards:
+            check("kc_shard_claim_times", self._lib.kc_shard_claim_times(h, C.byref(ms), C.byref(n), C.byref(p)))
+            tot = [tot[0] + ms.value, tot[1] + int(n.value), tot[2] + int(p.value)]
+        return tuple(tot)
+
+    def shard_result(self, i: int = 0) -> dict:
+        r = KcResult()
+        check("kc_shard_result", self._lib.kc_shard_result(self._shards[i], C.byref(r)))
+        return {"generated": int(r.generated), "init": int(r.init), "distinct": int(r.distinct)}
+
+    def close(self) -> None:
+        if self._g:
+            self._lib.kc_group_destroy(self._g)
+            self._g = C.c_void_p()
+        for h in self._shards:
+            self._lib.kc_shard_destroy(h)
+        self._shards = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ShardedModelChecker:
     """Level-synchronous sharded BFS driver (collectives via torch.distributed)."""
 
@@ -354,8 +458,12 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     rank, world = dist.get_rank(), dist.get_world_size()
     cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20, timing=0 if args.no_timing else 2)
-    be = HipShard(cfg, rank, world)
-    mc = ShardedModelChecker(cfg, be)
+    native = os.environ.get("KC_PY_DRIVER", "0") != "1"
+    if native:                                        # the C++ level loop over RCCL
+        mc = be = NativeShardedChecker(cfg, rank, world)
+    else:                                             # the Python level loop (torch.distributed)
+        be = HipShard(cfg, rank, world)
+        mc = ShardedModelChecker(cfg, be)
     for _ in range(args.warmup):
         mc.run()
     be.claim_times()                                  # reset
@@ -365,7 +473,7 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     res, sent = None, 0
     for _ in range(args.steps):
         res = mc.run()
-        sent += mc.records_sent
+        sent += 0 if native else mc.records_sent
         if not res["complete"] or res["error"]:
             raise RuntimeError(f"sharded check incomplete: error={res['error']} depth={res['depth']}")
     torch.cuda.synchronize()
@@ -374,15 +482,17 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     ms, launches, parents = be.claim_times()
-    mine = be.result()
+    mine = be.shard_result() if native else be.result()
     S = 8 * Spec(cfg).state_words
     gen_local = mine["generated"] * args.steps        # successors of this rank's parents
     claim_bytes = parents * S + gen_local * 64
+    if native:
+        sent = mc.records_sent * args.steps if rank == 0 else 0    # already summed over ranks
     agg = torch.tensor([claim_bytes, int(ms * 1e6), launches, sent * be.record_bytes],
                        dtype=torch.int64, device="cuda")
     dist.all_reduce(agg, op=dist.ReduceOp.SUM)
     tot_bytes, tot_ns, tot_launch, xgmi = [int(x) for x in agg.tolist()]
-    be.close()
+    mc.close() if native else be.close()
     out = None
     if rank == 0:
         golden = golden_check(args.workload, res) if golden_check else None
@@ -396,7 +506,8 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
             "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
                        "distinct": res["distinct"], "generated": res["generated"],
                        "depth": res["depth"], "golden_check": golden,
-                       "path": "sharded (kc_shard_* stages, fingerprint-owner sharding)",
+                       "path": ("sharded, native C++ level loop over RCCL (kc_group_run)" if native else
+                                "sharded, Python level loop over torch.distributed (kc_shard_* stages)"),
                        "parallelism": f"{world} GPUs, fingerprint-owner sharding, "
                                       "RCCL all-to-all per BFS level",
                        "xgmi_bytes_per_step": xgmi // max(args.steps, 1),
