@@ -57,7 +57,28 @@ def parse():
                     help="fpset workload: table load after the inserts")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded (multi-GPU) stages even at N=1 (run under torch.distributed.run)")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="only start the ranks (gloo, no GPU) and report what each saw: a CPU test of "
+                         "the --gpus N self-launch")
     return ap.parse_args()
+
+
+def launcher_check(args) -> dict:
+    """Every rank joins a gloo group and all-gathers (rank, world, local rank)."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    mine = torch.tensor([rank, world, int(os.environ.get("LOCAL_RANK", "-1"))], dtype=torch.int64)
+    out = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(out, mine)
+    dist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {"launcher_check": True, "n_gpus": args.gpus, "world": world,
+            "ranks": [o.tolist() for o in out],
+            "master_addr": os.environ.get("MASTER_ADDR")}
 
 
 def state_bytes(kw) -> int:
@@ -321,6 +342,11 @@ def main():
         sys.exit(relaunch(args))
     if args.gpus != world and world != 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launcher_check:
+        out = launcher_check(args)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        return
     if args.workload == "fpset":
         if args.gpus > 1:
             from kubecheck.sharded_fpset import bench_sharded_fpset

@@ -117,3 +117,21 @@ def test_sharded_error_paths(tmp_path, fixtures, key, kw, kind):
     if kind == "assertion":
         assert r["error_action"] == fx["err_action"]
     assert r["trace"][0] == fx["trace"][0]
+
+
+def test_bench_self_launch_two_ranks():
+    # `python bench.py --gpus 2` with no launcher around it must start the two
+    # ranks itself (torch.distributed.run as a child process, 127.0.0.1)
+    import subprocess
+
+    root = os.path.dirname(HERE)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"],
+                         capture_output=True, text=True, timeout=300, cwd=root,
+                         env={k: v for k, v in os.environ.items()
+                              if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")})
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    rep = json.loads(line)
+    assert rep["world"] == 2 and rep["n_gpus"] == 2 and rep["master_addr"] == "127.0.0.1"
+    assert sorted(r[0] for r in rep["ranks"]) == [0, 1] and all(r[1] == 2 for r in rep["ranks"])
+    assert sorted(r[2] for r in rep["ranks"]) == [0, 1]
