@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="np2", choices=list(WORKLOADS) + ["fpset"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="budget of the CPU baseline sample (oracle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
@@ -158,15 +158,43 @@ def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     return None, None
 
 
+def host_cores() -> int:
+    """Threads for the CPU comparator: this process's CPUs, at most 16 (the
+    GPU box's CPU share per GPU; os.cpu_count() there shows the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(kw, seconds):
+    """The CPU comparator (TLC's -workers = all host cores role):
+    the oracle's multi-threaded BFS of the same model from Init, on this
+    process's host cores (<= 16), stopped after `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
+    threads = host_cores()
     cfg = pyoracle.config(kw["nc"], kw["np"], kw["ns"], keep_trace=False)
-    rate, done = pyoracle.bench_sample(cfg, seconds)
-    return {"value": round(rate, 1), "unit": "distinct states/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/kubeapi_oracle.c single-threaded BFS of the same model from Init, "
-                      f"stopped after {seconds:.0f} s ({done} distinct states)"}
+    cfg.fpset_log2 = 22 if (kw["nc"], kw["np"], kw["ns"]) == (1, 1, 1) else 29
+    r = pyoracle.bench_parallel(cfg, threads, seconds)
+    what = "the whole model" if r["complete"] else f"{r['levels']} BFS levels from Init"
+    return {"value": round(r["rate"], 1), "unit": "distinct states/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"oracle/kubeapi_oracle.c ko_bench_parallel: level-synchronous BFS of the same "
+                      f"model on {threads} threads with a lock-free 64-bit fingerprint set, {what} "
+                      f"({r['distinct']} distinct, {r['generated']} generated) in {r['seconds']:.1f} s"}
 
 
 def bench_single(args, kw, desc):

@@ -1032,3 +1032,178 @@ done:
   if (states_done) *states_done = distinct;
   return el > 0 ? distinct / el : 0;
 }
+
+/* ------------------------------------------------ multi-core comparator */
+/* A level-synchronous BFS of the same spec on `threads` host threads: the
+ * CPU comparator bench.py times next to the GPU (TLC's "-workers = all host
+ * cores" role; the reference run used 4 workers, MC.out:5).
+ * A persistent pool of threads (one barrier per level) takes chunks of the
+ * frontier, expands them with the same action functions as ko_run, and
+ * inserts 64-bit fingerprints into one lock-free open-addressing set (CAS
+ * on the slot; the table is transparent-huge-page backed); new states go to
+ * the thread's own next-frontier buffer, concatenated after the level.
+ * Counts (distinct, generated, level widths) equal ko_run's; which parent
+ * first reaches a state depends on thread timing, so per-action distinct
+ * splits are not reproduced (they are not reported).  Stops after `budget`
+ * seconds (checked every chunk) or at the end of the state space. */
+#include <pthread.h>
+#include <stdatomic.h>
+#include <sys/mman.h>
+
+typedef struct {
+  const model *m;
+  pvec cur;
+  _Atomic uint64_t next;            /* next frontier index to take */
+  _Atomic uint64_t *slots;          /* fingerprint set (0 = empty) */
+  uint64_t mask;
+  struct timespec t0;
+  double budget;
+  _Atomic int stop;
+  int done;                         /* the pool exits */
+  pthread_barrier_t start, end;
+} par_level;
+
+typedef struct {
+  par_level *L;
+  pvec out;
+  uint64_t generated;
+} par_worker;
+
+static double elapsed_since(const struct timespec *t0) {
+  struct timespec t1; clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (t1.tv_sec - t0->tv_sec) + 1e-9 * (t1.tv_nsec - t0->tv_nsec);
+}
+
+static void pv_append(pvec *a, const uint64_t *w) {
+  if (a->n == a->cap) { a->cap = a->cap ? a->cap * 2 : 4096;
+    a->v = realloc(a->v, a->cap * a->words * 8);
+    if (!a->v) { fprintf(stderr, "kubeapi_oracle: out of memory\n"); abort(); } }
+  memcpy(a->v + a->n * a->words, w, a->words * 8); a->n++;
+}
+/* 64-bit fingerprint of packed canonical words (nonzero) */
+static uint64_t packed_fp(const uint64_t *w, int n) {
+  uint64_t a = 0x243f6a8885a308d3ull;
+  for (int i = 0; i < n; i++) a = mix64(a ^ w[i]) + 0x9e3779b97f4a7c15ull;
+  return a ? a : 1;
+}
+
+static int par_insert(par_level *L, uint64_t fp) {   /* 1 if new */
+  if (!fp) fp = 1;
+  uint64_t i = (fp * 0x9e3779b97f4a7c15ull >> 17) & L->mask;
+  for (;;) {
+    uint64_t e = atomic_load_explicit(&L->slots[i], memory_order_relaxed);
+    if (e == fp) return 0;
+    if (e == 0) {
+      uint64_t z = 0;
+      if (atomic_compare_exchange_strong(&L->slots[i], &z, fp)) return 1;
+      if (z == fp) return 0;
+    }
+    i = (i + 1) & L->mask;
+  }
+}
+
+static void *par_work(void *arg) {
+  par_worker *w = arg;
+  par_level *L = w->L;
+  const model *m = L->m;
+  kstate s, succ[MAXSUCC]; uint8_t act[MAXSUCC];
+  emitter e = {succ, act, 0, MAXSUCC, -1, -1, NULL};
+  const int pw = L->cur.words;
+  for (;;) {
+    pthread_barrier_wait(&L->start);
+    if (L->done) break;
+    for (;;) {
+      if (atomic_load_explicit(&L->stop, memory_order_relaxed)) break;
+      uint64_t i0 = atomic_fetch_add(&L->next, 512);
+      if (i0 >= L->cur.n) break;
+      uint64_t i1 = i0 + 512 < L->cur.n ? i0 + 512 : L->cur.n;
+      for (uint64_t i = i0; i < i1; i++) {
+        pv_get(&L->cur, m, i, &s);
+        expand(m, &s, &e);
+        for (int k = 0; k < e.n; k++) {
+          w->generated++;
+          /* the packed words are canonical: hash those (cheaper than the
+           * whole kstate) and store them as they are */
+          kpacked pk; kpack(m, &succ[k], &pk);
+          if (par_insert(L, packed_fp(pk.w, pw))) pv_append(&w->out, pk.w);
+        }
+      }
+      if (elapsed_since(&L->t0) > L->budget) atomic_store(&L->stop, 1);
+    }
+    pthread_barrier_wait(&L->end);
+  }
+  return NULL;
+}
+
+double ko_bench_parallel(const ko_config *cfg, int threads, double budget, ko_par_result *out) {
+  model m; model_init(&m, cfg);
+  memset(out, 0, sizeof *out);
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  const int log2 = cfg->fpset_log2 > 0 ? cfg->fpset_log2 : 28;
+  static par_level L;
+  memset(&L, 0, sizeof L);
+  L.m = &m; L.mask = (1ull << log2) - 1; L.budget = budget;
+  const size_t bytes = (1ull << log2) * sizeof(uint64_t);
+  clock_gettime(CLOCK_MONOTONIC, &L.t0);
+  L.slots = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (L.slots == MAP_FAILED) { fprintf(stderr, "kubeapi_oracle: out of memory\n"); abort(); }
+  madvise((void *)L.slots, bytes, MADV_HUGEPAGE);
+  const int pw = 1 + 2 * (cfg->nc + cfg->np + cfg->ns);
+  L.cur = (pvec){0, 0, 0, pw};
+  kstate inits[16]; int ni = init_states(&m, inits);
+  for (int i = 0; i < ni; i++) {
+    kpacked pk; kpack(&m, &inits[i], &pk);
+    out->generated++;
+    if (par_insert(&L, packed_fp(pk.w, pw))) pv_append(&L.cur, pk.w);
+  }
+  out->distinct = L.cur.n;
+  par_worker *W = calloc(threads, sizeof *W);
+  pthread_t *T = calloc(threads, sizeof *T);
+  pthread_barrier_init(&L.start, NULL, threads + 1);
+  pthread_barrier_init(&L.end, NULL, threads + 1);
+  for (int t = 0; t < threads; t++) {
+    W[t].L = &L; W[t].out.words = pw;
+    pthread_create(&T[t], NULL, par_work, &W[t]);
+  }
+  while (L.cur.n && !atomic_load(&L.stop)) {
+    out->levels++;
+    atomic_store(&L.next, 0);
+    for (int t = 0; t < threads; t++) W[t].out.n = 0;
+    pthread_barrier_wait(&L.start);
+    pthread_barrier_wait(&L.end);
+    uint64_t total = 0;
+    for (int t = 0; t < threads; t++) {
+      total += W[t].out.n;
+      out->generated += W[t].generated;
+      W[t].generated = 0;
+    }
+    pvec nxt = {0, 0, 0, pw};
+    nxt.cap = total ? total : 1;
+    nxt.v = malloc(nxt.cap * pw * 8);
+    if (!nxt.v) { fprintf(stderr, "kubeapi_oracle: out of memory\n"); abort(); }
+    for (int t = 0; t < threads; t++) {
+      memcpy(nxt.v + nxt.n * pw, W[t].out.v, W[t].out.n * pw * 8);
+      nxt.n += W[t].out.n;
+    }
+    out->distinct += total;
+    free(L.cur.v);
+    L.cur = nxt;
+    if ((out->distinct + L.cur.n) * 10 > (L.mask + 1) * 6) {   /* keep the set below 60% */
+      out->set_full = 1;
+      break;
+    }
+  }
+  L.done = 1;
+  pthread_barrier_wait(&L.start);
+  for (int t = 0; t < threads; t++) pthread_join(T[t], NULL);
+  out->complete = L.cur.n == 0;
+  out->seconds = elapsed_since(&L.t0);
+  out->threads = threads;
+  pthread_barrier_destroy(&L.start);
+  pthread_barrier_destroy(&L.end);
+  for (int t = 0; t < threads; t++) free(W[t].out.v);
+  free(W); free(T); free(L.cur.v);
+  munmap((void *)L.slots, bytes);
+  return out->seconds > 0 ? out->distinct / out->seconds : 0;
+}

@@ -131,6 +131,17 @@ int ko_successors(const ko_config *cfg, const uint64_t *tuple, int *actions,
  * expand+fingerprint+dedup work.  Used by bench.py's cpu_baseline leg. */
 double ko_bench_sample(const ko_config *cfg, double seconds_budget, uint64_t *states_done);
 
+/* Multi-core comparator (bench.py cpu_baseline): level-synchronous BFS on
+ * `threads` host threads with a lock-free 64-bit fingerprint set of
+ * 2^fpset_log2 slots (default 2^28), stopped after `seconds_budget`.
+ * Returns distinct states/s. */
+typedef struct {
+  uint64_t distinct, generated;
+  int levels, complete, set_full, threads;
+  double seconds;
+} ko_par_result;
+double ko_bench_parallel(const ko_config *cfg, int threads, double seconds_budget, ko_par_result *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,7 @@
  *
  *   kubeapi_oracle [-nc N] [-np N] [-ns N] [-nofail] [-notimeout]
  *                  [-nodeadlock] [-maxlevels L] [-maxdistinct D]
- *                  [-variant V] [-trace]
+ *                  [-variant V] [-trace] [-threads T [-budget S]]
  */
 #include "kubeapi_oracle.h"
 #include <stdio.h>
@@ -14,7 +14,8 @@
 
 int main(int argc, char **argv) {
   ko_config cfg = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 128, 0, 0, 0};
-  int print_trace = 0;
+  int print_trace = 0, threads = 0;
+  double budget = 1e30;
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "-nc") && i + 1 < argc) cfg.nc = atoi(argv[++i]);
     else if (!strcmp(argv[i], "-np") && i + 1 < argc) cfg.np = atoi(argv[++i]);
@@ -30,7 +31,19 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "-fp64")) cfg.fp_bits = 64;
     else if (!strcmp(argv[i], "-fpsetlog2") && i + 1 < argc) cfg.fpset_log2 = atoi(argv[++i]);
     else if (!strcmp(argv[i], "-progress")) cfg.progress = 1;
+    else if (!strcmp(argv[i], "-threads") && i + 1 < argc) threads = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "-budget") && i + 1 < argc) budget = atof(argv[++i]);
     else { fprintf(stderr, "unknown arg %s\n", argv[i]); return 2; }
+  }
+  if (threads > 0) {          /* the multi-core comparator: counts and wall time only */
+    ko_par_result p;
+    double rate = ko_bench_parallel(&cfg, threads, budget, &p);
+    printf("{\"nc\": %d, \"np\": %d, \"ns\": %d, \"threads\": %d, \"distinct\": %llu, "
+           "\"generated\": %llu, \"levels\": %d, \"complete\": %d, \"set_full\": %d, "
+           "\"seconds\": %.3f, \"distinct_per_s\": %.1f}\n",
+           cfg.nc, cfg.np, cfg.ns, p.threads, (unsigned long long)p.distinct,
+           (unsigned long long)p.generated, p.levels, p.complete, p.set_full, p.seconds, rate);
+    return 0;
   }
   static ko_result r;
   void *h = ko_run(&cfg, &r);

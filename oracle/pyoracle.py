@@ -144,6 +144,25 @@ def successors(cfg: KoConfig, tup):
     return [(ACTIONS[acts[i]], out[i]) for i in range(n)], None
 
 
+class KoParResult(C.Structure):
+    _fields_ = [("distinct", C.c_uint64), ("generated", C.c_uint64), ("levels", C.c_int),
+                ("complete", C.c_int), ("set_full", C.c_int), ("threads", C.c_int),
+                ("seconds", C.c_double)]
+
+
+def bench_parallel(cfg: KoConfig, threads: int, seconds: float) -> dict:
+    """Multi-core comparator (ko_bench_parallel): BFS from Init on `threads`
+    host threads for about `seconds`."""
+    L = lib()
+    L.ko_bench_parallel.restype = C.c_double
+    L.ko_bench_parallel.argtypes = [C.POINTER(KoConfig), C.c_int, C.c_double, C.POINTER(KoParResult)]
+    r = KoParResult()
+    rate = L.ko_bench_parallel(C.byref(cfg), threads, seconds, C.byref(r))
+    return {"rate": rate, "distinct": r.distinct, "generated": r.generated, "levels": r.levels,
+            "complete": bool(r.complete), "set_full": bool(r.set_full), "threads": r.threads,
+            "seconds": r.seconds}
+
+
 def bench_sample(cfg: KoConfig, seconds: float):
     done = C.c_uint64()
     rate = lib().ko_bench_sample(C.byref(cfg), seconds, C.byref(done))

@@ -83,3 +83,15 @@ def test_successor_semantics_spot(oracle):
     s = succ[0][1]
     succ2, _ = oracle.successors(cfg, s)
     assert [a for a, _ in succ2] == ["DoRequest"] * 3 + ["PVCStart"]
+
+
+def test_parallel_comparator_counts(mcout, oracle):
+    # the multi-core CPU comparator (bench.py cpu_baseline) explores the same
+    # state space: MC.out's totals (MC.out:1098) on 1 and 4 threads
+    for threads in (1, 4):
+        cfg = oracle.config(keep_trace=False)
+        cfg.fpset_log2 = 22
+        r = oracle.bench_parallel(cfg, threads, 60.0)
+        assert r["complete"] and not r["set_full"]
+        assert (r["distinct"], r["generated"], r["levels"]) == (
+            mcout["distinct"], mcout["generated"], mcout["depth"])
