@@ -179,6 +179,9 @@ typedef struct {
   uint64_t fpset_probes;   /* FPSet insert probes (level-unique successors) */
   uint64_t batch_inserts;  /* batch-table inserts (= generated successors) */
   uint64_t levels_chunks;  /* expansion chunks over the whole run */
+  uint64_t outdeg_hist[16]; /* TLC outdegree (msg 2268): expanded states by the number of
+                              new states first reached from them; [15] = 15 or more
+                              (single-GPU engine; zero in the sharded path) */
 } kc_result;
 
 typedef struct kc_engine kc_engine;
@@ -206,6 +209,10 @@ int kc_engine_kernel_times(kc_engine *e, double *ms4, uint64_t *launches4);
  * whole levels inside one single-workgroup launch): its device time in ms
  * (with cfg.timing), launches, and the BFS levels it expanded. */
 int kc_engine_narrow_times(kc_engine *e, double *ms, uint64_t *launches, uint64_t *levels);
+/* TLC's checkFPs on the last run's seen-set ("based on the actual
+ * fingerprints", MC.out:42): the minimum gap between sorted fingerprints;
+ * *prob_out = 1/min_gap. */
+int kc_engine_check_fps(kc_engine *e, uint64_t *min_gap_out, double *prob_out);
 
 /* --------------------------------------------------- Sharded (multi-GPU) */
 /* Fingerprint-owner-sharded BFS, one process per GPU (replaces TLC's

@@ -887,11 +887,13 @@ void *ko_run(const ko_config *cfg, ko_result *res) {
         if (s->lr_present[c]) { res->cov_lreq++; res->cov_objs += popc64(s->lr_objs[c]); }
       }
       expand(m, s, &e);
+      int fresh = 0;
       /* successors generated before a failing action are still generated */
       for (int k = 0; k < e.n; k++) {
         res->generated++; res->act_gen[act[k]]++;
         uint64_t a, b; fp128(&succ[k], &a, &b);
         if (fs_put(&fs, a, b)) {
+          fresh++;
           res->act_dist[act[k]]++;
           pv_push(&nxt, m, &succ[k]);
           if (cfg->keep_trace) tv_push(&tv, cur_base + i, k);
@@ -906,6 +908,7 @@ void *ko_run(const ko_config *cfg, ko_result *res) {
         fail_gidx = cur_base + i; res->err_level = level; break;
       }
       res->outdeg_hist[e.n < 31 ? e.n : 31]++;
+      res->newdeg_hist[fresh < 31 ? fresh : 31]++;
       if (e.n == 0 && cfg->check_deadlock) {
         res->err_kind = KO_ERR_DEADLOCK; fail_gidx = cur_base + i; res->err_level = level; break;
       }

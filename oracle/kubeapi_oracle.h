@@ -90,6 +90,8 @@ typedef struct {
   uint64_t cov_api2;       /* sum |apiState|^2        MC.out:1080 */
   uint64_t branch[KO_NBRANCH]; /* IF/CASE branch evaluation counts, KO_B_* */
   uint64_t outdeg_hist[32];/* successors-per-state histogram */
+  uint64_t newdeg_hist[32];/* new (first-reached) successors per expanded state: TLC's
+                              outdegree (msg 2268, MC.out:1104) under a sequential BFS */
   int nlevels;
   uint64_t level_width[KO_MAXLEVELS];
   /* error report */

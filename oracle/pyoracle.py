@@ -45,6 +45,7 @@ class KoResult(C.Structure):
                 ("cov_api", C.c_uint64), ("cov_req", C.c_uint64), ("cov_lreq", C.c_uint64),
                 ("cov_objs", C.c_uint64), ("cov_api2", C.c_uint64),
                 ("branch", C.c_uint64 * NBRANCH), ("outdeg_hist", C.c_uint64 * 32),
+                ("newdeg_hist", C.c_uint64 * 32),
                 ("nlevels", C.c_int), ("level_width", C.c_uint64 * MAXLV),
                 ("err_kind", C.c_int), ("err_action", C.c_int), ("err_self", C.c_int),
                 ("err_invariant", C.c_int), ("err_level", C.c_int), ("trace_len", C.c_int),
@@ -103,6 +104,7 @@ def run(cfg: KoConfig) -> dict:
                 "api2": r.cov_api2},
         "branch": {b: int(r.branch[i]) for i, b in enumerate(BRANCHES)},
         "level_width": [int(r.level_width[i]) for i in range(r.nlevels)],
+        "newdeg_hist": [int(x) for x in r.newdeg_hist],
         "err_kind": r.err_kind, "err_action": ACTIONS[r.err_action] if r.err_action >= 0 else None,
         "err_self": r.err_self, "err_invariant": r.err_invariant, "err_level": r.err_level,
         "trace_len": r.trace_len, "seconds": r.seconds, "trace": [], "trace_text": "",

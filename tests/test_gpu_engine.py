@@ -168,3 +168,25 @@ def test_config_switches(fixtures, key, kw):
     assert r.complete and r.error is None
     assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+
+
+@pytest.mark.parametrize("key,kw", [("model1", {}), ("np2_40levels", dict(np=2, max_levels=40)),
+                                    ("model1_fail0_timeout0", dict(can_fail=0, can_timeout=0)),
+                                    ("nc2_np0", dict(nc=2, np=0))])
+def test_outdegree_histogram(fixtures, key, kw):
+    # TLC's outdegree (msg 2268, MC.out:1104) = new states first reached from
+    # each expanded state; under sequential BFS order it is exactly the
+    # oracle's histogram (the wide and the narrow level paths both count it)
+    fx = fixtures[key]
+    r = run(**kw)
+    if r.error is None:
+        assert r.outdeg_hist == fx["outdeg_hist"]
+
+
+def test_check_fps_min_gap():
+    with ModelChecker(ModelConfig()) as mc:
+        mc.run()
+        gap, prob = mc.check_fps()
+    # 163,408 fingerprints spread over [1, 2^63): the minimum gap is far below
+    # the mean spacing and far above 0 (TLC reports 9.9E-10, MC.out:42)
+    assert 0 < gap < 2**63 // 163408 and prob == pytest.approx(1 / gap)

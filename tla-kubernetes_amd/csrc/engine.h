@@ -29,6 +29,7 @@ class EngineBase {
   virtual int64_t level_tuples(int level, uint64_t* out, uint64_t cap) = 0;
   virtual int state_words() const = 0;
   virtual int tuple_words() const = 0;
+  virtual int check_fps(uint64_t* min_gap, double* prob) = 0;
   void set_capture(int level) { capture_level_ = level; }
   void set_timing(bool on) { timing_ = on ? 1 : 0; }
   void kernel_times(double* ms, uint64_t* launches) const {

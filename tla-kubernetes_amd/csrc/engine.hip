@@ -67,6 +67,22 @@ __global__ void k_level_reset(Counters* __restrict__ C) {
 
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
 
+// fingerprints of a ClaimSet into a dense array (order irrelevant: sorted next)
+__global__ void k_claimset_fps(const ClaimEntry* __restrict__ t, uint64_t nslots,
+                               unsigned long long* __restrict__ out, uint64_t cap,
+                               unsigned long long* __restrict__ n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots && t[i].fp) {
+    const unsigned long long k = atomicAdd(n, 1ull);
+    if (k < cap) out[k] = t[i].fp;
+  }
+}
+__global__ void k_adjacent_min_gap(const unsigned long long* __restrict__ s, uint64_t n,
+                                   unsigned long long* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 < n) atomicMin(out, s[i + 1] - s[i]);
+}
+
 constexpr uint64_t kMaxChunk = (1ull << 27) - 256;
 
 template <class M>
@@ -367,6 +383,56 @@ class EngineT final : public EngineBase {
   }
 
   size_t trace_text(char* buf, size_t cap) const override;
+
+  // TLC checkFPs over the ClaimSet's fingerprints: compact, radix-sort,
+  // minimum adjacent gap (MC.out:42 "based on the actual fingerprints").
+  int check_fps(uint64_t* min_gap, double* prob) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    const uint64_t cnt = std::max<uint64_t>(cs_.count, 2);
+    unsigned long long *a = nullptr, *b = nullptr, *d_n = nullptr;
+    void* tmp = nullptr;
+    int rc = 0;
+    unsigned long long n = 0, gap = ~0ull;
+    if (hipMalloc(&a, cnt * 8) != hipSuccess || hipMalloc(&b, cnt * 8) != hipSuccess ||
+        hipMalloc(&d_n, 16) != hipSuccess) {
+      set_error("kc_engine_check_fps: out of device memory");
+      rc = -ENOMEM;
+    }
+    if (!rc) {
+      (void)hipMemsetAsync(d_n, 0, 8, st_);
+      (void)hipMemcpyAsync(d_n + 1, &gap, 8, hipMemcpyHostToDevice, st_);
+      hipLaunchKernelGGL(k_claimset_fps, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_,
+                         cs_.t, cs_.nslots, a, cnt, d_n);
+      (void)hipMemcpyAsync(&n, d_n, 8, hipMemcpyDeviceToHost, st_);
+      if (hipStreamSynchronize(st_) != hipSuccess || n > cnt) {
+        set_error("kc_engine_check_fps: fingerprint count %llu > %llu", n, (unsigned long long)cnt);
+        rc = -EIO;
+      }
+    }
+    if (!rc && n > 1) {
+      size_t tb = 0;
+      if (hipcub::DeviceRadixSort::SortKeys(nullptr, tb, a, b, (int)n, 0, 64, st_) != hipSuccess ||
+          hipMalloc(&tmp, tb) != hipSuccess) {
+        set_error("kc_engine_check_fps: sort setup");
+        rc = -EIO;
+      } else {
+        (void)hipcub::DeviceRadixSort::SortKeys(tmp, tb, a, b, (int)n, 0, 64, st_);
+        hipLaunchKernelGGL(k_adjacent_min_gap, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st_, b, n,
+                           d_n + 1);
+        (void)hipMemcpyAsync(&gap, d_n + 1, 8, hipMemcpyDeviceToHost, st_);
+        if (hipStreamSynchronize(st_) != hipSuccess) {
+          set_error("kc_engine_check_fps: HIP failure");
+          rc = -EIO;
+        }
+      }
+    }
+    for (void* p : {(void*)a, (void*)b, (void*)d_n, tmp})
+      if (p) (void)hipFree(p);
+    if (rc) return rc;
+    *min_gap = gap;
+    *prob = (n > 1 && gap && gap != ~0ull) ? 1.0 / (double)gap : 0.0;
+    return 0;
+  }
   int trace_tuple(int i, uint64_t* out) const override {
     if (i < 0 || i >= (int)trace_.size()) {
       set_error("trace index out of range");
@@ -523,6 +589,7 @@ class EngineT final : public EngineBase {
     res->collision_optimistic = d * (gg - d) / 18446744073709551616.0;
     res->fpset_slots = cs_.capacity();
     res->fpset_probes = h_ctr_->probes() + narrow_probes_;
+    for (int b = 0; b < OUTDEG_BINS; ++b) res->outdeg_hist[b] = h_ctr_->outdeg(b);
     res->batch_inserts = h_ctr_->settles();
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -752,6 +819,11 @@ int kc_engine_narrow_times(kc_engine* e, double* ms, uint64_t* launches, uint64_
   if (!e || !ms || !launches || !levels) { set_error("kc_engine_narrow_times: NULL"); return -EINVAL; }
   e->impl->narrow_times(ms, launches, levels);
   return 0;
+}
+
+int kc_engine_check_fps(kc_engine* e, uint64_t* min_gap, double* prob) {
+  if (!e || !min_gap || !prob) { set_error("kc_engine_check_fps: NULL"); return -EINVAL; }
+  return e->impl->check_fps(min_gap, prob);
 }
 
 int kc_engine_kernel_times(kc_engine* e, double* ms4, uint64_t* launches4) {

@@ -26,13 +26,18 @@ namespace kc {
 // address taking an atomic from every workgroup serialises at the memory
 // side (it cost k_settle_rec 4/5 of its time).  The host sums the rows.
 constexpr int CTR_STRIPES = 64;
+constexpr int OUTDEG_BINS = 16;
 struct CtrStripe {                  // 512 B
   unsigned long long act_gen[A_COUNT];
   unsigned long long act_dist[A_COUNT];
   unsigned long long probes;        // FPSet / ClaimSet probes
   unsigned long long settles;       // ClaimSet re-reads in k_settle_*
   unsigned long long next_cand;     // successors of the new states (cumulative)
-  unsigned long long pad[64 - 2 * A_COUNT - 3];
+  // TLC's outdegree (msg 2268, MC.out:1104): new states first reached from
+  // a parent, histogram over the expanded parents (bin OUTDEG_BINS-1 = that
+  // many or more)
+  unsigned long long outdeg[OUTDEG_BINS];
+  unsigned long long pad[64 - 2 * A_COUNT - 3 - OUTDEG_BINS];
 };
 struct Counters {
   unsigned long long err_key;     // min error key of the level (~0 = none)
@@ -49,6 +54,11 @@ struct Counters {
   unsigned long long probes() const { return sum1(&CtrStripe::probes); }
   unsigned long long settles() const { return sum1(&CtrStripe::settles); }
   unsigned long long next_cand() const { return sum1(&CtrStripe::next_cand); }
+  unsigned long long outdeg(int b) const {
+    unsigned long long t = 0;
+    for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].outdeg[b];
+    return t;
+  }
 
  private:
   unsigned long long sum(unsigned long long (CtrStripe::*f)[A_COUNT], int a) const {
@@ -425,8 +435,10 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
        unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
        Counters* __restrict__ C) {
   __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned int sh_deg[OUTDEG_BINS];
   __shared__ unsigned long long sh_cand;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh_cand = 0;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -442,6 +454,7 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
     if (mask) counts = M::plan(load_state<M>(cur, i), f).counts;
   }
   const int cnt = __builtin_popcount(mask);
+  if (i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
   const int lane = (int)(threadIdx.x & 63);
   int incl = cnt;
 #pragma unroll
@@ -494,6 +507,8 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
+    atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
 

@@ -246,10 +246,12 @@ k_nemit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bu
   using State = typename M::State;
   if (!ctl->active) return;
   __shared__ unsigned int sh_dist[A_COUNT];
+  __shared__ unsigned int sh_deg[OUTDEG_BINS];
   __shared__ unsigned int sh_w[4];
   __shared__ unsigned int sh_base;
   __shared__ unsigned long long sh_cand;
   if (threadIdx.x < A_COUNT) sh_dist[threadIdx.x] = 0;
+  if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh_cand = 0;
   const uint64_t n = ctl->n, level_gidx = ctl->level_gidx;
   const unsigned long long tag = pub_tag(ctl->epoch, ctl->level);
@@ -265,6 +267,7 @@ k_nemit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bu
   }
   if (lane == 63) sh_w[wv] = (unsigned int)incl;
   __syncthreads();
+  if (i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
   // publish this workgroup's total tagged with the level (no reset needed),
   // then take the totals of the lower workgroups as they arrive: all
   // NARROW_WG workgroups fit the chip at once, so every one is running
@@ -320,6 +323,8 @@ k_nemit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bu
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_dist[threadIdx.x])
     atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_dist[threadIdx.x]);
+  if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
+    atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&ctl->cand_acc, sh_cand);
 }
 

@@ -88,6 +88,7 @@ class CheckResult:
     fpset_probes: int = 0
     batch_inserts: int = 0
     levels_chunks: int = 0
+    outdeg_hist: List[int] = field(default_factory=list)
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -110,7 +111,8 @@ def _result(r: KcResult) -> CheckResult:
         error_level=r.err_level, trace_len=r.trace_len, seconds=r.seconds,
         collision_optimistic=r.collision_optimistic, fpset_slots=r.fpset_slots,
         peak_frontier=r.peak_frontier, fpset_probes=r.fpset_probes,
-        batch_inserts=r.batch_inserts, levels_chunks=r.levels_chunks)
+        batch_inserts=r.batch_inserts, levels_chunks=r.levels_chunks,
+        outdeg_hist=[int(x) for x in r.outdeg_hist])
 
 
 class ModelChecker:
@@ -157,6 +159,12 @@ class ModelChecker:
         check("kc_engine_kernel_times", self._lib.kc_engine_kernel_times(self._h, ms, cnt))
         names = ["expand", "resolve", "scan", "emit"]
         return {k: (ms[i], int(cnt[i])) for i, k in enumerate(names)}
+
+    def check_fps(self):
+        """TLC checkFPs on the last run's seen-set: (min gap, 1/min gap)."""
+        gap, prob = C.c_uint64(), C.c_double()
+        check("kc_engine_check_fps", self._lib.kc_engine_check_fps(self._h, C.byref(gap), C.byref(prob)))
+        return int(gap.value), prob.value
 
     def narrow_times(self):
         """(ms, launches, levels) of the narrow-level kernel in the last run."""

@@ -47,7 +47,7 @@ class KcResult(C.Structure):
         ("seconds", C.c_double), ("collision_optimistic", C.c_double),
         ("fpset_slots", C.c_uint64), ("peak_frontier", C.c_uint64),
         ("fpset_probes", C.c_uint64), ("batch_inserts", C.c_uint64),
-        ("levels_chunks", C.c_uint64),
+        ("levels_chunks", C.c_uint64), ("outdeg_hist", C.c_uint64 * 16),
     ]
 
 
@@ -95,6 +95,7 @@ SIGNATURES = [
     ("kc_engine_capture_level", C.c_int, [_P, C.c_int]),
     ("kc_engine_kernel_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
     ("kc_engine_narrow_times", C.c_int, [_P, C.POINTER(C.c_double), _U64P, _U64P]),
+    ("kc_engine_check_fps", C.c_int, [_P, _U64P, C.POINTER(C.c_double)]),
     ("kc_shard_create", C.c_int, [C.POINTER(KcModelConfig), C.c_int, C.c_int, C.POINTER(_P)]),
     ("kc_shard_destroy", None, [_P]),
     ("kc_shard_init", C.c_int, [_P, _U64P]),

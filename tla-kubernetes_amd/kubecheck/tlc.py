@@ -8,8 +8,11 @@ Reads the same inputs as the reference's toolbox run: a TLC model config
 `X = TRUE` or TLC's `X <- def` indirection resolved through MC.tla:5-12;
 SPECIFICATION; INVARIANT) and prints TLC's `-tool` message stream
 (@!@!@STARTMSG code:class ... @!@!@ENDMSG code) for the messages the
-reference run shows (MC.out: 2262, 2187, 2185, 2189/2190, 2193, 2201/2772/
-2202, 2199, 2194, 2186) plus violation reports.  The model check itself
+reference run shows (MC.out: 2262, 2187, 2185, 2189/2190, 2193 with both
+collision estimates, 2201/2773/2772/2202 coverage with TLC's source spans,
+2200 progress, 2199, 2194, 2268 outdegree, 2186) plus violation reports.
+SANY's messages (2220/2219) and expression-level coverage (2221) are not
+produced (no TLA+ front end).  The model check itself
 runs on the GPU (kubecheck.ModelChecker); -workers and -fp are accepted for
 command-line compatibility (the GPU replaces the worker pool; fingerprints
 are kubecheck's own 64-bit hash, not TLC's FP64 #K).
@@ -99,8 +102,9 @@ def model_from_cfg(cfg: dict) -> dict:
     unknown = set(cfg["constants"]) - set(KNOWN_CONSTANTS)
     if unknown:
         raise CfgError(f"unknown CONSTANT(s) {sorted(unknown)}")
-    if cfg["invariants"] and set(cfg["invariants"]) != set(KNOWN_INVARIANTS):
-        raise CfgError("kubecheck always checks both TypeOK and OnlyOneVersion")
+    # the INVARIANT list selects the checks (an empty list checks none, as in TLC)
+    kw["invariants"] = (1 if "TypeOK" in cfg["invariants"] else 0) | \
+        (2 if "OnlyOneVersion" in cfg["invariants"] else 0)
     return kw
 
 
@@ -108,6 +112,109 @@ def msg(code: int, text: str, cls: int = 0, tool: bool = True) -> str:
     if not tool:
         return text
     return f"@!@!@STARTMSG {code}:{cls} @!@!@\n{text}\n@!@!@ENDMSG {code} @!@!@"
+
+
+# Source locations TLC's coverage messages print for each action (msg 2772)
+# and for Init (msg 2773): the definition heads in KubeAPI.tla, e.g.
+# "DoRequest(self) ==" at KubeAPI.tla:471, columns 1-15 (MC.out:78-621, :48).
+INIT_SPAN = (455, 1, 455, 4)
+ACTION_SPANS = {
+    "DoRequest": (471, 1, 471, 15), "DoReply": (485, 1, 485, 13),
+    "DoListRequest": (499, 1, 499, 19), "DoListReply": (513, 1, 513, 17),
+    "CStart": (528, 1, 528, 12), "C1": (551, 1, 551, 8), "C10": (558, 1, 558, 9),
+    "C11": (570, 1, 570, 9), "c12": (577, 1, 577, 9), "C13": (589, 1, 589, 9),
+    "C2": (596, 1, 596, 8), "C3": (604, 1, 604, 8), "C8": (611, 1, 611, 8),
+    "C6": (618, 1, 618, 8), "C7": (631, 1, 631, 8), "C4": (638, 1, 638, 8),
+    "C5": (645, 1, 645, 8), "PVCStart": (655, 1, 655, 14), "PVCListedPVCs": (665, 1, 665, 19),
+    "PVCHavePVCs": (673, 1, 673, 17), "PVCDone": (690, 1, 690, 13), "APIStart": (698, 1, 698, 14),
+}
+
+
+def span_text(name: str, span) -> str:
+    l1, c1, l2, c2 = span
+    return f"<{name} line {l1}, col {c1} to line {l2}, col {c2} of module KubeAPI>"
+
+
+def outdegree_stats(hist) -> Optional[tuple]:
+    """(average, minimum, maximum, 95th percentile) of TLC's outdegree (new
+    states first reached from an expanded state) from a 16-bin histogram
+    (the last bin holds 15 or more)."""
+    total = sum(hist)
+    if not total:
+        return None
+    avg = sum(k * v for k, v in enumerate(hist)) / total
+    lo = min(k for k, v in enumerate(hist) if v)
+    hi = max(k for k, v in enumerate(hist) if v)
+    acc, p95 = 0, hi
+    for k, v in enumerate(hist):
+        acc += v
+        if acc >= 0.95 * total:
+            p95 = k
+            break
+    return round(avg), lo, hi, p95
+
+
+def java_e(x: float) -> str:
+    """TLC's rendering of a probability: one decimal, exponent without
+    padding (MC.out:41-42 "3.7E-9", "9.9E-10")."""
+    m, e = f"{x:.1E}".split("E")
+    return f"{m}E{int(e)}"
+
+
+def tstamp(t: float) -> str:
+    return time.strftime("%Y-%m-%d %H:%M:%S", time.localtime(t))
+
+
+def messages(r, t_start: float, t_end: float, actual_fp_prob: Optional[float] = None,
+             engine: str = "", ngpus: int = 1) -> List[tuple]:
+    """TLC -tool messages (code, class, body) for one check's result, in the
+    order of the reference run (MC.out:1-1108).  SANY's (2220/2219) and the
+    expression-level coverage (2221) are not produced: there is no TLA+ front
+    end here."""
+    out = []
+    add = lambda code, text, cls=0: out.append((code, cls, text))  # noqa: E731
+    add(2262, f"kubecheck (TLC-compatible counts) {engine}".rstrip())
+    add(2187, f"Running breadth-first search Model-Checking with {ngpus} MI355X GPU(s) "
+              f"(kubecheck ClaimSet FPSet, HBM StateQueue).")
+    add(2185, f"Starting... ({tstamp(t_start)})")
+    add(2189, "Computing initial states...")
+    add(2190, f"Finished computing initial states: {r.init} distinct states generated at {tstamp(t_start)}.")
+    d, g = r.distinct, r.generated
+    minutes = max(t_end - t_start, 1e-9) / 60.0
+    if r.error is None:
+        body = ("Model checking completed. No error has been found.\n"
+                "  Estimates of the probability that TLC did not check all reachable states\n"
+                "  because two distinct states had the same fingerprint:\n"
+                f"  calculated (optimistic):  val = {java_e(d * (g - d) / 2**64)}")
+        if actual_fp_prob is not None:
+            body += f"\n  based on the actual fingerprints:  val = {java_e(actual_fp_prob)}"
+        add(2193, body)
+    else:
+        if r.error == "invariant":
+            add(2110, f"Invariant {r.error_invariant} is violated.", 1)
+        elif r.error == "assertion":
+            add(2132, f"The first argument of Assert evaluated to FALSE (action {r.error_action}).", 1)
+        else:
+            add(2114, "Deadlock reached.", 1)
+        add(2121, "The behavior up to this point is:", 1)
+        blocks = re.split(r"^State (\d+):$", r.trace_text, flags=re.M)[1:]
+        for num, body in zip(blocks[0::2], blocks[1::2]):
+            add(2217, f"{num}: {body.strip()}", 4)
+    add(2201, f"The coverage statistics at {tstamp(t_end)}")
+    add(2773, f"{span_text('Init', INIT_SPAN)}: {r.init}:{r.init}")
+    for name, span in ACTION_SPANS.items():
+        add(2772, f"{span_text(name, span)}: {r.act_dist[name]}:{r.act_gen[name]}")
+    add(2202, "End of statistics.")
+    add(2200, f"Progress({r.depth}) at {tstamp(t_end)}: {g:,} states generated ({int(g / minutes):,} s/min), "
+              f"{d:,} distinct states found ({int(d / minutes):,} ds/min), {r.queue_left:,} states left on queue.")
+    add(2199, f"{g} states generated, {d} distinct states found, {r.queue_left} states left on queue.")
+    add(2194, f"The depth of the complete state graph search is {r.depth}.")
+    st = outdegree_stats(getattr(r, "outdeg_hist", []) or [])
+    if st:
+        add(2268, f"The average outdegree of the complete state graph is {st[0]} (minimum is {st[1]}, "
+                  f"the maximum {st[2]} and the 95th percentile is {st[3]}).")
+    add(2186, f"Finished in {int(round((t_end - t_start) * 1000))}ms at ({tstamp(t_end)})")
+    return out
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -123,6 +230,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("-ns", type=int, default=1)
     ap.add_argument("-variant", type=int, default=0)
     ap.add_argument("-device", type=int, default=0)
+    ap.add_argument("-nocheckfps", action="store_true",
+                    help="skip the 'based on the actual fingerprints' estimate (a sort of the seen-set)")
     a = ap.parse_args(argv)
 
     cfg_path = a.config or f"{a.spec}.cfg"
@@ -135,45 +244,17 @@ def main(argv: Optional[List[str]] = None) -> int:
 
     import kubecheck
 
-    out = lambda code, text, cls=0: print(msg(code, text, cls, a.tool), flush=True)  # noqa: E731
-    out(2262, f"kubecheck (TLC-compatible counts) {kubecheck.load().kc_build_info().decode()}")
     mc_cfg = kubecheck.ModelConfig(nc=a.nc, np=a.np, ns=a.ns, variant=a.variant, device=a.device,
                                    check_deadlock=not a.deadlock, **kw)
-    out(2187, f"Running breadth-first search Model-Checking on {kubecheck.device_count()} "
-              f"MI355X GPU(s) (HBM FPSet, HBM StateQueue) for {mc_cfg.name}.")
-    out(2185, f"Starting... ({time.strftime('%Y-%m-%d %H:%M:%S')})")
-    out(2189, "Computing initial states...")
+    t0 = time.time()
     with kubecheck.ModelChecker(mc_cfg) as mc:
         r = mc.run()
-    out(2190, f"Finished computing initial states: {r.init} distinct states generated.")
-    rc = 0
-    if r.error is None:
-        d, g = r.distinct, r.generated
-        out(2193, "Model checking completed. No error has been found.\n"
-                  "  Estimates of the probability that TLC did not check all reachable states\n"
-                  "  because two distinct states had the same fingerprint:\n"
-                  f"  calculated (optimistic):  val = {d * (g - d) / 2**64:.1E}")
-    else:
-        rc = 12
-        if r.error == "invariant":
-            out(2110, f"Invariant {r.error_invariant} is violated.", 1)
-        elif r.error == "assertion":
-            out(2132, f"The first argument of Assert evaluated to FALSE (action {r.error_action}).", 1)
-        else:
-            out(2114, "Deadlock reached.", 1)
-        out(2121, "The behavior up to this point is:", 1)
-        blocks = re.split(r"^State (\d+):$", r.trace_text, flags=re.M)[1:]
-        for num, body in zip(blocks[0::2], blocks[1::2]):
-            out(2217, f"{num}: {body.strip()}", 4)
-    out(2201, "The coverage statistics:")
-    for name in kubecheck.ACTIONS:
-        out(2772, f"<{name}>: {r.act_dist[name]}:{r.act_gen[name]}")
-    out(2202, "End of statistics.")
-    out(2199, f"{r.generated} states generated, {r.distinct} distinct states found, "
-              f"{r.queue_left} states left on queue.")
-    out(2194, f"The depth of the complete state graph search is {r.depth}.")
-    out(2186, f"Finished in {int(r.seconds * 1000)}ms at ({time.strftime('%Y-%m-%d %H:%M:%S')})")
-    return rc
+        prob = None if (a.nocheckfps or r.error is not None) else mc.check_fps()[1]
+    t1 = t0 + r.seconds
+    for code, cls, body in messages(r, t0, t1, prob, kubecheck.load().kc_build_info().decode(),
+                                    kubecheck.device_count()):
+        print(msg(code, body, cls, a.tool), flush=True)
+    return 0 if r.error is None else 12
 
 
 if __name__ == "__main__":

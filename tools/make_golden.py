@@ -82,16 +82,21 @@ def parse_mcout(path: str) -> dict:
     out["init"] = int(re.search(r"(\d+) distinct states generated", l).group(1))
     out["line_init"] = i
     out["no_error"] = "No error has been found" in text
-    act_gen, act_dist, act_line = {}, {}, {}
+    act_gen, act_dist, act_line, act_span = {}, {}, {}, {}
     for i, l in enumerate(lines, 1):
-        m = re.match(r"<(\w+) line \d+, col \d+ to line \d+, col \d+ of module KubeAPI>: (\d+):(\d+)", l)
-        if m and m.group(1) == "Init":               # msg 2773, Init's own line
-            out["init_coverage"] = {"distinct": int(m.group(2)), "generated": int(m.group(3)),
-                                    "mcout_line": i}
-        elif m:
-            act_dist[m.group(1)] = int(m.group(2))   # worker-order dependent
-            act_gen[m.group(1)] = int(m.group(3))
+        m = re.match(r"<(\w+) line (\d+), col (\d+) to line (\d+), col (\d+) of module KubeAPI>: (\d+):(\d+)", l)
+        if not m:
+            continue
+        span = [int(m.group(k)) for k in range(2, 6)]
+        if m.group(1) == "Init":                     # msg 2773, Init's own line
+            out["init_coverage"] = {"distinct": int(m.group(6)), "generated": int(m.group(7)),
+                                    "mcout_line": i, "span": span}
+        else:
+            act_dist[m.group(1)] = int(m.group(6))   # worker-order dependent
+            act_gen[m.group(1)] = int(m.group(7))
             act_line[m.group(1)] = i
+            act_span[m.group(1)] = span              # msg 2772's location of the action
+    out["act_span"] = act_span
     out["act_gen"] = act_gen
     out["act_dist_tlc_4workers"] = act_dist
     out["act_line"] = act_line
@@ -108,6 +113,14 @@ def parse_mcout(path: str) -> dict:
     out["spans"] = spans
     m = re.search(r"calculated \(optimistic\):\s+val = ([\dE.-]+)", text)
     out["collision_optimistic"] = float(m.group(1))
+    # message bodies a TLC -tool parser reads (code -> body text), for the
+    # CLI's message-format test; 2200/2268 values are run dependent
+    bodies = {}
+    for m in re.finditer(r"@!@!@STARTMSG (\d+):\d+ @!@!@\n(.*?)\n@!@!@ENDMSG \1 @!@!@", text, flags=re.S):
+        code = int(m.group(1))
+        if code in (2190, 2193, 2199, 2194, 2268, 2200, 2201, 2202, 2186, 2185, 2189):
+            bodies.setdefault(str(code), m.group(2))
+    out["message_bodies"] = bodies
     return out
 
 
@@ -119,9 +132,13 @@ def oracle_fixtures(with_np2: bool) -> dict:
     fx: dict = {"generator": "tools/make_golden.py (oracle/kubeapi_oracle.c)"}
 
     def summary(r):
-        return {k: r[k] for k in ("init", "generated", "distinct", "depth", "complete", "act_gen",
-                                  "act_dist", "level_width", "err_kind", "err_action", "err_self",
-                                  "err_level", "trace_len")}
+        out = {k: r[k] for k in ("init", "generated", "distinct", "depth", "complete", "act_gen",
+                                 "act_dist", "level_width", "err_kind", "err_action", "err_self",
+                                 "err_level", "trace_len")}
+        # new states first reached per expanded state (TLC outdegree), 16 bins, last = 15+
+        h = r["newdeg_hist"]
+        out["outdeg_hist"] = h[:15] + [sum(h[15:])]
+        return out
 
     fx["model1"] = summary(O.run(O.config()))
     for f, t in [(0, 0), (0, 1), (1, 0)]:
