@@ -190,11 +190,26 @@ def cpu_baseline(kw, seconds):
     cfg.fpset_log2 = 22 if (kw["nc"], kw["np"], kw["ns"]) == (1, 1, 1) else 29
     r = pyoracle.bench_parallel(cfg, threads, seconds)
     what = "the whole model" if r["complete"] else f"{r['levels']} BFS levels from Init"
-    return {"value": round(r["rate"], 1), "unit": "distinct states/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"oracle/kubeapi_oracle.c ko_bench_parallel: level-synchronous BFS of the same "
-                      f"model on {threads} threads with a lock-free 64-bit fingerprint set, {what} "
-                      f"({r['distinct']} distinct, {r['generated']} generated) in {r['seconds']:.1f} s"}
+    out = {"value": round(r["rate"], 1), "unit": "distinct states/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
+           "sample": f"oracle/kubeapi_oracle.c ko_bench_parallel: level-synchronous BFS of the same "
+                     f"model on {threads} threads with a lock-free 64-bit fingerprint set, {what} "
+                     f"({r['distinct']} distinct, {r['generated']} generated) in {r['seconds']:.1f} s"}
+    # the same comparator over the WHOLE model, run once on a GPU box's host
+    # (tools/gpu_prof_r02.sh ... cpu): too long for every bench run
+    if (kw["nc"], kw["np"], kw["ns"]) == (1, 2, 1):
+        import glob
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_cpu_np2_full.json")))[-1:]:
+            try:
+                with open(f) as fh:
+                    full = json.load(fh)
+                out["full_model_run"] = {"seconds": full["seconds"], "threads": full["threads"],
+                                         "distinct": full["distinct"], "generated": full["generated"],
+                                         "distinct_per_s": full["distinct_per_s"],
+                                         "source": os.path.relpath(f, ROOT)}
+            except (OSError, ValueError, KeyError):
+                pass
+    return out
 
 
 def bench_single(args, kw, desc):
