@@ -51,6 +51,8 @@ def parse():
                     help="HIP events on every kernel (default: on the roofline kernel k_claim only;"
                          " events on all five per-level launches cost the NP=2 check ~6 ms)")
     ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
+    ap.add_argument("--frontier-hbm-mb", type=int, default=0,
+                    help="frontier spill mode: keep the frontiers in a StateQueue with this HBM budget")
     ap.add_argument("--fp-count", type=float, default=1e10,
                     help="fpset workload: fingerprints inserted (and looked up) per step")
     ap.add_argument("--fp-load", type=float, default=0.5, choices=[0.5, 0.75],
@@ -218,7 +220,8 @@ def bench_single(args, kw, desc):
 
     cfg = kubecheck.ModelConfig(**kw, keep_trace=True,
                                 timing=0 if args.no_timing else (1 if args.all_kernel_timing else 2),
-                                fpset_slots=1 << 20, chunk_states=args.chunk)
+                                fpset_slots=1 << 20, chunk_states=args.chunk,
+                                frontier_hbm_bytes=args.frontier_hbm_mb << 20)
     mc = kubecheck.ModelChecker(cfg)
     for _ in range(args.warmup):
         mc.run()
@@ -261,7 +264,9 @@ def bench_single(args, kw, desc):
                    "constants": "REQUESTS_CAN_FAIL=TRUE,REQUESTS_CAN_TIMEOUT=TRUE",
                    "invariants": "TypeOK,OnlyOneVersion", "distinct": r.distinct,
                    "generated": r.generated, "depth": r.depth, "parallelism": "1 GPU",
-                   "path": "single-GPU engine (kc_engine_run)", "golden_check": golden,
+                   "path": "single-GPU engine (kc_engine_run)" + (
+                       f", frontiers in the StateQueue with a {args.frontier_hbm_mb} MiB HBM budget"
+                       if args.frontier_hbm_mb else ""), "golden_check": golden,
                    "claimset_probes": r.fpset_probes, "settle_reads": r.batch_inserts,
                    "chunks": r.levels_chunks},
     }

@@ -128,12 +128,52 @@ uint64_t kc_stress_fp(uint64_t seed, int kind, uint64_t n_ins, uint64_t i);
 
 /* ----------------------------------------------------------- StateQueue */
 typedef struct kc_squeue kc_squeue;
-/* FIFO of fixed-width packed states (words per state = `state_words`). */
+/* FIFO of fixed-width packed states (words per state = `state_words`) in
+ * segments over three tiers: HBM, pinned host RAM beyond `hbm_bytes`, and
+ * spill files in `spill_dir` beyond `host_bytes` (DiskStateQueue's role).
+ * The tail segment is always in HBM; a spilled segment comes back to HBM
+ * when a reader reaches it.  The segments being read (front runs handed
+ * out since the last pop) and written stay resident whatever the budget.
+ * Every call takes a HIP stream (NULL = the queue's own blocking stream);
+ * drive one queue from one stream: copies and kernels are then ordered
+ * without events. */
+typedef struct {
+  int state_words;
+  int device;
+  uint64_t segment_states;  /* states per segment (0 = 2^20) */
+  uint64_t hbm_bytes;       /* HBM budget of the segments (0 = unlimited) */
+  uint64_t host_bytes;      /* pinned host RAM budget (0 = unlimited) */
+  const char *spill_dir;    /* disk tier (NULL = none: past both budgets -ENOMEM) */
+} kc_squeue_config;
+typedef struct {
+  uint64_t size, segments, seg_hbm, seg_host, seg_disk;
+  uint64_t hbm_bytes, host_bytes, disk_bytes;      /* now */
+  uint64_t spilled_host_bytes, spilled_disk_bytes, reloaded_bytes, peak_hbm_bytes;  /* cumulative */
+} kc_squeue_stats;
+int kc_squeue_create2(const kc_squeue_config *cfg, kc_squeue **out);
+/* one HBM tier of `capacity_states`-state segments, no budget (round-1 API) */
 int kc_squeue_create(int state_words, uint64_t capacity_states, int device, kc_squeue **out);
 void kc_squeue_destroy(kc_squeue *q);
+/* host buffers (synchronous) */
 int kc_squeue_enqueue(kc_squeue *q, const uint64_t *states, size_t n);
 /* dequeue up to `max_n` states into `out`; *n_out = number dequeued */
 int kc_squeue_dequeue(kc_squeue *q, uint64_t *out, size_t max_n, size_t *n_out);
+/* device buffers, stream-ordered (TLC's sEnqueue / sDequeue(n) batches) */
+int kc_squeue_enqueue_dev(kc_squeue *q, const uint64_t *dev_states, size_t n, void *hip_stream);
+int kc_squeue_dequeue_dev(kc_squeue *q, uint64_t *dev_out, size_t max_n, size_t *n_out, void *hip_stream);
+/* In place: a device run of n states at the tail for a kernel to write,
+ * valid until the next call; commit(k <= n) appends its first k states. */
+int kc_squeue_reserve_dev(kc_squeue *q, size_t n, uint64_t **dev_ptr, void *hip_stream);
+int kc_squeue_commit(kc_squeue *q, size_t n, void *hip_stream);
+/* In place: a contiguous device run of up to max_n states starting `offset`
+ * states after the head (*n_out may be smaller, at a segment end), valid
+ * until it is popped; pop(n) drops n states from the head. */
+int kc_squeue_front_dev(kc_squeue *q, size_t offset, size_t max_n, const uint64_t **dev_ptr,
+                        size_t *n_out, void *hip_stream);
+int kc_squeue_pop(kc_squeue *q, size_t n, void *hip_stream);
+/* host copy of states [offset, offset + n) after the head, from any tier */
+int kc_squeue_peek(kc_squeue *q, size_t offset, size_t n, uint64_t *host_out, void *hip_stream);
+int kc_squeue_get_stats(kc_squeue *q, kc_squeue_stats *out);
 uint64_t kc_squeue_size(const kc_squeue *q);
 
 /* -------------------------------------------------------------- Engine */
@@ -156,6 +196,18 @@ typedef struct {
                               2 = only k_claim (the roofline kernel) */
   int invariants;          /* MC.cfg INVARIANT list: bit 0 TypeOK, bit 1
                               OnlyOneVersion (default 3; 0 = check none) */
+  /* Frontier spill (single-GPU engine).  frontier_hbm_bytes > 0 keeps the
+   * frontiers in a kc_squeue with that HBM budget: levels run in chunks of
+   * <= frontier_segment_states parents, read from the queue's head and
+   * written into its tail; segments past the budget go to pinned host RAM
+   * (up to frontier_host_bytes, 0 = unlimited), then to files in spill_dir.
+   * trace_host = 1 keeps the trace file (parent index + ordinal, 9 B per
+   * state) in pinned host RAM instead of HBM. */
+  uint64_t frontier_hbm_bytes;
+  uint64_t frontier_host_bytes;
+  uint64_t frontier_segment_states;   /* 0 = 2^22 */
+  const char *spill_dir;
+  int trace_host;
 } kc_model_config;
 
 typedef struct {
@@ -182,6 +234,9 @@ typedef struct {
   uint64_t outdeg_hist[16]; /* TLC outdegree (msg 2268): expanded states by the number of
                               new states first reached from them; [15] = 15 or more
                               (single-GPU engine; zero in the sharded path) */
+  uint64_t frontier_spilled_bytes;   /* frontier bytes written to host RAM or disk */
+  uint64_t frontier_reloaded_bytes;  /* ... and read back into HBM */
+  uint64_t frontier_peak_hbm_bytes;  /* peak HBM held by the frontier queue */
 } kc_result;
 
 typedef struct kc_engine kc_engine;

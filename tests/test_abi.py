@@ -66,3 +66,26 @@ def test_spec_words():
     assert kubecheck.Spec(kubecheck.ModelConfig()).state_words == 4        # 32 B per Model_1 state
     assert kubecheck.Spec(kubecheck.ModelConfig(np=2)).state_words == 6    # 48 B for NP=2
     assert kubecheck.Spec(kubecheck.ModelConfig()).tuple_words == 1 + 19 * 3
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of the C structs have the header's sizes and field
+    offsets (compiled with the host C compiler against include/kubecheck.h)."""
+    structs = {"kc_model_config": _lib.KcModelConfig, "kc_result": _lib.KcResult,
+               "kc_squeue_config": _lib.KcSqueueConfig, "kc_squeue_stats": _lib.KcSqueueStats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "kubecheck.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'  printf("{cname}.{f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                         check=True).stdout.split("\n") if l)
+    for cname, py in structs.items():
+        assert int(got[cname]) == C.sizeof(py), cname
+        for f in py._fields_:
+            assert int(got[f"{cname}.{f[0]}"]) == getattr(py, f[0]).offset, (cname, f[0])

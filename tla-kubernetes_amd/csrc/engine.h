@@ -20,7 +20,10 @@ constexpr int KK_ALL = KA_TOTAL + 1;
 
 class EngineBase {
  public:
-  explicit EngineBase(const kc_model_config& cfg) : cfg_(cfg) {}
+  // the config is kept by value; its one string is copied too
+  explicit EngineBase(const kc_model_config& cfg) : cfg_(cfg), spill_dir_(cfg.spill_dir ? cfg.spill_dir : "") {
+    cfg_.spill_dir = cfg.spill_dir ? spill_dir_.c_str() : nullptr;
+  }
   virtual ~EngineBase() = default;
   virtual int setup() = 0;
   virtual int run(kc_result* res) = 0;
@@ -46,6 +49,7 @@ class EngineBase {
 
  protected:
   kc_model_config cfg_;
+  std::string spill_dir_;
   int capture_level_ = 0;
   int timing_ = 0;   // 1: HIP events on every kernel; 2: on k_claim only
   double ktime_ms_[KK_ALL] = {};

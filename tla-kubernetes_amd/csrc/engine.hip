@@ -26,6 +26,7 @@
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
+#include "squeue.h"
 
 namespace kc {
 
@@ -101,6 +102,9 @@ class EngineT final : public EngineBase {
     // KC_NARROW=0
     const char* nw = getenv("KC_NARROW");
     narrow_on_ = cfg.chunk_states == 0 && !(nw && nw[0] == '0') && !ablate_;
+    // frontiers in the StateQueue (spill mode): the chunked wide path only
+    queued_ = cfg.frontier_hbm_bytes > 0;
+    if (queued_) narrow_on_ = false;
   }
   ~EngineT() override { release(); }
 
@@ -165,8 +169,7 @@ class EngineT final : public EngineBase {
       KC_TRY(cs_.init(fp_slots, st_));
     }
     KC_TRY(grow_buffer(cur_, cur_cap_, (uint64_t)ni, false, st_));
-    KC_TRY(grow_buffer(parent_, par_cap_, (uint64_t)ni + cand, false, st_));
-    KC_TRY(grow_buffer(ord_, ord_cap_, (uint64_t)ni + cand, false, st_));
+    KC_TRY(grow_trace((uint64_t)ni + cand, false));
     KC_HIP_TRY(hipMemcpyAsync(cur_, init.data(), ni * sizeof(State), hipMemcpyHostToDevice, st_));
     uint64_t* d_fps = nullptr;
     int* d_res = nullptr;
@@ -179,8 +182,14 @@ class EngineT final : public EngineBase {
     std::vector<unsigned long long> ipar(ni, ~0ull);
     std::vector<uint8_t> iord(ni);
     for (int k = 0; k < ni; ++k) iord[k] = (uint8_t)k;
-    KC_HIP_TRY(hipMemcpyAsync(parent_, ipar.data(), ni * 8, hipMemcpyHostToDevice, st_));
-    KC_HIP_TRY(hipMemcpyAsync(ord_, iord.data(), ni, hipMemcpyHostToDevice, st_));
+    if (cfg_.trace_host) {
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      memcpy(parent_, ipar.data(), ni * 8);
+      memcpy(ord_, iord.data(), ni);
+    } else {
+      KC_HIP_TRY(hipMemcpyAsync(parent_, ipar.data(), ni * 8, hipMemcpyHostToDevice, st_));
+      KC_HIP_TRY(hipMemcpyAsync(ord_, iord.data(), ni, hipMemcpyHostToDevice, st_));
+    }
     KC_HIP_TRY(hipStreamSynchronize(st_));
     (void)hipFree(d_fps);
     (void)hipFree(d_res);
@@ -214,6 +223,8 @@ class EngineT final : public EngineBase {
         return 0;
       }
     }
+
+    if (queued_) return run_queued(res, t0, n, cand, init);
 
     // default: one chunk per level; chunk_states bounds the per-chunk
     // buffers.  Claims are level-global (keys grow with the parent index),
@@ -264,10 +275,7 @@ class EngineT final : public EngineBase {
       // previous level)
       KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
       const uint64_t next_gidx = level_gidx + n;
-      if (cfg_.keep_trace) {
-        KC_TRY(grow_buffer(parent_, par_cap_, next_gidx + cand + 1, true, st_));
-        KC_TRY(grow_buffer(ord_, ord_cap_, next_gidx + cand + 1, true, st_));
-      }
+      if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + cand + 1, true));
       KC_TRY(cs_.reserve(cand, st_));
       {
         const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
@@ -323,7 +331,7 @@ class EngineT final : public EngineBase {
         KC_HIP_TRY(scan_err);
         timed(KK_EMIT, [&] {
           hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
-                             flags_, newmask_, offsets_, next_, level_gidx, next_gidx, parent_, ord_,
+                             flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
                              cfg_.keep_trace, d_ctr_);
         });
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_);
@@ -491,7 +499,10 @@ class EngineT final : public EngineBase {
     ev_used_ = 0;
   }
 
-  int report_error(kc_result* res, uint64_t key, int level, uint64_t level_gidx, uint64_t n) {
+  // parent_host: the parent state when the caller already holds it (the
+  // queued path); otherwise it is read from the frontier (cur_)
+  int report_error(kc_result* res, uint64_t key, int level, uint64_t level_gidx, uint64_t n,
+                   const State* parent_host = nullptr) {
     const int kind = (int)(key & 0xff);
     const int pos = (int)((key >> 8) & 0xff);
     const uint64_t pidx = key >> 16;
@@ -505,6 +516,8 @@ class EngineT final : public EngineBase {
     std::vector<State> path;
     if (cfg_.keep_trace) {
       KC_TRY(path_to(level_gidx + pidx, path));
+    } else if (parent_host) {
+      path.assign(1, *parent_host);
     } else {
       path.resize(1);
       KC_HIP_TRY(hipMemcpy(&path[0], cur_ + pidx, sizeof(State), hipMemcpyDeviceToHost));
@@ -546,8 +559,14 @@ class EngineT final : public EngineBase {
     for (;;) {
       unsigned long long p = 0;
       uint8_t o = 0;
-      KC_HIP_TRY(hipMemcpy(&p, parent_ + g, 8, hipMemcpyDeviceToHost));
-      KC_HIP_TRY(hipMemcpy(&o, ord_ + g, 1, hipMemcpyDeviceToHost));
+      if (cfg_.trace_host) {
+        KC_HIP_TRY(hipStreamSynchronize(st_));
+        p = parent_[g];
+        o = ord_[g];
+      } else {
+        KC_HIP_TRY(hipMemcpy(&p, parent_ + g, 8, hipMemcpyDeviceToHost));
+        KC_HIP_TRY(hipMemcpy(&o, ord_ + g, 1, hipMemcpyDeviceToHost));
+      }
       chain.push_back({g, o});
       if (p == ~0ull) break;
       g = p;
@@ -591,16 +610,31 @@ class EngineT final : public EngineBase {
     res->fpset_probes = h_ctr_->probes() + narrow_probes_;
     for (int b = 0; b < OUTDEG_BINS; ++b) res->outdeg_hist[b] = h_ctr_->outdeg(b);
     res->batch_inserts = h_ctr_->settles();
+    if (q_) {
+      kc_squeue_stats qs;
+      q_->stats(&qs);
+      res->frontier_spilled_bytes = qs.spilled_host_bytes + qs.spilled_disk_bytes;
+      res->frontier_reloaded_bytes = qs.reloaded_bytes;
+      res->frontier_peak_hbm_bytes = qs.peak_hbm_bytes;
+    }
     res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
   void release() {
     (void)hipSetDevice(cfg_.device);
     cs_.release();
+    q_.reset();
+    if (cfg_.trace_host) {
+      if (parent_) (void)hipHostFree(parent_);
+      if (ord_) (void)hipHostFree(ord_);
+      parent_ = nullptr;
+      ord_ = nullptr;
+    }
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
                     (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (h_last_) (void)hipHostFree(h_last_);
     if (d_ns_) (void)hipFree(d_ns_);
     if (d_nsc_) (void)hipFree(d_nsc_);
     if (h_ns_) (void)hipHostFree(h_ns_);
@@ -621,10 +655,7 @@ class EngineT final : public EngineBase {
     KC_TRY(grow_buffer(cur_, cur_cap_, bufs, true, st_));
     KC_TRY(grow_buffer(next_, next_cap_, bufs, false, st_));
     const uint64_t need_par = level_gidx + n + std::max(cand, kNew) + 1;
-    if (cfg_.keep_trace) {
-      KC_TRY(grow_buffer(parent_, par_cap_, need_par, true, st_));
-      KC_TRY(grow_buffer(ord_, ord_cap_, need_par, true, st_));
-    }
+    if (cfg_.keep_trace) KC_TRY(grow_trace(need_par, true));
     KC_TRY(cs_.reserve(std::max(cand, kNew), st_));
     NarrowCtl& h = *h_ns_;
     memset(&h, 0, offsetof(NarrowCtl, widths));
@@ -696,7 +727,205 @@ class EngineT final : public EngineBase {
     return 0;
   }
 
+  // the trace file (parent index + ordinal per state) in HBM, or in pinned
+  // host RAM with cfg.trace_host (kernels store into it directly)
+  int grow_trace(uint64_t need, bool keep) {
+    if (cfg_.trace_host) {
+      KC_TRY(grow_host_buffer(parent_, par_cap_, need, st_));
+      return grow_host_buffer(ord_, ord_cap_, need, st_);
+    }
+    KC_TRY(grow_buffer(parent_, par_cap_, need, keep, st_));
+    return grow_buffer(ord_, ord_cap_, need, keep, st_);
+  }
+
+  // ---- frontiers in the StateQueue (cfg.frontier_hbm_bytes > 0; squeue.h).
+  // The queue holds level L's states followed by level L+1's as they are
+  // made.  Each chunk of <= one segment of parents is read in place from the
+  // head (front), expanded by the same kernels as the in-HBM path, and its
+  // new states go straight into a run reserved at the tail; segments past
+  // the HBM budget spill to host RAM / disk and come back when the head
+  // reaches them.  A chunk's parents are popped one chunk later, after the
+  // sync that would report an error found among them.  One host sync per
+  // chunk: its new-state count sizes the reservation.  Same kernels, same
+  // order keys: results equal the in-HBM path's.
+  int run_queued(kc_result* res, std::chrono::steady_clock::time_point t0, uint64_t n, uint64_t cand,
+                 const std::vector<State>& init) {
+    if (!q_) {
+      SegQueue::Config qc;
+      qc.words = M::W;
+      qc.device = cfg_.device;
+      qc.seg_states = cfg_.frontier_segment_states ? cfg_.frontier_segment_states : (1ull << 22);
+      qc.hbm_bytes = cfg_.frontier_hbm_bytes;
+      qc.host_bytes = cfg_.frontier_host_bytes;
+      qc.dir = cfg_.spill_dir ? cfg_.spill_dir : "";
+      q_.reset(new SegQueue());
+      KC_TRY(q_->init(qc));
+    }
+    if (!h_last_) KC_HIP_TRY(hipHostMalloc(&h_last_, 16));
+    KC_TRY(q_->clear(st_));
+    KC_TRY(q_->enqueue_host(reinterpret_cast<const uint64_t*>(init.data()), n, st_));
+    const uint64_t chunk = std::min<uint64_t>(
+        std::min<uint64_t>(cfg_.chunk_states ? cfg_.chunk_states : kMaxChunk, kMaxChunk), q_->seg_states());
+    uint64_t level_gidx = 0, cand_total = 0;
+    int level = 1;
+    State err_parent{};
+    hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
+    while (n > 0) {
+      if (cfg_.max_levels && level >= cfg_.max_levels) break;
+      if (n >= (1ull << 32)) {
+        set_error("kubecheck: level wider than 2^32 states");
+        return -ENOMEM;
+      }
+      const uint64_t next_gidx = level_gidx + n;
+      if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + cand + 1, true));
+      KC_TRY(cs_.reserve(cand, st_));
+      const uint64_t cmax = std::min(n, chunk);
+      {
+        const uint64_t tiles = (cmax + CLAIM_TILE - 1) / CLAIM_TILE;
+        KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
+        KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
+        KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+      }
+      KC_TRY(grow_buffer(newmask_, mask_cap_, cmax, false, st_));
+      KC_TRY(grow_buffer(offsets_, off_cap_, cmax, false, st_));
+      const uint32_t succ_level = (uint32_t)level + 1;
+      uint64_t start = 0, level_new = 0, popped = 0, pend = 0;
+      unsigned long long seen_err = ~0ull;
+      bool have_parent = false;
+      // after a sync: overflow, and a new minimum error key, whose parent
+      // (in this chunk or the one before, neither popped yet) is copied out
+      auto check = [&](uint64_t hi) -> int {
+        const Counters& c = *h_ctr_;
+        if (c.overflow || c.batch_used) {
+          set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
+          return -ENOMEM;
+        }
+        if (c.err_key != seen_err) {
+          seen_err = c.err_key;
+          const uint64_t pidx = seen_err >> 16;
+          if (pidx < popped || pidx >= hi) {
+            set_error("kubecheck: bad error key");
+            return -EIO;
+          }
+          const uint64_t* p = nullptr;
+          uint64_t got = 0;
+          KC_TRY(q_->front(pidx - popped, 1, &p, &got, st_));
+          KC_HIP_TRY(hipMemcpyAsync(&err_parent, p, sizeof(State), hipMemcpyDeviceToHost, st_));
+          KC_HIP_TRY(hipStreamSynchronize(st_));
+          have_parent = true;
+        }
+        return 0;
+      };
+      while (start < n) {
+        const uint64_t* p = nullptr;
+        uint64_t m = 0;
+        KC_TRY(q_->front(start - popped, std::min(chunk, n - start), &p, &m, st_));
+        if (m == 0) {
+          set_error("kubecheck: StateQueue holds fewer states than the level");
+          return -EIO;
+        }
+        const State* cur = reinterpret_cast<const State*>(p);
+        ++res->levels_chunks;
+        const unsigned tiles = (unsigned)((m + CLAIM_TILE - 1) / CLAIM_TILE);
+        timed(KK_EXPAND, [&] {
+          hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur, m, start, flags_,
+                             cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level, abl_mask_, rcount_, rec_fp_,
+                             rec_lk_, newmask_, d_ctr_, ShardArgs{});
+        });
+        timed(KK_RESOLVE, [&] {
+          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+          hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+        });
+        size_t tmp_bytes = 0;
+        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)m, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        hipError_t scan_err = hipSuccess;
+        timed(KK_SCAN, [&] {
+          scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)m, st_);
+        });
+        KC_HIP_TRY(scan_err);
+        KC_HIP_TRY(hipMemcpyAsync(h_last_, offsets_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
+        KC_HIP_TRY(hipMemcpyAsync(h_last_ + 1, newmask_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
+        KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+        KC_HIP_TRY(hipStreamSynchronize(st_));
+        collect_times();
+        KC_TRY(check(start + m));
+        const uint64_t nn = (uint64_t)h_last_[0] + NewCount()(h_last_[1]);
+        uint64_t* dst = nullptr;
+        if (nn) KC_TRY(q_->reserve(nn, &dst, st_));
+        timed(KK_EMIT, [&] {
+          hipLaunchKernelGGL(k_emit<M>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st_, cur, m, start,
+                             flags_, newmask_, offsets_, reinterpret_cast<State*>(dst), level_new, level_gidx,
+                             next_gidx, parent_, ord_, cfg_.keep_trace, d_ctr_);
+        });
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_);
+        KC_HIP_TRY(hipGetLastError());
+        if (nn) KC_TRY(q_->commit(nn, st_));
+        level_new += nn;
+        if (pend) KC_TRY(q_->pop(pend, st_));
+        popped += pend;
+        pend = m;
+        start += m;
+      }
+      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      collect_times();
+      KC_TRY(check(n));
+      if (h_ctr_->chunk_base != level_new) {
+        set_error("kubecheck: StateQueue level count %llu != %llu", (unsigned long long)level_new,
+                  (unsigned long long)h_ctr_->chunk_base);
+        return -EIO;
+      }
+      const uint64_t cand_now = h_ctr_->cand_total;
+      hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);   // next level's head
+      cs_.count += level_new;
+      res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
+      if (seen_err != ~0ull) {
+        KC_TRY(report_error(res, seen_err, level, level_gidx, n, have_parent ? &err_parent : nullptr));
+        res->distinct += level_new;
+        finish(res, t0, 0);
+        return 0;
+      }
+      if (pend) KC_TRY(q_->pop(pend, st_));
+      res->distinct += level_new;
+      if (cfg_.verbose) {
+        kc_squeue_stats qs;
+        q_->stats(&qs);
+        fprintf(stderr, "kubecheck: level %d width %llu -> %llu new, %llu distinct; queue %llu HBM / %llu host / %llu disk segments\n",
+                level, (unsigned long long)n, (unsigned long long)level_new, (unsigned long long)res->distinct,
+                (unsigned long long)qs.seg_hbm, (unsigned long long)qs.seg_host, (unsigned long long)qs.seg_disk);
+      }
+      if (capture_level_ == level + 1 && level_new) {
+        captured_.resize(level_new);
+        KC_TRY(q_->peek_host(0, level_new, reinterpret_cast<uint64_t*>(captured_.data()), st_));
+      }
+      level_gidx = next_gidx;
+      n = level_new;
+      cand = cand_now - cand_total;
+      cand_total = cand_now;
+      ++level;
+      if (n) {
+        if (level > KC_MAX_LEVELS) {
+          set_error("kubecheck: more than %d levels", KC_MAX_LEVELS);
+          return -ENOMEM;
+        }
+        res->level_width[level - 1] = n;
+        res->nlevels = level;
+      }
+    }
+    last_level_ = res->nlevels;
+    last_n_ = n;
+    finish(res, t0, n);
+    return 0;
+  }
+
   Flags flags_{};
+  bool queued_ = false;
+  std::unique_ptr<SegQueue> q_;
+  uint32_t* h_last_ = nullptr;       // pinned: a chunk's last offset and mask
   hipStream_t st_ = nullptr;
   NarrowCtl *d_ns_ = nullptr, *h_ns_ = nullptr;
   NarrowScratch* d_nsc_ = nullptr;

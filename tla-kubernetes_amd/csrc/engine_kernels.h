@@ -431,7 +431,7 @@ template <class M>
 __global__ void __launch_bounds__(256)
 k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
        const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
-       typename M::State* __restrict__ next, uint64_t level_gidx, uint64_t next_gidx,
+       typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
        unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
        Counters* __restrict__ C) {
   __shared__ unsigned int sh_act[A_COUNT];
@@ -489,7 +489,7 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
     typename M::State x;
     M::apply(s, slot, j, f, x);
     const uint64_t o = C->chunk_base + obase + (uint64_t)g;
-    store_state<M>(next, o, x);
+    store_state<M>(next, o - next_base, x);   // next_base: the StateQueue run starts at o = next_base
     if (keep_trace) {
       parent[next_gidx + o] = level_gidx + pidx;
       ord[next_gidx + o] = (uint8_t)t;

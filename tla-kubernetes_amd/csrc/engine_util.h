@@ -28,6 +28,25 @@ int grow_buffer(T*& p, uint64_t& cap, uint64_t need, bool keep, hipStream_t st) 
   return 0;
 }
 
+// The same for pinned host memory that kernels write directly (the trace
+// file with kc_model_config.trace_host); contents always kept.
+template <class T>
+int grow_host_buffer(T*& p, uint64_t& cap, uint64_t need, hipStream_t st) {
+  if (need <= cap) return 0;
+  uint64_t nc = cap ? cap : 1024;
+  while (nc < need) nc *= 2;
+  T* np = nullptr;
+  KC_HIP_TRY(hipHostMalloc(&np, nc * sizeof(T)));
+  KC_HIP_TRY(hipStreamSynchronize(st));          // kernels may still write the old buffer
+  if (p) {
+    memcpy(np, p, cap * sizeof(T));
+    KC_HIP_TRY(hipHostFree(p));
+  }
+  p = np;
+  cap = nc;
+  return 0;
+}
+
 // Run-time switches of a model config (constants, seeded variant,
 // invariants to check: 0 = none, as TLC with no INVARIANT in the .cfg).
 inline Flags flags_of(const kc_model_config& c) {

@@ -288,6 +288,7 @@ class ShardT final : public ShardBase {
   ShardT(const kc_model_config& cfg, int rank, int world)
       : cfg_(cfg), rank_(rank), world_(world) {
     flags_ = flags_of(cfg);
+    cfg_.spill_dir = nullptr;      // (the engine's frontier spill; the caller's string is not kept)
   }
   ~ShardT() override { release(); }
 

@@ -262,6 +262,7 @@ class Group {
   Group(std::vector<ShardBase*> local, std::unique_ptr<Comm> comm, const kc_model_config& cfg)
       : local_(std::move(local)), comm_(std::move(comm)), cfg_(cfg) {
     world_ = local_[0]->world();
+    cfg_.spill_dir = nullptr;
     for (auto* s : local_) s->set_async_pack(true);
     send_.assign(local_.size(), nullptr);
     recv_.assign(local_.size(), nullptr);

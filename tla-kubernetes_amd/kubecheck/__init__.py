@@ -23,7 +23,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
-from ._lib import (ACTIONS, ERR_KINDS, INVARIANTS, KcModelConfig, KcResult, KubecheckError,
+from ._lib import (ACTIONS, ERR_KINDS, INVARIANTS, KcModelConfig, KcResult, KcSqueueConfig,
+                   KcSqueueStats, KubecheckError,
                    check, load)
 
 __all__ = ["ModelConfig", "ModelChecker", "CheckResult", "FPSet", "StateQueue", "Spec",
@@ -52,11 +53,23 @@ class ModelConfig:
     verbose: int = 0
     timing: int = 0             # HIP-event timing (kernel_times()): 1 every kernel, 2 k_claim only
     invariants: int = 3         # MC.cfg INVARIANT: bit 0 TypeOK, bit 1 OnlyOneVersion (0 = none)
+    # frontier spill (TLC's DiskStateQueue role): > 0 keeps the frontiers in a
+    # StateQueue with this HBM budget; past it segments go to pinned host RAM
+    # (frontier_host_bytes, 0 = unlimited), then to files in spill_dir
+    frontier_hbm_bytes: int = 0
+    frontier_host_bytes: int = 0
+    frontier_segment_states: int = 0   # parents per chunk / states per segment (0 = 2^22)
+    spill_dir: Optional[str] = None
+    trace_host: bool = False    # the trace file (9 B per state) in pinned host RAM
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()
         for f in KcModelConfig._fields_:
+            if f[0] == "spill_dir":
+                continue
             setattr(c, f[0], int(getattr(self, f[0])))
+        # the C string must outlive the engine's use of the config (copied at create)
+        c.spill_dir = self.spill_dir.encode() if self.spill_dir else None
         return c
 
     @property
@@ -89,6 +102,9 @@ class CheckResult:
     batch_inserts: int = 0
     levels_chunks: int = 0
     outdeg_hist: List[int] = field(default_factory=list)
+    frontier_spilled_bytes: int = 0
+    frontier_reloaded_bytes: int = 0
+    frontier_peak_hbm_bytes: int = 0
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -112,7 +128,9 @@ def _result(r: KcResult) -> CheckResult:
         collision_optimistic=r.collision_optimistic, fpset_slots=r.fpset_slots,
         peak_frontier=r.peak_frontier, fpset_probes=r.fpset_probes,
         batch_inserts=r.batch_inserts, levels_chunks=r.levels_chunks,
-        outdeg_hist=[int(x) for x in r.outdeg_hist])
+        outdeg_hist=[int(x) for x in r.outdeg_hist],
+        frontier_spilled_bytes=r.frontier_spilled_bytes, frontier_reloaded_bytes=r.frontier_reloaded_bytes,
+        frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes)
 
 
 class ModelChecker:
@@ -309,13 +327,36 @@ class FPSet:
 
 
 class StateQueue:
-    """tlc2.tool.queue.StateQueue over fixed-width packed states in HBM."""
+    """tlc2.tool.queue.StateQueue (the recorded run's DiskStateQueue,
+    MC.out:5): a FIFO of fixed-width packed states in segments over HBM,
+    pinned host RAM past `hbm_bytes`, and spill files in `spill_dir` past
+    `host_bytes` (include/kubecheck.h kc_squeue_*).  Host-array calls are
+    synchronous; the ``*_dev`` calls take device pointers or CUDA tensors and
+    an optional HIP stream (None = the queue's own stream, ordered with the
+    default stream)."""
 
-    def __init__(self, state_words: int, capacity: int, device: int = 0):
+    def __init__(self, state_words: int, capacity: int = 0, device: int = 0, *, segment_states: int = 0,
+                 hbm_bytes: int = 0, host_bytes: int = 0, spill_dir: Optional[str] = None):
         self._lib = load()
         self.words = state_words
         self._h = C.c_void_p()
-        check("kc_squeue_create", self._lib.kc_squeue_create(state_words, capacity, device, C.byref(self._h)))
+        if capacity and not (segment_states or hbm_bytes or host_bytes or spill_dir):
+            check("kc_squeue_create", self._lib.kc_squeue_create(state_words, capacity, device, C.byref(self._h)))
+            return
+        c = KcSqueueConfig(state_words=state_words, device=device, segment_states=segment_states or capacity,
+                           hbm_bytes=hbm_bytes, host_bytes=host_bytes,
+                           spill_dir=spill_dir.encode() if spill_dir else None)
+        check("kc_squeue_create2", self._lib.kc_squeue_create2(C.byref(c), C.byref(self._h)))
+
+    @staticmethod
+    def _ptr(x) -> int:
+        return int(x.data_ptr()) if hasattr(x, "data_ptr") else int(x)
+
+    @staticmethod
+    def _st(stream):
+        if stream is None:
+            return None
+        return C.c_void_p(int(getattr(stream, "cuda_stream", stream)))
 
     def enqueue(self, states: np.ndarray) -> None:
         a = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, self.words)
@@ -326,6 +367,52 @@ class StateQueue:
         n = C.c_size_t()
         check("kc_squeue_dequeue", self._lib.kc_squeue_dequeue(self._h, _u64(out), max_n, C.byref(n)))
         return out[: n.value]
+
+    def enqueue_dev(self, states, n: Optional[int] = None, stream=None) -> None:
+        """Append n states from device memory (a CUDA tensor of n x words
+        64-bit values, or a device pointer with n given)."""
+        if n is None:
+            n = states.numel() // self.words
+        check("kc_squeue_enqueue_dev",
+              self._lib.kc_squeue_enqueue_dev(self._h, C.c_void_p(self._ptr(states)), n, self._st(stream)))
+
+    def dequeue_dev(self, out, max_n: int, stream=None) -> int:
+        """Move up to max_n head states into device memory; returns the count."""
+        got = C.c_size_t()
+        check("kc_squeue_dequeue_dev", self._lib.kc_squeue_dequeue_dev(
+            self._h, C.c_void_p(self._ptr(out)), max_n, C.byref(got), self._st(stream)))
+        return got.value
+
+    def reserve_dev(self, n: int, stream=None) -> int:
+        """Device pointer to n writable states at the tail (then commit)."""
+        p = C.c_void_p()
+        check("kc_squeue_reserve_dev", self._lib.kc_squeue_reserve_dev(self._h, n, C.byref(p), self._st(stream)))
+        return int(p.value)
+
+    def commit(self, n: int, stream=None) -> None:
+        check("kc_squeue_commit", self._lib.kc_squeue_commit(self._h, n, self._st(stream)))
+
+    def front_dev(self, offset: int, max_n: int, stream=None):
+        """(device pointer, count) of a contiguous run `offset` states after
+        the head; count may be < max_n at a segment end."""
+        p = C.c_void_p()
+        got = C.c_size_t()
+        check("kc_squeue_front_dev", self._lib.kc_squeue_front_dev(
+            self._h, offset, max_n, C.byref(p), C.byref(got), self._st(stream)))
+        return int(p.value or 0), got.value
+
+    def pop(self, n: int, stream=None) -> None:
+        check("kc_squeue_pop", self._lib.kc_squeue_pop(self._h, n, self._st(stream)))
+
+    def peek(self, offset: int, n: int) -> np.ndarray:
+        out = np.zeros((n, self.words), dtype=np.uint64)
+        check("kc_squeue_peek", self._lib.kc_squeue_peek(self._h, offset, n, _u64(out), None))
+        return out
+
+    def stats(self) -> Dict[str, int]:
+        st = KcSqueueStats()
+        check("kc_squeue_get_stats", self._lib.kc_squeue_get_stats(self._h, C.byref(st)))
+        return {f[0]: int(getattr(st, f[0])) for f in KcSqueueStats._fields_}
 
     def size(self) -> int:
         return int(self._lib.kc_squeue_size(self._h))

@@ -33,6 +33,8 @@ class KcModelConfig(C.Structure):
         ("variant", C.c_int), ("device", C.c_int), ("keep_trace", C.c_int),
         ("max_levels", C.c_int), ("fpset_slots", C.c_uint64), ("chunk_states", C.c_uint64),
         ("verbose", C.c_int), ("timing", C.c_int), ("invariants", C.c_int),
+        ("frontier_hbm_bytes", C.c_uint64), ("frontier_host_bytes", C.c_uint64),
+        ("frontier_segment_states", C.c_uint64), ("spill_dir", C.c_char_p), ("trace_host", C.c_int),
     ]
 
 
@@ -48,7 +50,22 @@ class KcResult(C.Structure):
         ("fpset_slots", C.c_uint64), ("peak_frontier", C.c_uint64),
         ("fpset_probes", C.c_uint64), ("batch_inserts", C.c_uint64),
         ("levels_chunks", C.c_uint64), ("outdeg_hist", C.c_uint64 * 16),
+        ("frontier_spilled_bytes", C.c_uint64), ("frontier_reloaded_bytes", C.c_uint64),
+        ("frontier_peak_hbm_bytes", C.c_uint64),
     ]
+
+
+class KcSqueueConfig(C.Structure):
+    _fields_ = [
+        ("state_words", C.c_int), ("device", C.c_int), ("segment_states", C.c_uint64),
+        ("hbm_bytes", C.c_uint64), ("host_bytes", C.c_uint64), ("spill_dir", C.c_char_p),
+    ]
+
+
+class KcSqueueStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "size", "segments", "seg_hbm", "seg_host", "seg_disk", "hbm_bytes", "host_bytes", "disk_bytes",
+        "spilled_host_bytes", "spilled_disk_bytes", "reloaded_bytes", "peak_hbm_bytes")]
 
 
 # (name, restype, argtypes) for every symbol of include/kubecheck.h
@@ -81,6 +98,15 @@ SIGNATURES = [
     ("kc_stress_fps_dev", C.c_int, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P]),
     ("kc_stress_fp", C.c_uint64, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]),
     ("kc_squeue_create", C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(_P)]),
+    ("kc_squeue_create2", C.c_int, [C.POINTER(KcSqueueConfig), C.POINTER(_P)]),
+    ("kc_squeue_enqueue_dev", C.c_int, [_P, _P, C.c_size_t, _P]),
+    ("kc_squeue_dequeue_dev", C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_size_t), _P]),
+    ("kc_squeue_reserve_dev", C.c_int, [_P, C.c_size_t, C.POINTER(_P), _P]),
+    ("kc_squeue_commit", C.c_int, [_P, C.c_size_t, _P]),
+    ("kc_squeue_front_dev", C.c_int, [_P, C.c_size_t, C.c_size_t, C.POINTER(_P), C.POINTER(C.c_size_t), _P]),
+    ("kc_squeue_pop", C.c_int, [_P, C.c_size_t, _P]),
+    ("kc_squeue_peek", C.c_int, [_P, C.c_size_t, C.c_size_t, _U64P, _P]),
+    ("kc_squeue_get_stats", C.c_int, [_P, C.POINTER(KcSqueueStats)]),
     ("kc_squeue_destroy", None, [_P]),
     ("kc_squeue_enqueue", C.c_int, [_P, _U64P, C.c_size_t]),
     ("kc_squeue_dequeue", C.c_int, [_P, _U64P, C.c_size_t, C.POINTER(C.c_size_t)]),
