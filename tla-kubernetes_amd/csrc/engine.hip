@@ -129,10 +129,6 @@ class EngineT final : public EngineBase {
     KC_HIP_TRY(hipHostMalloc(&h_ns_, sizeof(NarrowCtl)));
     if (narrow_on_) {
       KC_HIP_TRY(hipMalloc(&d_nsc_, sizeof(NarrowScratch)));
-      hipLaunchKernelGGL(k_narrow_scratch_init, dim3((unsigned)((NARROW_LT + 255) / 256)), dim3(256), 0, st_,
-                         d_nsc_);
-      KC_HIP_TRY(hipGetLastError());
-      KC_HIP_TRY(hipStreamSynchronize(st_));
     }
     return 0;
   }
@@ -637,6 +633,7 @@ class EngineT final : public EngineBase {
     if (h_last_) (void)hipHostFree(h_last_);
     if (d_ns_) (void)hipFree(d_ns_);
     if (d_nsc_) (void)hipFree(d_nsc_);
+    if (d_ntrace_) (void)hipFree(d_ntrace_);
     if (h_ns_) (void)hipHostFree(h_ns_);
     for (auto& e : ev_pool_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
@@ -678,23 +675,26 @@ class EngineT final : public EngineBase {
       return 0;
     }
     KC_HIP_TRY(hipMemcpyAsync(d_ns_, h_ns_, offsetof(NarrowCtl, widths), hipMemcpyHostToDevice, st_));
+    // both level tables clear (the last level of the previous run left one dirty)
+    KC_HIP_TRY(hipMemsetAsync(d_nsc_, 0, sizeof(NarrowScratch), st_));
+    const char* nt = getenv("KC_NARROW_TRACE");
+    if (nt && nt[0] == '1' && !d_ntrace_) KC_HIP_TRY(hipMalloc(&d_ntrace_, kNtraceBytes));
+    if (d_ntrace_) KC_HIP_TRY(hipMemsetAsync(d_ntrace_, 0, kNtraceBytes, st_));
     // NARROW_BATCH levels' launches per host sync; they all read the control
     // block, so the ones after the run has ended return at once
     State *a = cur_, *b = next_;
+    uint32_t lev = 0;                            // level launches enqueued in this run
     for (;;) {
       timed(KK_NARROW, [&] {
-        for (int k = 0; k < NARROW_BATCH; ++k) {
-          hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
-                             cfg_.check_deadlock, d_ns_, d_nsc_, d_ctr_);
-          hipLaunchKernelGGL(k_ninsert, dim3((unsigned)(NARROW_LT / NARROW_THREADS)), dim3(NARROW_THREADS), 0,
-                             st_, d_ns_, d_nsc_, cs_.t, cs_.nslots);
-          hipLaunchKernelGGL(k_nemit<M>, dim3(NARROW_WG), dim3(NARROW_THREADS), 0, st_, a, b, flags_, parent_,
-                             ord_, cfg_.keep_trace, d_ns_, d_nsc_, d_ctr_);
-          hipLaunchKernelGGL(k_nstep, dim3(1), dim3(64), 0, st_, d_ns_, d_ctr_);
+        for (int k = 0; k < NARROW_BATCH; ++k, ++lev) {
+          hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG * NARROW_SUB), dim3(NARROW_THREADS), 0, st_, a, b,
+                             flags_, cfg_.check_deadlock, lev, d_ns_, d_nsc_, d_ctr_, d_ntrace_);
+          hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_, parent_,
+                             ord_, cfg_.keep_trace, lev, d_ns_, d_nsc_, cs_.t, cs_.nslots, d_ctr_, d_ntrace_);
         }
       });
       KC_HIP_TRY(hipGetLastError());
-      KC_HIP_TRY(hipMemcpyAsync(h_ns_, d_ns_, offsetof(NarrowCtl, cand_acc), hipMemcpyDeviceToHost, st_));
+      KC_HIP_TRY(hipMemcpyAsync(h_ns_, d_ns_, offsetof(NarrowCtl, close_acc), hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
       KC_HIP_TRY(hipStreamSynchronize(st_));
       if (h_ctr_->overflow) {
@@ -704,6 +704,7 @@ class EngineT final : public EngineBase {
       if (!h.active) break;
     }
     collect_times();
+    if (d_ntrace_) KC_TRY(print_ntrace(lev));
     KC_HIP_TRY(hipMemcpy(h_ns_->widths + level, d_ns_->widths + level,
                          sizeof(uint64_t) * std::min<uint64_t>(h.levels + 1, KC_MAX_LEVELS - level),
                          hipMemcpyDeviceToHost));
@@ -921,6 +922,56 @@ class EngineT final : public EngineBase {
     finish(res, t0, n);
     return 0;
   }
+
+  // KC_NARROW_TRACE=1: per-phase timestamps of the narrow kernels (thread 0
+  // of every workgroup), summarised on stderr after each narrow run
+  static constexpr size_t kNtraceBytes = (NTRACE_FOFF + NTRACE_LEVELS * NARROW_FWG * NTRACE_PH) * 8;
+  int print_ntrace(uint32_t launches) {
+    std::vector<unsigned long long> t(kNtraceBytes / 8);
+    KC_HIP_TRY(hipMemcpy(t.data(), d_ntrace_, kNtraceBytes, hipMemcpyDeviceToHost));
+    const int XW = NARROW_WG * NARROW_SUB, FW = NARROW_FWG;
+    double acc[12] = {};
+    int nl = 0;
+    for (uint32_t l = 0; l < launches && l < NTRACE_LEVELS; ++l) {
+      const unsigned long long* x = &t[(uint64_t)l * XW * NTRACE_PH];
+      const unsigned long long* f = &t[NTRACE_FOFF + (uint64_t)l * FW * NTRACE_PH];
+      if (!x[1] || !f[1]) continue;                    // inactive launch
+      unsigned long long x0 = ~0ull, x3 = 0, f0 = ~0ull, f6 = 0, f7 = 0, f0max = 0, f3min = ~0ull, f3max = 0;
+      double ph[8] = {};
+      for (int w = 0; w < XW; ++w) {
+        x0 = std::min(x0, x[w * NTRACE_PH]);
+        x3 = std::max(x3, x[w * NTRACE_PH + 3]);
+      }
+      for (int w = 0; w < FW; ++w) {
+        const unsigned long long* q = f + w * NTRACE_PH;
+        f0 = std::min(f0, q[0]);
+        f0max = std::max(f0max, q[0]);
+        f3min = std::min(f3min, q[3]);
+        f3max = std::max(f3max, q[3]);
+        f6 = std::max(f6, q[6]);
+        if (q[7]) f7 = q[7];
+        for (int k = 1; k <= 6; ++k) ph[k] += (double)(q[k] - q[k - 1]) / FW;
+      }
+      acc[0] += (double)(x3 - x0);          // k_nexpand span
+      acc[1] += (double)(f0 - x3);          // gap to k_nfinish
+      for (int k = 1; k <= 6; ++k) acc[1 + k] += ph[k];
+      acc[8] += (double)(f7 - f6);          // close (last workgroup)
+      acc[9] += (double)(f7 - f0);          // k_nfinish span
+      acc[10] += (double)(f0max - f0);      // workgroup start spread
+      acc[11] += (double)(f3max - f3min);   // publish spread
+      ++nl;
+    }
+    if (!nl) return 0;
+    const double u = 0.01 / nl;             // 100 MHz ticks -> us, per level
+    fprintf(stderr,
+            "kubecheck narrow trace (%d levels, us per level): k_nexpand span %.2f | gap %.2f | k_nfinish: "
+            "start %.2f, successors+ClaimSet %.2f, mask scan %.2f, publish+wait %.2f, emit+clear %.2f, "
+            "counters %.2f, close %.2f; span %.2f; start spread %.2f, publish spread %.2f\n",
+            nl, acc[0] * u, acc[1] * u, acc[2] * u, acc[3] * u, acc[4] * u, acc[5] * u, acc[6] * u,
+            acc[7] * u, acc[8] * u, acc[9] * u, acc[10] * u, acc[11] * u);
+    return 0;
+  }
+  unsigned long long* d_ntrace_ = nullptr;
 
   Flags flags_{};
   bool queued_ = false;
