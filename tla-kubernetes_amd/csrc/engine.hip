@@ -665,7 +665,7 @@ class EngineT final : public EngineBase {
     h.par_cap = cfg_.keep_trace ? std::min(par_cap_, ord_cap_) : ~0ull;
     h.room = cs_.capacity() / 2 > cs_.count ? cs_.capacity() / 2 - cs_.count : 0;
     h.stop_level = (uint32_t)stop;
-    h.err = ~0ull;
+    h.err[0] = h.err[1] = ~0ull;
     h.epoch = ++narrow_epoch_;
     h.reason = narrow_exit_reason(h);
     h.active = h.reason == 0;
@@ -684,14 +684,16 @@ class EngineT final : public EngineBase {
     // block, so the ones after the run has ended return at once
     State *a = cur_, *b = next_;
     uint32_t lev = 0;                            // level launches enqueued in this run
+    // the run's first level is expanded on its own; every k_nfinish then
+    // expands the states it emits for the level after it
+    hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG * NARROW_SUB), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
+                       cfg_.check_deadlock, 0u, d_ns_, d_nsc_, d_ctr_, d_ntrace_);
     for (;;) {
       timed(KK_NARROW, [&] {
-        for (int k = 0; k < NARROW_BATCH; ++k, ++lev) {
-          hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG * NARROW_SUB), dim3(NARROW_THREADS), 0, st_, a, b,
-                             flags_, cfg_.check_deadlock, lev, d_ns_, d_nsc_, d_ctr_, d_ntrace_);
-          hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_, parent_,
-                             ord_, cfg_.keep_trace, lev, d_ns_, d_nsc_, cs_.t, cs_.nslots, d_ctr_, d_ntrace_);
-        }
+        for (int k = 0; k < NARROW_BATCH; ++k, ++lev)
+          hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
+                             cfg_.check_deadlock, parent_, ord_, cfg_.keep_trace, lev, d_ns_, d_nsc_, cs_.t,
+                             cs_.nslots, d_ctr_, d_ntrace_);
       });
       KC_HIP_TRY(hipGetLastError());
       KC_HIP_TRY(hipMemcpyAsync(h_ns_, d_ns_, offsetof(NarrowCtl, close_acc), hipMemcpyDeviceToHost, st_));
@@ -929,46 +931,52 @@ class EngineT final : public EngineBase {
   int print_ntrace(uint32_t launches) {
     std::vector<unsigned long long> t(kNtraceBytes / 8);
     KC_HIP_TRY(hipMemcpy(t.data(), d_ntrace_, kNtraceBytes, hipMemcpyDeviceToHost));
-    const int XW = NARROW_WG * NARROW_SUB, FW = NARROW_FWG;
-    double acc[12] = {};
-    int nl = 0;
+    const int FW = NARROW_FWG;
+    constexpr int P = NTRACE_PH;
+    double all[P] = {}, w0[P] = {}, span = 0, gap = 0, close = 0, pub_spread = 0;
+    int nl = 0, ng = 0;
+    unsigned long long prev_end = 0;
     for (uint32_t l = 0; l < launches && l < NTRACE_LEVELS; ++l) {
-      const unsigned long long* x = &t[(uint64_t)l * XW * NTRACE_PH];
-      const unsigned long long* f = &t[NTRACE_FOFF + (uint64_t)l * FW * NTRACE_PH];
-      if (!x[1] || !f[1]) continue;                    // inactive launch
-      unsigned long long x0 = ~0ull, x3 = 0, f0 = ~0ull, f6 = 0, f7 = 0, f0max = 0, f3min = ~0ull, f3max = 0;
-      double ph[8] = {};
-      for (int w = 0; w < XW; ++w) {
-        x0 = std::min(x0, x[w * NTRACE_PH]);
-        x3 = std::max(x3, x[w * NTRACE_PH + 3]);
+      const unsigned long long* f = &t[NTRACE_FOFF + (uint64_t)l * FW * P];
+      if (!f[1]) {                                     // inactive launch
+        prev_end = 0;
+        continue;
       }
+      unsigned long long f0 = ~0ull, f9 = 0, f10 = 0, f4min = ~0ull, f4max = 0;
       for (int w = 0; w < FW; ++w) {
-        const unsigned long long* q = f + w * NTRACE_PH;
+        const unsigned long long* q = f + w * P;
         f0 = std::min(f0, q[0]);
-        f0max = std::max(f0max, q[0]);
-        f3min = std::min(f3min, q[3]);
-        f3max = std::max(f3max, q[3]);
-        f6 = std::max(f6, q[6]);
-        if (q[7]) f7 = q[7];
-        for (int k = 1; k <= 6; ++k) ph[k] += (double)(q[k] - q[k - 1]) / FW;
+        f4min = std::min(f4min, q[3]);
+        f4max = std::max(f4max, q[3]);
+        f9 = std::max(f9, q[9]);
+        if (q[10]) f10 = q[10];
+        for (int k = 1; k <= 9; ++k) all[k] += (double)(q[k] - q[k - 1]) / FW;
       }
-      acc[0] += (double)(x3 - x0);          // k_nexpand span
-      acc[1] += (double)(f0 - x3);          // gap to k_nfinish
-      for (int k = 1; k <= 6; ++k) acc[1 + k] += ph[k];
-      acc[8] += (double)(f7 - f6);          // close (last workgroup)
-      acc[9] += (double)(f7 - f0);          // k_nfinish span
-      acc[10] += (double)(f0max - f0);      // workgroup start spread
-      acc[11] += (double)(f3max - f3min);   // publish spread
+      for (int k = 1; k <= 9; ++k) w0[k] += (double)(f[k] - f[k - 1]);   // workgroup 0 (always live)
+      close += (double)(f10 - f9);
+      span += (double)(f10 - f0);
+      pub_spread += (double)(f4max - f4min);
+      if (prev_end && f0 > prev_end) {
+        gap += (double)(f0 - prev_end);
+        ++ng;
+      }
+      prev_end = f10;
       ++nl;
     }
     if (!nl) return 0;
     const double u = 0.01 / nl;             // 100 MHz ticks -> us, per level
-    fprintf(stderr,
-            "kubecheck narrow trace (%d levels, us per level): k_nexpand span %.2f | gap %.2f | k_nfinish: "
-            "start %.2f, successors+ClaimSet %.2f, mask scan %.2f, publish+wait %.2f, emit+clear %.2f, "
-            "counters %.2f, close %.2f; span %.2f; start spread %.2f, publish spread %.2f\n",
-            nl, acc[0] * u, acc[1] * u, acc[2] * u, acc[3] * u, acc[4] * u, acc[5] * u, acc[6] * u,
-            acc[7] * u, acc[8] * u, acc[9] * u, acc[10] * u, acc[11] * u);
+    static const char* names[P] = {"", "start", "successors+ClaimSet", "mask scan", "publish+wait", "emit",
+                                   "task scan", "expand tasks", "clear", "counters", "", ""};
+    std::string a = "kubecheck narrow trace (" + std::to_string(nl) + " levels, us per level; mean over workgroups / workgroup 0):";
+    char buf[96];
+    for (int k = 1; k <= 9; ++k) {
+      snprintf(buf, sizeof buf, " %s %.2f/%.2f,", names[k], all[k] * u, w0[k] * u);
+      a += buf;
+    }
+    snprintf(buf, sizeof buf, " close %.2f; span %.2f; publish spread %.2f; gap between levels %.2f\n", close * u,
+             span * u, pub_spread * u, ng ? gap * 0.01 / ng : 0.0);
+    a += buf;
+    fputs(a.c_str(), stderr);
     return 0;
   }
   unsigned long long* d_ntrace_ = nullptr;

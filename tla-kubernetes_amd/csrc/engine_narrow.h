@@ -107,7 +107,13 @@ struct NarrowCtl {
   uint64_t err_key;      // the error that ended the run (NX_ERROR)
   // per level (returned to 0 / ~0 when the level closes)
   unsigned long long close_acc;            // k_nfinish workgroups done << 56 | new states << 28 | their successors
-  unsigned long long err;                  // min error key (~0 = none)
+  // by level parity: [L & 1] = level L's min error key (~0 = none): its
+  // parents' assertion / deadlock errors (found when they were emitted, by
+  // the previous level's k_nfinish, or by k_nexpand) and its successors'
+  // invariant errors
+  unsigned long long err[2];
+  unsigned int act_next[2][A_COUNT];       // level L's per-action successor counts, committed when L runs
+  unsigned int lt_over[2];                 // level L's table overflowed: it cannot run narrow
   unsigned long long wg_pub[NARROW_FWG];   // k_nfinish: pub_tag(epoch, level) | workgroup's new states
   uint64_t widths[KC_MAX_LEVELS];          // widths[L] = width of level L + 1
 };
@@ -117,10 +123,22 @@ struct NarrowLT {
   unsigned int nkey;       // ~(min order key (parent << 5 | t)); 0 = none
   unsigned int pad;
 };
-// two level tables, by level parity; all-zero = clear (hipMemset)
+// three level tables, by level mod 3: k_nfinish of level L reads T[L],
+// fills T[L + 1] with the successors of the states it emits, and clears
+// T[L + 2] (last read by level L - 1); all-zero = clear (hipMemset)
+constexpr int NARROW_NLT = 3;
+constexpr int NARROW_LT_PROBES = 256;        // a longer probe run = table overflow (the level goes wide)
 struct NarrowScratch {
-  NarrowLT lt[2][NARROW_LT];
+  NarrowLT lt[NARROW_NLT][NARROW_LT];
+  // by level parity, for every state of a level (written when it was
+  // expanded into the table): its plan's slot counts and successor total,
+  // and the table slot of each successor, so k_nfinish finds its entries
+  // without re-deriving anything
+  unsigned long long pcnt[2][NARROW_MAX];
+  unsigned char ptot[2][NARROW_MAX];
+  unsigned short hidx[2][NARROW_MAX * 32];
 };
+static_assert(NARROW_LT <= 65536, "table slots fit hidx");
 
 // The rule a level is checked against before it runs narrow (the host
 // before a run, the closing wave after every level).
@@ -144,7 +162,7 @@ __device__ __forceinline__ unsigned long long pub_tag(uint32_t epoch, uint32_t l
 
 // Phase timestamps (diagnostic: KC_NARROW_TRACE=1; ntrace == nullptr
 // otherwise): thread 0 of every workgroup, wall clock (100 MHz), per launch.
-constexpr int NTRACE_PH = 8;
+constexpr int NTRACE_PH = 12;
 constexpr uint64_t NTRACE_LEVELS = 1024;
 constexpr uint64_t NTRACE_FOFF = NTRACE_LEVELS * NARROW_WG * NARROW_SUB * NTRACE_PH;
 #define NTRACE_X(ph)                                                                                  \
@@ -160,6 +178,38 @@ constexpr uint64_t NTRACE_FOFF = NTRACE_LEVELS * NARROW_WG * NARROW_SUB * NTRACE
 
 __device__ __forceinline__ uint64_t lt_slot(uint64_t fp) {
   return (fp * 0xd6e8feb86659fd93ull) >> (64 - NARROW_LT_BITS);
+}
+
+// Enter up to NB successors (fingerprint fp[k] != 0, order key key[k]) of
+// one lane into a level table: the CASes back to back (independent round
+// trips in flight), linear probing on for the few that collide, then the
+// key minimums (kept as ~max).  False if a probe run passed
+// NARROW_LT_PROBES (the table is too full for this level).
+template <int NB>
+__device__ __forceinline__ bool lt_enter(NarrowLT* __restrict__ lt, const uint64_t (&fp)[NB],
+                                         const unsigned int (&key)[NB], uint64_t (&h)[NB]) {
+  unsigned long long e[NB];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    h[k] = lt_slot(fp[k]);
+    e[k] = fp[k] ? atomicCAS(&lt[h[k]].fp, 0ull, (unsigned long long)fp[k]) : 0ull;
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    for (int q = 0; fp[k] && e[k] != 0ull && e[k] != fp[k]; ++q) {
+      if (q >= NARROW_LT_PROBES) {
+        ok = false;
+        break;
+      }
+      h[k] = (h[k] + 1) & (NARROW_LT - 1);
+      e[k] = atomicCAS(&lt[h[k]].fp, 0ull, (unsigned long long)fp[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    if (fp[k] && (e[k] == 0ull || e[k] == fp[k])) atomicMax(&lt[h[k]].nkey, ~key[k]);
+  return ok;
 }
 
 // grid: NARROW_WG * NARROW_SUB workgroups; lane g = parent g / NARROW_SUB,
@@ -186,14 +236,16 @@ k_nexpand(const typename M::State* __restrict__ bufA, const typename M::State* _
   __shared__ unsigned int sh_act[A_COUNT];
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
-  NarrowLT* __restrict__ lt = sc->lt[lev & 1];
+  NarrowLT* __restrict__ lt = sc->lt[lev % NARROW_NLT];
   if (i < n) {
     const typename M::Plan pl = M::plan(s, f);
     if (sub == 0) {
+      sc->pcnt[lev & 1][i] = pl.counts;
+      sc->ptot[lev & 1][i] = (unsigned char)(pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC);
       if (pl.fail_pos >= 0)
-        atomicMin(&ctl->err, (i << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
+        atomicMin(&ctl->err[lev & 1], (i << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
       else if (pl.total == 0 && check_deadlock)
-        atomicMin(&ctl->err, (i << 16) | E_DEADLOCK);
+        atomicMin(&ctl->err[lev & 1], (i << 16) | E_DEADLOCK);
 #pragma unroll
       for (int slot = 0; slot < M::NSLOT; ++slot) {
         const int c = (int)((pl.counts >> (6 * slot)) & 63);
@@ -208,15 +260,13 @@ k_nexpand(const typename M::State* __restrict__ bufA, const typename M::State* _
       M::locate(pl, t, slot, j);
       State x;
       M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
-      uint64_t h = lt_slot(fp);
-      unsigned long long e = atomicCAS(&lt[h].fp, 0ull, (unsigned long long)fp);
-      // collision: probe on (rare at <= 1/2 load)
-      for (uint64_t q = 0; e != 0ull && e != fp && q < NARROW_LT; ++q) {
-        h = (h + 1) & (NARROW_LT - 1);
-        e = atomicCAS(&lt[h].fp, 0ull, (unsigned long long)fp);
-      }
-      atomicMax(&lt[h].nkey, ~(unsigned int)((i << 5) | (uint64_t)t));
+      const uint64_t fp[1] = {M::fingerprint_succ(s, fold, x, who)};
+      const unsigned int key[1] = {(unsigned int)((i << 5) | (uint64_t)t)};
+      // (the host admitted this level at <= 1/2 table load: a probe run this
+      // long cannot happen; fail the run loudly if it does)
+      uint64_t h[1];
+      if (!lt_enter<1>(lt, fp, key, h)) atomicAdd(&C->overflow, 1ull);
+      sc->hidx[lev & 1][i * 32 + t] = (unsigned short)h[0];
     }
   }
   NTRACE_X(2);
@@ -227,12 +277,46 @@ k_nexpand(const typename M::State* __restrict__ bufA, const typename M::State* _
 }
 
 __device__ __forceinline__ void narrow_step(NarrowCtl* __restrict__ ctl, Counters* __restrict__ C, uint64_t total,
-                                            unsigned long long cnext);
+                                            unsigned long long cnext, uint32_t lev);
+
+// k_nfinish stages up to NX_LDS emitted states per workgroup for the next
+// level's expansion; past that a lane enters its state's successors itself
+constexpr int NX_LDS = 256;
+template <class M>
+__device__ __forceinline__ bool lt_enter_succ(NarrowLT* __restrict__ lt, unsigned short* __restrict__ hx,
+                                              const typename M::State& x, const typename M::Plan& px, int tx,
+                                              unsigned int o, Flags f) {
+  bool ok = true;
+  const uint64_t foldx = M::fp_fold(x);
+  constexpr int NB = 8;
+  for (int t0 = 0; t0 < tx; t0 += NB) {
+    uint64_t fpx[NB];
+    unsigned int kx[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      fpx[q] = 0;
+      kx[q] = (o << 5) | (unsigned int)(t0 + q);
+      if (t0 + q < tx) {
+        int sl, j, who;
+        M::locate(px, t0 + q, sl, j);
+        typename M::State y;
+        M::apply(x, sl, j, f, y, who);
+        fpx[q] = M::fingerprint_succ(x, foldx, y, who);
+      }
+    }
+    uint64_t h[NB];
+    ok &= lt_enter<NB>(lt, fpx, kx, h);
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+      if (t0 + q < tx && o < (unsigned int)NARROW_MAX) hx[o * 32 + t0 + q] = (unsigned short)h[q];
+  }
+  return ok;
+}
 
 template <class M>
 __global__ void __launch_bounds__(NARROW_THREADS)
 k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bufB, Flags f,
-          unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
+          int check_deadlock, unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
           uint32_t lev, NarrowCtl* __restrict__ ctl, NarrowScratch* __restrict__ sc, ClaimEntry* __restrict__ cs,
           uint64_t nslots, Counters* __restrict__ C, unsigned long long* __restrict__ ntrace) {
   using State = typename M::State;
@@ -251,39 +335,56 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   __shared__ unsigned int sh_w[4];
   __shared__ unsigned int sh_base;
   __shared__ unsigned long long sh_cand;
+  __shared__ unsigned int sh_actn[A_COUNT];
+  // emitted states staged for the expansion of level L + 1
+  __shared__ State sh_xs[NX_LDS];
+  __shared__ unsigned long long sh_xc[NX_LDS];
+  __shared__ unsigned int sh_xo[NX_LDS], sh_xt[NX_LDS], sh_xoff[NX_LDS];
+  __shared__ unsigned int sh_nx, sh_ntask, sh_last;
+  __shared__ State sh_ps[NARROW_THREADS / NARROW_ESUB];
+  __shared__ unsigned long long sh_pc[NARROW_THREADS / NARROW_ESUB];
+  __shared__ unsigned int sh_pm[NARROW_THREADS / NARROW_ESUB], sh_pincl[NARROW_THREADS / NARROW_ESUB];
+  __shared__ unsigned long long sh_all;
+  if (threadIdx.x == 0) sh_nx = 0;
+  if (threadIdx.x < A_COUNT) sh_actn[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT) sh_dist[threadIdx.x] = 0;
   if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh_cand = 0;
-  const NarrowLT* __restrict__ lt = sc->lt[lev & 1];
+  // clear level L + 2's table (level L - 1 read it; the stores overlap the loads below)
+  {
+    NarrowLT* __restrict__ other = sc->lt[(lev + 2) % NARROW_NLT];
+    for (uint64_t h = g; h < NARROW_LT; h += (uint64_t)NARROW_FWG * NARROW_THREADS)
+      *reinterpret_cast<ulonglong2*>(&other[h]) = make_ulonglong2(0ull, 0ull);
+  }
+  const NarrowLT* __restrict__ lt = sc->lt[lev % NARROW_NLT];
+  NarrowLT* __restrict__ lt_next = sc->lt[(lev + 1) % NARROW_NLT];
+  const unsigned int pq = lev & 1, qq = pq ^ 1u;      // this level's / the next level's slots
   const unsigned long long tag = pub_tag(epoch, level);
   const bool live = i < n;
   typename M::Plan pl{};
   uint32_t mine = 0;
   unsigned long long probes = 0;
   if (live) {
-    pl = M::plan(s, f);
-    const int tot = pl.total < M::MAXSUCC ? pl.total : M::MAXSUCC;
-    const uint64_t fold = M::fp_fold(s);
+    // the plan and the table slots were stored when this level was expanded
+    pl.counts = sc->pcnt[lev & 1][i];
+    const int tot = sc->ptot[lev & 1][i];
+    const unsigned short* __restrict__ hx = &sc->hidx[lev & 1][i * 32];
     const uint32_t succ_level = level + 1;
-    for (int t = sub; t < tot; t += NARROW_ESUB) {
-      int slot, j, who;
-      M::locate(pl, t, slot, j);
-      State x;
-      M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
-      // its level-table entry (k_nexpand entered every successor)
-      uint64_t h = lt_slot(fp);
-      ulonglong2 e = *reinterpret_cast<const ulonglong2*>(&lt[h]);
-      for (uint64_t q = 0; e.x != fp && e.x != 0ull && q < NARROW_LT; ++q) {
-        h = (h + 1) & (NARROW_LT - 1);
-        e = *reinterpret_cast<const ulonglong2*>(&lt[h]);
-      }
-      if (e.x != fp) {
-        atomicAdd(&C->overflow, 1ull);          // cannot happen: fail the run loudly
-        continue;
-      }
+    constexpr int PT = 32 / NARROW_ESUB;            // successors per lane, at most
+    unsigned int hs[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) hs[k] = sub + k * NARROW_ESUB < tot ? hx[sub + k * NARROW_ESUB] : 0u;
+    ulonglong2 e[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k)
+      e[k] = sub + k * NARROW_ESUB < tot ? *reinterpret_cast<const ulonglong2*>(&lt[hs[k]]) : make_ulonglong2(0, 0);
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const int t = sub + k * NARROW_ESUB;
+      if (t >= tot) continue;
       const unsigned int key = (unsigned int)((i << 5) | (uint64_t)t);
-      if ((unsigned int)~(unsigned int)e.y != key) continue;    // an earlier copy of the level holds it
+      if ((unsigned int)~(unsigned int)e[k].y != key) continue;    // an earlier copy of the level holds it
+      const uint64_t fp = e[k].x;
       // the level's first copy: into the ClaimSet, new unless an earlier level stored it
       ++probes;
       uint64_t ix = bucket_of(fp, nslots);
@@ -313,8 +414,22 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
     if (lane >= off) incl += v;
   }
   if (lane == 63) sh_w[wv] = (unsigned int)incl;
+  // the workgroup's parents (NARROW_THREADS / NARROW_ESUB of them) for the
+  // emit: state, plan counts and new-state mask
+  constexpr int WP = NARROW_THREADS / NARROW_ESUB;
+  const int pl_local = (int)(threadIdx.x / NARROW_ESUB);
+  if (sub == 0) {
+    sh_ps[pl_local] = s;
+    sh_pc[pl_local] = pl.counts;
+    sh_pm[pl_local] = live ? m : 0u;
+  }
   __syncthreads();
   NTRACE_F(3);
+  if (sub == 0) {                                   // inclusive new-state offset in the workgroup
+    unsigned int before = 0;
+    for (int w = 0; w < wv; ++w) before += sh_w[w];
+    sh_pincl[pl_local] = before + (unsigned int)incl;
+  }
   if (live && sub == 0) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
   // publish this workgroup's total tagged with (run, level), no reset needed;
   // then take the totals of the lower workgroups as they arrive
@@ -336,39 +451,147 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   }
   __syncthreads();
   NTRACE_F(4);
-  unsigned int base = sh_base;
-  for (int w = 0; w < wv; ++w) base += sh_w[w];
-  // the parent's first output slot: its sub-0 lane's exclusive prefix
-  const int excl0 = __shfl(incl - cnt, lane & ~(NARROW_ESUB - 1), 64);
+  const unsigned int base = sh_base;
   unsigned long long cnd = 0;
-  if (live && m) {
+  // the workgroup's new states dealt out one per lane (r = rank in the
+  // workgroup, in (parent, t) order): no lane runs more than ceil(wtot/256)
+  // of the emit + expand chains
+  for (unsigned int r = threadIdx.x; r < wtot; r += NARROW_THREADS) {
     State* __restrict__ nxt = (lev & 1) ? bufA : bufB;
     const uint64_t next_gidx = level_gidx + n;
-    uint64_t o = (uint64_t)base + (unsigned int)excl0;
-    int k = 0;
-    for (uint32_t mm = m; mm; mm &= mm - 1, ++k, ++o) {
-      if ((k % NARROW_ESUB) != sub) continue;
-      const int t = __ffs(mm) - 1;
+    unsigned int lo = 0, hi = WP - 1;               // first parent whose inclusive offset > r
+    while (lo < hi) {
+      const unsigned int mid = (lo + hi) >> 1;
+      if (sh_pincl[mid] > r) hi = mid; else lo = mid + 1;
+    }
+    const unsigned int pr = lo;
+    uint32_t mm = sh_pm[pr];
+    for (unsigned int k = r - (sh_pincl[pr] - (unsigned int)__builtin_popcount(mm)); k > 0; --k) mm &= mm - 1;
+    const int t = __ffs(mm) - 1;
+    const uint64_t i = (uint64_t)blockIdx.x * WP + pr;    // the parent
+    const uint64_t o = (uint64_t)base + r;                 // the new state's index in level L + 1
+    const State sp = sh_ps[pr];
+    const typename M::Plan ppl{sh_pc[pr], 0, -1, -1};
+    {
       int slot, j;
-      M::locate(pl, t, slot, j);
+      M::locate(ppl, t, slot, j);
       State x;
-      M::apply(s, slot, j, f, x);
+      M::apply(sp, slot, j, f, x);
       store_state<M>(nxt, o, x);
       if (keep_trace) {
         parent[next_gidx + o] = level_gidx + i;
         ord[next_gidx + o] = (uint8_t)t;
       }
-      if (M::check(x, f.inv_mask) >= 0) atomicMin(&ctl->err, (i << 16) | ((uint64_t)t << 8) | E_INVARIANT);
-      atomicAdd(&sh_dist[M::slot_action(s, slot)], 1u);
-      cnd += (unsigned long long)M::plan(x, f).total;
+      if (M::check(x, f.inv_mask) >= 0)
+        atomicMin(&ctl->err[pq], (i << 16) | ((uint64_t)t << 8) | E_INVARIANT);
+      atomicAdd(&sh_dist[M::slot_action(sp, slot)], 1u);
+      // expand x for level L + 1 while it is in registers: its errors,
+      // per-action counts and its successors' table entries (key: its index
+      // o in level L + 1) are level L + 1's, kept only if that level runs
+      // narrow (the closing step commits or discards them)
+      const typename M::Plan px = M::plan(x, f);
+      cnd += (unsigned long long)px.total;
+      if (px.fail_pos >= 0)
+        atomicMin(&ctl->err[qq], (o << 16) | ((uint64_t)px.fail_pos << 8) | E_ASSERT);
+      else if (px.total == 0 && check_deadlock)
+        atomicMin(&ctl->err[qq], (o << 16) | E_DEADLOCK);
+#pragma unroll
+      for (int sl = 0; sl < M::NSLOT; ++sl) {
+        const int c = (int)((px.counts >> (6 * sl)) & 63);
+        if (c) atomicAdd(&sh_actn[M::slot_action(x, sl)], (unsigned)c);
+      }
+      if (px.total > M::MAXSUCC) atomicOr(&ctl->lt_over[qq], 1u);   // (the wide path reports it, if it gets there)
+      const int tx = px.total < M::MAXSUCC ? px.total : M::MAXSUCC;
+      if (o < (uint64_t)NARROW_MAX) {
+        sc->pcnt[qq][o] = px.counts;
+        sc->ptot[qq][o] = (unsigned char)tx;
+      }
+      if (tx) {
+        // its successors are spread over the whole workgroup below: stage it
+        const unsigned int xs = atomicAdd(&sh_nx, 1u);
+        if (xs < NX_LDS) {
+          sh_xs[xs] = x;
+          sh_xc[xs] = px.counts;
+          sh_xo[xs] = (unsigned int)o;
+          sh_xt[xs] = (unsigned int)tx;
+        } else if (!lt_enter_succ<M>(lt_next, sc->hidx[qq], x, px, tx, (unsigned int)o, f)) {   // LDS full: this lane
+          atomicOr(&ctl->lt_over[qq], 1u);
+        }
+      }
     }
   }
-  // clear the other level table for level L + 1 (level L - 1 read it)
+  // the staged states' successors, one (state, t) task per lane: their
+  // fingerprints go into level L + 1's table
+  __syncthreads();
+  NTRACE_F(5);
   {
-    NarrowLT* __restrict__ other = sc->lt[(lev + 1) & 1];
-    for (uint64_t h = g; h < NARROW_LT; h += (uint64_t)NARROW_FWG * NARROW_THREADS)
-      *reinterpret_cast<ulonglong2*>(&other[h]) = make_ulonglong2(0ull, 0ull);
+    const unsigned int nx = sh_nx < NX_LDS ? sh_nx : NX_LDS;
+    if (wv == 0) {                                  // exclusive prefix of the successor counts
+      constexpr int PER = (NX_LDS + 63) / 64;
+      unsigned int sum = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const unsigned int ix = lane * PER + k;
+        sum += ix < nx ? sh_xt[ix] : 0u;
+      }
+      unsigned int inc = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned int v = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += v;
+      }
+      unsigned int run = inc - sum;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const unsigned int ix = lane * PER + k;
+        if (ix < nx) {
+          sh_xoff[ix] = run;
+          run += sh_xt[ix];
+        }
+      }
+      if (lane == 63) sh_ntask = inc;
+    }
+    __syncthreads();
+    NTRACE_F(6);
+    const unsigned int T = sh_ntask;
+    bool ok = true;
+    constexpr int NB2 = 2;
+    for (unsigned int b0 = threadIdx.x; b0 < T; b0 += NARROW_THREADS * NB2) {
+      uint64_t fpx[NB2];
+      unsigned int kx[NB2];
+#pragma unroll
+      for (int q = 0; q < NB2; ++q) {
+        const unsigned int j = b0 + (unsigned int)q * NARROW_THREADS;
+        fpx[q] = 0;
+        kx[q] = 0;
+        if (j < T) {
+          unsigned int lo = 0, hi = nx;             // last staged state with offset <= j
+          while (hi - lo > 1) {
+            const unsigned int mid = (lo + hi) >> 1;
+            if (sh_xoff[mid] <= j) lo = mid; else hi = mid;
+          }
+          const int t = (int)(j - sh_xoff[lo]);
+          const State xx = sh_xs[lo];
+          const typename M::Plan pxx{sh_xc[lo], 0, -1, -1};
+          int sl2, j2, who2;
+          M::locate(pxx, t, sl2, j2);
+          State y;
+          M::apply(xx, sl2, j2, f, y, who2);
+          fpx[q] = M::fingerprint_succ(xx, M::fp_fold(xx), y, who2);
+          kx[q] = (sh_xo[lo] << 5) | (unsigned int)t;
+        }
+      }
+      uint64_t h[NB2];
+      ok &= lt_enter<NB2>(lt_next, fpx, kx, h);
+#pragma unroll
+      for (int q = 0; q < NB2; ++q) {
+        const unsigned int o2 = kx[q] >> 5;
+        if (fpx[q] && o2 < (unsigned int)NARROW_MAX) sc->hidx[qq][o2 * 32 + (kx[q] & 31)] = (unsigned short)h[q];
+      }
+    }
+    if (!ok) atomicOr(&ctl->lt_over[qq], 1u);
   }
+  NTRACE_F(7);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     cnd += __shfl_down(cnd, off, 64);
@@ -377,11 +600,12 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   if (lane == 0 && cnd) atomicAdd(&sh_cand, cnd);
   if (lane == 0 && probes) atomicAdd((unsigned long long*)&ctl->probes, probes);
   __syncthreads();
-  NTRACE_F(5);
+  NTRACE_F(8);
   if (threadIdx.x < A_COUNT && sh_dist[threadIdx.x])
     atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_dist[threadIdx.x]);
   if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
     atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
+  if (threadIdx.x < A_COUNT && sh_actn[threadIdx.x]) atomicAdd(&ctl->act_next[qq][threadIdx.x], sh_actn[threadIdx.x]);
   // The last workgroup to get here closes the level.  Its inputs are all
   // device-scope atomics: every wave waits for its own to complete (an
   // s_waitcnt on all counters; no L2 write-back needed), then one returning
@@ -390,46 +614,68 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   // reads only the error key.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  NTRACE_F(6);
+  NTRACE_F(9);
   if (threadIdx.x == 0) {
     const unsigned long long mine_acc = (1ull << 56) | ((unsigned long long)wtot << 28) | sh_cand;
     const unsigned long long prev = atomicAdd(&ctl->close_acc, mine_acc);
-    if ((prev >> 56) == NARROW_FWG - 1) {
-      const unsigned long long all = prev + mine_acc;
-      narrow_step(ctl, C, (all >> 28) & ((1ull << 28) - 1), all & ((1ull << 28) - 1));
-      NTRACE_F(7);
-    }
+    sh_last = (prev >> 56) == NARROW_FWG - 1;
+    sh_all = prev + mine_acc;
+  }
+  __syncthreads();
+  if (sh_last && wv == 0) {
+    const unsigned long long all = sh_all;
+    narrow_step(ctl, C, (all >> 28) & ((1ull << 28) - 1), all & ((1ull << 28) - 1), lev);
+    NTRACE_F(10);
   }
 }
 
-// One thread (of the last k_nfinish workgroup to finish): close the level
-// (its `total` new states with `cnext` successors) and decide about the next.
+// Wave 0 of the last k_nfinish workgroup to finish: close level L (its
+// `total` new states with `cnext` successors) and decide about L + 1; lane
+// a commits (L + 1 runs narrow) or drops action a's pre-expansion count.
 __device__ __forceinline__ void narrow_step(NarrowCtl* __restrict__ ctl, Counters* __restrict__ C, uint64_t total,
-                                            unsigned long long cnext) {
+                                            unsigned long long cnext, uint32_t lev) {
   NarrowCtl& c = *ctl;
-  const unsigned long long err = __hip_atomic_load(&c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  c.close_acc = 0;
-  c.err = ~0ull;
-  ++c.levels;
-  c.new_total += total;
-  c.room = c.room > total ? c.room - total : 0;
-  if (err != ~0ull) {                    // the level stays the current one
-    c.err_key = err;
-    C->err_key = err;
-    c.reason = NX_ERROR;
-    c.active = 0;
-    return;
+  const unsigned int pq = lev & 1, qq = pq ^ 1u;
+  const int lane = threadIdx.x & 63;
+  int keep = 0;                                  // level L + 1 runs narrow
+  if (lane == 0) {
+    const unsigned long long err = __hip_atomic_load(&c.err[pq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c.close_acc = 0;
+    c.err[pq] = ~0ull;
+    ++c.levels;
+    c.new_total += total;
+    c.room = c.room > total ? c.room - total : 0;
+    if (err != ~0ull) {                          // the level stays the current one
+      c.err_key = err;
+      C->err_key = err;
+      c.reason = NX_ERROR;
+      c.active = 0;
+    } else {
+      if (c.level < KC_MAX_LEVELS) c.widths[c.level] = total;
+      c.level_gidx += c.n;
+      c.n = total;
+      c.cand = cnext;
+      c.level += 1;
+      c.cur_is_b ^= 1u;
+      int r = narrow_exit_reason(c);
+      if (!r && __hip_atomic_load(&c.lt_over[qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) r = NX_ROOM;
+      if (r) {
+        c.reason = r;
+        c.active = 0;
+      } else {
+        keep = 1;
+      }
+    }
+    if (!keep) c.err[qq] = ~0ull;              // drop level L + 1's pre-expansion
+    c.lt_over[qq] = 0;
   }
-  if (c.level < KC_MAX_LEVELS) c.widths[c.level] = total;
-  c.level_gidx += c.n;
-  c.n = total;
-  c.cand = cnext;
-  c.level += 1;
-  c.cur_is_b ^= 1u;
-  const int r = narrow_exit_reason(c);
-  if (r) {
-    c.reason = r;
-    c.active = 0;
+  keep = __shfl(keep, 0, 64);
+  if (lane < A_COUNT) {
+    const unsigned int v = __hip_atomic_load(&c.act_next[qq][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v) {
+      if (keep) atomicAdd(&C->s[0].act_gen[lane], (unsigned long long)v);
+      c.act_next[qq][lane] = 0;
+    }
   }
 }
 
