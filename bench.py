@@ -396,7 +396,7 @@ def main():
             print(json.dumps(out), flush=True)
         return
     if args.workload == "fpset":
-        if args.gpus > 1:
+        if args.gpus > 1 or args.sharded:
             from kubecheck.sharded_fpset import bench_sharded_fpset
 
             out = bench_sharded_fpset(args)
