@@ -226,3 +226,19 @@ def test_native_rccl_world1(fixtures, monkeypatch):
         assert r["error"] == "assertion" and r["trace"] == fixtures["nc2"]["trace"]
     finally:
         mc.close()
+
+
+@pytest.mark.parametrize("R", [8])
+def test_native_enlarged_full_emulated(fixtures, R):
+    # the whole NP=2 model through the native sharded loop with 8 ranks on one
+    # GPU (LocalComm): the 8-GPU protocol at full size, against the golden
+    fx = fixtures["np2_full"]
+    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False), emulate=R)
+    try:
+        r = mc.run()
+    finally:
+        mc.close()
+    assert r["complete"] and r["error"] is None
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["level_width"] == fx["level_width"]
+    assert r["act_gen"] == fx["act_gen"]
