@@ -104,7 +104,9 @@ class EngineT final : public EngineBase {
     narrow_on_ = cfg.chunk_states == 0 && !(nw && nw[0] == '0') && !ablate_;
     // frontiers in the StateQueue (spill mode): the chunked wide path only
     queued_ = cfg.frontier_hbm_bytes > 0;
-    if (queued_) narrow_on_ = false;
+    if (queued_) narrow_on_ = false;    // k_claim tile order (engine_kernels.h spread_tile; KC_TILE_SPREAD=0: block order)
+    const char* sp = getenv("KC_TILE_SPREAD");
+    if (sp) claim_args_.spread = (uint32_t)atoi(sp);
   }
   ~EngineT() override { release(); }
 
@@ -290,24 +292,24 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
+                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
           timed(KA_LDS, [&] {
             hipLaunchKernelGGL((k_claim<M, 1>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
           timed(KA_COMPUTE, [&] {
             hipLaunchKernelGGL((k_claim<M, 2>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
           timed(KA_PLAN, [&] {
             hipLaunchKernelGGL((k_claim<M, 3>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, ShardArgs{});
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
         }
         timed(KK_RESOLVE, [&] {
@@ -833,7 +835,7 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur, m, start, flags_,
                              cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level, abl_mask_, rcount_, rec_fp_,
-                             rec_lk_, newmask_, d_ctr_, ShardArgs{});
+                             rec_lk_, newmask_, d_ctr_, claim_args_);
         });
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
@@ -982,6 +984,7 @@ class EngineT final : public EngineBase {
   unsigned long long* d_ntrace_ = nullptr;
 
   Flags flags_{};
+  ShardArgs claim_args_{};
   bool queued_ = false;
   std::unique_ptr<SegQueue> q_;
   uint32_t* h_last_ = nullptr;       // pinned: a chunk's last offset and mask

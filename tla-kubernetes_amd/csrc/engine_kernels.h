@@ -176,11 +176,29 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
 // representative is marked in repmask and counted per owner for the record
 // exchange.  Claim keys carry the rank above the parent index.
 constexpr int CLAIM_RANK_SHIFT = 40;
+constexpr uint32_t CLAIM_SPREAD = 768;   // k_claim tile-order columns (spread_tile)
 struct ShardArgs {
   uint32_t world = 1, rank = 0;
+  uint32_t spread = CLAIM_SPREAD; // tile order strided by `spread` (spread_tile); 0 = block order
   uint32_t* repmask = nullptr;   // [n]: remote representatives of each parent
   uint32_t* cnt = nullptr;       // [world][n]: remote representatives per owner and parent
 };
+// Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
+// workgroups resident together (~1,536: 6 per CU) work on tiles spread over
+// the whole level, and each of the S columns of tiles is walked in order.
+// Same-level duplicates come mostly from neighbouring parents, i.e. from
+// neighbouring tiles; in block order those run at the same time and the
+// later key often claims first (a settle candidate, an atomicMax); spread,
+// tile t + 1 of a column runs after tile t, finds t's smaller claim and
+// loses at once.  NP=2: settle candidates 440M -> 110M per check, 171 ->
+// 157 ms (S = CLAIM_SPREAD = 768 measured best of 128..3072).  A bijection
+// of [0, G).
+__device__ __forceinline__ uint32_t spread_tile(uint32_t b, uint32_t G, uint32_t S) {
+  if (S == 0 || S >= G) return b;
+  const uint32_t x = b % S, k = b / S, g = G / S, rem = G % S;
+  return x * g + (x < rem ? x : rem) + k;
+}
+
 __device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
   return (uint32_t)__umul64hi(fp << 1, (uint64_t)world);
 }
@@ -226,7 +244,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   sh_cur[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
+  const uint32_t tile = spread_tile(blockIdx.x, gridDim.x, sh.spread);
+  const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
   const uint64_t i = tile0 + threadIdx.x;
   const bool live = i < n;
   unsigned probes = 0;
@@ -279,7 +298,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         if (r == CL_NEW)
           atomicOr(&sh_cur[threadIdx.x], 1u << t);
         else if (r == CL_CUR)
-          push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
+          push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
         else if (r == CL_FULL)
           atomicAdd(&C->overflow, 1ull);
       }
@@ -337,12 +356,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     if (r == CL_NEW)
       atomicOr(&sh_cur[lp], 1u << t);
     else if (r == CL_CUR)
-      push_candidate(&sh_rc, blockIdx.x, rec_fp, rec_lk, fp, lk);
+      push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk);
     else if (r == CL_FULL)
       atomicAdd(&C->overflow, 1ull);
   }
   __syncthreads();
-  if (threadIdx.x == 0) rcount[blockIdx.x] = sh_rc;
+  if (threadIdx.x == 0) rcount[tile] = sh_rc;
   if (live) newmask[i] = sh_cur[threadIdx.x];
   if (SH && live) {
     sh.repmask[i] = sh_rep[threadIdx.x];
