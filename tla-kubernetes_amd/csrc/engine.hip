@@ -327,6 +327,27 @@ class EngineT final : public EngineBase {
           scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)cn, st_);
         });
         KC_HIP_TRY(scan_err);
+        if (ablate_) {
+          // cut-down k_emit variants on scratch counters, before the real
+          // launch (which rewrites whatever they stored)
+          if (!d_ctr_abl_) KC_HIP_TRY(hipMalloc(&d_ctr_abl_, sizeof(Counters)));
+          KC_HIP_TRY(hipMemsetAsync(d_ctr_abl_, 0, sizeof(Counters), st_));
+          timed(KA_E1, [&] {
+            hipLaunchKernelGGL((k_emit<M, 1>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_abl_);
+          });
+          timed(KA_E2, [&] {
+            hipLaunchKernelGGL((k_emit<M, 2>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_abl_);
+          });
+          timed(KA_E3, [&] {
+            hipLaunchKernelGGL((k_emit<M, 3>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_abl_);
+          });
+        }
         timed(KK_EMIT, [&] {
           hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                              flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
@@ -381,10 +402,18 @@ class EngineT final : public EngineBase {
     last_level_ = res->nlevels;
     last_n_ = n;
     finish(res, t0, n);
-    if (ablate_)
-      fprintf(stderr, "kubecheck ablate: claim %.2f ms | successors+LDS %.2f ms | successors only %.2f ms | plan only %.2f ms | settle %.2f | emit %.2f ms\n",
+    if (ablate_) {
+      fprintf(stderr, "kubecheck ablate: claim %.2f ms | successors+LDS %.2f ms | successors only %.2f ms | plan only %.2f ms | settle %.2f | emit %.2f ms"
+              " | emit-no-plan %.2f | emit-no-plan-no-check %.2f | emit-parent-only %.2f\n",
               ktime_ms_[KK_EXPAND], ktime_ms_[KA_LDS], ktime_ms_[KA_COMPUTE], ktime_ms_[KA_PLAN], ktime_ms_[KK_RESOLVE],
-              ktime_ms_[KK_EMIT]);
+              ktime_ms_[KK_EMIT], ktime_ms_[KA_E1], ktime_ms_[KA_E2], ktime_ms_[KA_E3]);
+      KC_HIP_TRY(hipMemcpy(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost));
+      fprintf(stderr, "kubecheck claim outcomes (KC_DIAG builds): old %llu lost %llu cur %llu new %llu\n",
+              h_ctr_->claim_out(0), h_ctr_->claim_out(1), h_ctr_->claim_out(2), h_ctr_->claim_out(3));
+      fprintf(stderr, "kubecheck old-state level distance (KC_DIAG): 1:%llu 2:%llu 3:%llu 4:%llu 5-8:%llu 9-16:%llu 17+:%llu\n",
+              h_ctr_->old_dist(0), h_ctr_->old_dist(1), h_ctr_->old_dist(2), h_ctr_->old_dist(3), h_ctr_->old_dist(4),
+              h_ctr_->old_dist(5), h_ctr_->old_dist(6));
+    }
     return 0;
   }
 
@@ -629,7 +658,7 @@ class EngineT final : public EngineBase {
       ord_ = nullptr;
     }
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
-                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_})
+                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_last_) (void)hipHostFree(h_last_);
@@ -1002,6 +1031,7 @@ class EngineT final : public EngineBase {
   uint64_t par_cap_ = 0, ord_cap_ = 0;
   uint32_t *newmask_ = nullptr, *offsets_ = nullptr;
   uint32_t* abl_mask_ = nullptr;
+  Counters* d_ctr_abl_ = nullptr;   // KC_ABLATE: scratch counters of the k_emit variants
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
   uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;

@@ -27,7 +27,7 @@ namespace kc {
 // side (it cost k_settle_rec 4/5 of its time).  The host sums the rows.
 constexpr int CTR_STRIPES = 64;
 constexpr int OUTDEG_BINS = 16;
-struct CtrStripe {                  // 512 B
+struct CtrStripe {                  // 1 KiB
   unsigned long long act_gen[A_COUNT];
   unsigned long long act_dist[A_COUNT];
   unsigned long long probes;        // FPSet / ClaimSet probes
@@ -37,7 +37,11 @@ struct CtrStripe {                  // 512 B
   // a parent, histogram over the expanded parents (bin OUTDEG_BINS-1 = that
   // many or more)
   unsigned long long outdeg[OUTDEG_BINS];
-  unsigned long long pad[64 - 2 * A_COUNT - 3 - OUTDEG_BINS];
+  // KC_DIAG builds only: k_claim ClaimSet outcomes (CL_OLD, CL_LOST, CL_CUR,
+  // CL_NEW) and CL_OLD outcomes by level distance (1, 2, 3, 4, 5-8, 9-16, 17+)
+  unsigned long long claim_out[4];
+  unsigned long long old_dist[8];
+  unsigned long long pad[128 - 2 * A_COUNT - 15 - OUTDEG_BINS];
 };
 struct Counters {
   unsigned long long err_key;     // min error key of the level (~0 = none)
@@ -57,6 +61,16 @@ struct Counters {
   unsigned long long outdeg(int b) const {
     unsigned long long t = 0;
     for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].outdeg[b];
+    return t;
+  }
+  unsigned long long claim_out(int r) const {
+    unsigned long long t = 0;
+    for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].claim_out[r];
+    return t;
+  }
+  unsigned long long old_dist(int b) const {
+    unsigned long long t = 0;
+    for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].old_dist[b];
     return t;
   }
 
@@ -245,6 +259,25 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t tile = spread_tile(blockIdx.x, gridDim.x, sh.spread);
+#ifdef KC_DIAG
+  // diagnostic builds: ClaimSet outcomes (16-bit counts per ClaimResult 0..3
+  // per lane) and the level distance of CL_OLD hits (one extra probe each)
+  uint64_t outc = 0;
+  __shared__ unsigned int sh_odist[8];
+  if (threadIdx.x < 8) sh_odist[threadIdx.x] = 0;
+  __syncthreads();
+#define KC_DIAG_OUT(r)                                                                        \
+  do {                                                                                        \
+    outc += (r) < 4 ? 1ull << (16 * (r)) : 0ull;                                              \
+    if ((r) == CL_OLD) {                                                                      \
+      const uint32_t lv = (uint32_t)((~claimset_get(cs, nbuckets, fp)) >> CLAIM_KEY_BITS);   \
+      const uint32_t d = level - lv;                                                          \
+      atomicAdd(&sh_odist[d <= 4 ? (d ? d - 1 : 7) : d <= 8 ? 4 : d <= 16 ? 5 : 6], 1u);       \
+    }                                                                                         \
+  } while (0)
+#else
+#define KC_DIAG_OUT(r) ((void)0)
+#endif
   const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
   const uint64_t i = tile0 + threadIdx.x;
   const bool live = i < n;
@@ -295,6 +328,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         }
         ++probes;
         const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | (uint64_t)t), level);
+        KC_DIAG_OUT(r);
         if (r == CL_NEW)
           atomicOr(&sh_cur[threadIdx.x], 1u << t);
         else if (r == CL_CUR)
@@ -353,6 +387,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     ++probes;
     const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level);
+    KC_DIAG_OUT(r);
     if (r == CL_NEW)
       atomicOr(&sh_cur[lp], 1u << t);
     else if (r == CL_CUR)
@@ -374,6 +409,19 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+#ifdef KC_DIAG
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    unsigned long long v = (outc >> (16 * r)) & 0xffffull;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&stripe(C).claim_out[r], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && sh_odist[threadIdx.x])
+    atomicAdd(&stripe(C).old_dist[threadIdx.x], (unsigned long long)sh_odist[threadIdx.x]);
+#endif
+#undef KC_DIAG_OUT
 }
 
 // A claim displaced the stored ~prev in settle pass A: clear the displaced
@@ -446,7 +494,11 @@ struct NewCount {
   }
 };
 
-template <class M>
+// ABL (diagnostic builds of the same kernel, KC_ABLATE=1, on scratch
+// counters): 1 = no plan of the new state (the next level's candidate
+// count), 2 = also no invariant check, 3 = also no successor rebuild and no
+// state store (parent pointers only).
+template <class M, int ABL = 0>
 __global__ void __launch_bounds__(256)
 k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
        const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
@@ -501,23 +553,26 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
     const int t = __ffs(m) - 1;
     const uint64_t pi = wave0 + (uint64_t)p;
     const uint64_t pidx = base + pi;
+    const uint64_t o = C->chunk_base + obase + (uint64_t)g;
+    if (keep_trace) {
+      parent[next_gidx + o] = level_gidx + pidx;
+      ord[next_gidx + o] = (uint8_t)t;
+    }
+    if (ABL >= 3) continue;
     const typename M::State s = load_state<M>(cur, pi);
     const typename M::Plan pl{pc, 0, -1, -1};
     int slot, j;
     M::locate(pl, t, slot, j);
     typename M::State x;
     M::apply(s, slot, j, f, x);
-    const uint64_t o = C->chunk_base + obase + (uint64_t)g;
     store_state<M>(next, o - next_base, x);   // next_base: the StateQueue run starts at o = next_base
-    if (keep_trace) {
-      parent[next_gidx + o] = level_gidx + pidx;
-      ord[next_gidx + o] = (uint8_t)t;
-    }
-    if (M::check(x, f.inv_mask) >= 0)
+    if (ABL < 2 && M::check(x, f.inv_mask) >= 0)
       atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
     atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
-    const typename M::Plan px = M::plan(x, f);
-    cand += (unsigned long long)px.total;
+    if (ABL == 0) {
+      const typename M::Plan px = M::plan(x, f);
+      cand += (unsigned long long)px.total;
+    }
   }
   // wave reduction of the candidate count, then one LDS atomic per wave
 #pragma unroll
