@@ -39,18 +39,38 @@ const char* kActionNames[A_COUNT] = {
 
 }  // namespace
 
-// chunk_base += (last exclusive offset + last count); cand_total = sum of the
-// next_cand stripes (one 64-lane wave, one stripe per lane)
+// chunk_base += the chunk's new states (last exclusive offset + last count,
+// or the tile scan's total tile_off[tiles]); cand_total = sum of the
+// next_cand stripes (one 64-lane wave, one stripe per lane).  host != nullptr
+// (the level's last chunk): the level's head goes straight into pinned host
+// memory and the device head is reset for the next level (no copy launch,
+// no separate reset launch).
 __global__ void __launch_bounds__(64)
 k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask, uint64_t n,
-          Counters* __restrict__ C) {
+          Counters* __restrict__ C, const uint32_t* __restrict__ tile_off, uint64_t tiles,
+          unsigned long long* __restrict__ host) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
   unsigned long long v = C->s[threadIdx.x].next_cand;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   if (threadIdx.x == 0) {
     C->cand_total = v;
-    if (n > 0) C->chunk_base += (unsigned long long)offsets[n - 1] + NewCount()(newmask[n - 1]);
+    if (tile_off)
+      C->chunk_base += tile_off[tiles];
+    else if (n > 0)
+      C->chunk_base += (unsigned long long)offsets[n - 1] + NewCount()(newmask[n - 1]);
+    if (host) {
+      host[0] = C->err_key;
+      host[1] = C->chunk_base;
+      host[2] = C->overflow;
+      host[3] = C->batch_used;
+      host[4] = C->cand_total;
+      host[5] = C->level_new;
+      C->err_key = ~0ull;
+      C->chunk_base = 0;
+      C->overflow = 0;
+      C->batch_used = 0;
+    }
   }
 }
 
@@ -107,6 +127,12 @@ class EngineT final : public EngineBase {
     if (queued_) narrow_on_ = false;    // k_claim tile order (engine_kernels.h spread_tile; KC_TILE_SPREAD=0: block order)
     const char* sp = getenv("KC_TILE_SPREAD");
     if (sp) claim_args_.spread = (uint32_t)atoi(sp);
+    const char* ts = getenv("KC_TSCAN");
+    tscan_ = !(ts && ts[0] == '0');
+    const char* eo = getenv("KC_EMIT_OCC");
+    if (eo) emit_occ_ = atoi(eo);
+    const char* hc = getenv("KC_HEADCOPY");
+    headcopy_ = hc && hc[0] == '1';
   }
   ~EngineT() override { release(); }
 
@@ -278,6 +304,10 @@ class EngineT final : public EngineBase {
       {
         const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
         KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
+        if (tscan_) {
+          KC_TRY(grow_buffer(ttot_, ttot_cap_, tiles + 4, false, st_));
+          KC_TRY(grow_buffer(toff_, toff_cap_, tiles + 4, false, st_));
+        }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
       }
@@ -316,8 +346,14 @@ class EngineT final : public EngineBase {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                             tscan_ ? ttot_ : (uint32_t*)nullptr);
         });
+        if (tscan_) {
+          timed(KK_SCAN, [&] {
+            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_);
+          });
+        } else {
         size_t tmp_bytes = 0;
         const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
         KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)cn, st_));
@@ -327,6 +363,8 @@ class EngineT final : public EngineBase {
           scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)cn, st_);
         });
         KC_HIP_TRY(scan_err);
+        }
+        const uint32_t* toff = tscan_ ? toff_ : nullptr;
         if (ablate_) {
           // cut-down k_emit variants on scratch counters, before the real
           // launch (which rewrites whatever they stored)
@@ -335,29 +373,43 @@ class EngineT final : public EngineBase {
           timed(KA_E1, [&] {
             hipLaunchKernelGGL((k_emit<M, 1>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                               cfg_.keep_trace, d_ctr_abl_);
+                               cfg_.keep_trace, d_ctr_abl_, toff);
           });
           timed(KA_E2, [&] {
             hipLaunchKernelGGL((k_emit<M, 2>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                               cfg_.keep_trace, d_ctr_abl_);
+                               cfg_.keep_trace, d_ctr_abl_, toff);
           });
           timed(KA_E3, [&] {
             hipLaunchKernelGGL((k_emit<M, 3>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                               cfg_.keep_trace, d_ctr_abl_);
+                               cfg_.keep_trace, d_ctr_abl_, toff);
           });
         }
         timed(KK_EMIT, [&] {
-          hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
-                             flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                             cfg_.keep_trace, d_ctr_);
+          if (emit_occ_ == 7)
+            hipLaunchKernelGGL((k_emit_occ<M, 7>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_, toff);
+          else if (emit_occ_ == 6)
+            hipLaunchKernelGGL((k_emit_occ<M, 6>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_, toff);
+          else
+            hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
+                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
+                               cfg_.keep_trace, d_ctr_, toff);
         });
-        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_);
+        const bool last = start + cn >= n;
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_,
+                           tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)tiles,
+                           last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr);
       }
       KC_HIP_TRY(hipGetLastError());
-      KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
-      hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);   // next level's head
+      if (headcopy_) {
+        KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+        hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);   // next level's head
+      }
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
@@ -658,7 +710,7 @@ class EngineT final : public EngineBase {
       ord_ = nullptr;
     }
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
-                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_})
+                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_last_) (void)hipHostFree(h_last_);
@@ -817,6 +869,10 @@ class EngineT final : public EngineBase {
       {
         const uint64_t tiles = (cmax + CLAIM_TILE - 1) / CLAIM_TILE;
         KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
+        if (tscan_) {
+          KC_TRY(grow_buffer(ttot_, ttot_cap_, tiles + 4, false, st_));
+          KC_TRY(grow_buffer(toff_, toff_cap_, tiles + 4, false, st_));
+        }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
       }
@@ -895,7 +951,8 @@ class EngineT final : public EngineBase {
                              flags_, newmask_, offsets_, reinterpret_cast<State*>(dst), level_new, level_gidx,
                              next_gidx, parent_, ord_, cfg_.keep_trace, d_ctr_);
         });
-        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_);
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_,
+                           (const uint32_t*)nullptr, (uint64_t)0, (unsigned long long*)nullptr);
         KC_HIP_TRY(hipGetLastError());
         if (nn) KC_TRY(q_->commit(nn, st_));
         level_new += nn;
@@ -1032,6 +1089,16 @@ class EngineT final : public EngineBase {
   uint32_t *newmask_ = nullptr, *offsets_ = nullptr;
   uint32_t* abl_mask_ = nullptr;
   Counters* d_ctr_abl_ = nullptr;   // KC_ABLATE: scratch counters of the k_emit variants
+  // Default: settle pass B counts each tile's new states and one workgroup
+  // scans the tile counts (k_tile_scan); KC_TSCAN=0: the per-parent hipcub
+  // scan instead.  KC_HEADCOPY=1: the level head read back by a copy launch
+  // plus a reset launch instead of k_advance's direct write.  (Same-box A/B,
+  // NP=2 with events on every kernel: 165.7 ms both off, 163.9 direct head,
+  // 162.5 both on; profiles/r02o_ab1.txt.)
+  bool tscan_ = false, headcopy_ = false;
+  int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
+  uint32_t *ttot_ = nullptr, *toff_ = nullptr;
+  uint64_t ttot_cap_ = 0, toff_cap_ = 0;
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
   uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;

@@ -455,15 +455,26 @@ __device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_
 // to this chunk: earlier chunks' claims are smaller and final.  Sharded: a
 // displaced claim of another rank (a received record's) has no bit here;
 // records re-read their claims themselves (shard.hip).
+//
+// PASS 1 with tile_total (the engine's default): also the tile's new-state count
+// (popcount of its newmask words after pass A, plus this pass's winners),
+// the input of k_tile_scan.
 template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
              uint32_t level, const unsigned int* __restrict__ rcount,
              const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank) {
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ tile_total = nullptr) {
+  __shared__ unsigned int sh_tot[CLAIM_TILE / 64];
   const unsigned int cnt = rcount[blockIdx.x];
   const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
-  unsigned reads = 0;
+  unsigned reads = 0, newc = 0;
+  if (PASS == 1 && tile_total) {
+    // read before any of this pass's bit sets (the barrier orders them)
+    if (tile0 + threadIdx.x < n) newc = (unsigned)__builtin_popcount(newmask[tile0 + threadIdx.x]);
+    __syncthreads();
+  }
   for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
     const uint64_t r = (uint64_t)blockIdx.x * CLAIM_RCAP + k;
     const unsigned int lk = rec_lk[r];
@@ -478,13 +489,92 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
       if (prev < ~claim)                         // displaced ~prev (or found no claim)
         settle_displace(prev, level, rank, base, n, newmask, C, &rec_lk[r], lk | CAND_DISPLACER);
     } else if (~claimset_get(cs, nbuckets, fp) == claim) {
-      atomicOr(&newmask[tile0 + lp], 1u << t);
+      atomicOr(&newmask[tile0 + lp], 1u << t);   // a candidate's bit is never set before
+      ++newc;
     }
   }
   unsigned long long rw = reads;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
   if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
+  if (PASS == 1 && tile_total) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) newc += __shfl_down(newc, off, 64);
+    if ((threadIdx.x & 63) == 0) sh_tot[threadIdx.x >> 6] = newc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int t = 0;
+#pragma unroll
+      for (int w = 0; w < CLAIM_TILE / 64; ++w) t += sh_tot[w];
+      tile_total[blockIdx.x] = t;
+    }
+  }
+}
+
+// Exclusive prefix sum of the tiles' new-state counts (engine default; one
+// workgroup): off[t] = sum of tot[0..t), off[T] = the chunk's total (a chunk
+// is at most 2^27 parents, so the totals fit u32).  Each thread takes a
+// contiguous run of 16-B groups (4 tiles); up to TS_REG groups per thread
+// (T <= 65,536 tiles) stay in registers, all their loads in flight at once.
+constexpr int TSCAN_THREADS = 1024;
+static __global__ void __launch_bounds__(TSCAN_THREADS)
+k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off) {
+  __shared__ unsigned int sh_w[TSCAN_THREADS / 64];
+  const uint32_t G = (T + 3) / 4, per = (G + TSCAN_THREADS - 1) / TSCAN_THREADS;
+  const uint32_t b = threadIdx.x * per, e = min(G, b + per);
+  const uint4* t4 = reinterpret_cast<const uint4*>(tot);
+  auto grp = [&](uint32_t g) {                    // tiles >= T read as 0
+    uint4 v = t4[g];
+    const uint32_t k = 4 * g;
+    if (k + 1 >= T) v.y = 0;
+    if (k + 2 >= T) v.z = 0;
+    if (k + 3 >= T) v.w = 0;
+    return v;
+  };
+  constexpr uint32_t TS_REG = 16;
+  const bool inreg = per <= TS_REG;
+  uint4 rv[TS_REG];
+  unsigned int sum = 0;
+  if (inreg) {
+#pragma unroll
+    for (uint32_t j = 0; j < TS_REG; ++j) rv[j] = b + j < e ? grp(b + j) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < TS_REG; ++j) sum += rv[j].x + rv[j].y + rv[j].z + rv[j].w;
+  } else {
+    for (uint32_t g = b; g < e; ++g) {
+      const uint4 v = grp(g);
+      sum += v.x + v.y + v.z + v.w;
+    }
+  }
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  unsigned int incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) sh_w[wv] = incl;
+  __syncthreads();
+  unsigned int run = incl - sum;
+  for (int w = 0; w < wv; ++w) run += sh_w[w];
+  uint4* o4 = reinterpret_cast<uint4*>(off);
+  auto put = [&](uint32_t g, const uint4& v) {
+    uint4 r;
+    r.x = run;
+    r.y = run + v.x;
+    r.z = r.y + v.y;
+    r.w = r.z + v.z;
+    run = r.w + v.w;
+    o4[g] = r;
+  };
+  if (inreg) {
+#pragma unroll
+    for (uint32_t j = 0; j < TS_REG; ++j)
+      if (b + j < e) put(b + j, rv[j]);
+  } else {
+    for (uint32_t g = b; g < e; ++g) put(g, grp(g));
+  }
+  if (threadIdx.x == TSCAN_THREADS - 1) off[T] = run;
 }
 
 // popcount(newmask): the scan's input (new states per parent)
@@ -498,16 +588,18 @@ struct NewCount {
 // counters): 1 = no plan of the new state (the next level's candidate
 // count), 2 = also no invariant check, 3 = also no successor rebuild and no
 // state store (parent pointers only).
-template <class M, int ABL = 0>
-__global__ void __launch_bounds__(256)
-k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+template <class M, int ABL>
+__device__ __forceinline__ void emit_body(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
        const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
        typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
        unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
-       Counters* __restrict__ C) {
+       Counters* __restrict__ C, const uint32_t* __restrict__ tile_off) {
+  // offsets: per-parent exclusive offsets; or (tile_off != nullptr) per
+  // 256-parent block, the wave bases then come from the block's own counts
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_deg[OUTDEG_BINS];
   __shared__ unsigned long long sh_cand;
+  __shared__ unsigned int sh_wtot[4];
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh_cand = 0;
@@ -535,7 +627,14 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   }
   const int wtot = __shfl(incl, 63, 64);
   const int excl = incl - cnt;
-  if (wtot) obase = __shfl(i < n ? offsets[i] - (uint32_t)excl : 0u, 0, 64);
+  if (tile_off) {
+    if (lane == 0) sh_wtot[threadIdx.x >> 6] = (unsigned int)wtot;
+    __syncthreads();
+    obase = tile_off[blockIdx.x];
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) obase += sh_wtot[w];
+  } else if (wtot) {
+    obase = __shfl(i < n ? offsets[i] - (uint32_t)excl : 0u, 0, 64);
+  }
   const uint64_t wave0 = i - (uint64_t)lane;
   for (int r = 0; r < wtot; r += 64) {
     const int g = r + lane;
@@ -584,6 +683,30 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
     atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
+}
+
+// Pinned to 8 waves per SIMD (64 VGPRs; unpinned it took 68 = 7 waves):
+// NP=2 emit 31.6 -> 28.7 ms on the same box (profiles/r02o_ab2.txt).
+template <class M, int ABL = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+       const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
+       typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
+       unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
+       Counters* __restrict__ C, const uint32_t* __restrict__ tile_off = nullptr) {
+  emit_body<M, ABL>(cur, n, base, f, newmask, offsets, next, next_base, level_gidx, next_gidx, parent, ord,
+                    keep_trace, C, tile_off);
+}
+// the same pinned to OCC waves per SIMD instead (KC_EMIT_OCC=6|7; A/B)
+template <class M, int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
+k_emit_occ(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
+           const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
+           typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
+           unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
+           Counters* __restrict__ C, const uint32_t* __restrict__ tile_off) {
+  emit_body<M, 0>(cur, n, base, f, newmask, offsets, next, next_base, level_gidx, next_gidx, parent, ord,
+                  keep_trace, C, tile_off);
 }
 
 }  // namespace kc
