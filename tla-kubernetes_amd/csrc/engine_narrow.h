@@ -339,6 +339,7 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   // emitted states staged for the expansion of level L + 1
   __shared__ State sh_xs[NX_LDS];
   __shared__ unsigned long long sh_xc[NX_LDS];
+  __shared__ unsigned long long sh_xf[NX_LDS];   // fp_fold of each staged state (its tasks share it)
   __shared__ unsigned int sh_xo[NX_LDS], sh_xt[NX_LDS], sh_xoff[NX_LDS];
   __shared__ unsigned int sh_nx, sh_ntask, sh_last;
   __shared__ State sh_ps[NARROW_THREADS / NARROW_ESUB];
@@ -455,8 +456,15 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   unsigned long long cnd = 0;
   // the workgroup's new states dealt out one per lane (r = rank in the
   // workgroup, in (parent, t) order): no lane runs more than ceil(wtot/256)
-  // of the emit + expand chains
-  for (unsigned int r = threadIdx.x; r < wtot; r += NARROW_THREADS) {
+  // of the emit + expand chains.  When they fit half the workgroup (most
+  // narrow levels), each state is rebuilt by two lanes in different waves:
+  // waves 0-1 store it and check its invariants, waves 2-3 plan and stage
+  // its expansion, so the two halves of the chain run side by side on
+  // different SIMDs (a level's time is one lane's chain).
+  const bool split = wtot <= (unsigned int)NARROW_THREADS / 2;
+  const int part = split ? (threadIdx.x < (unsigned int)NARROW_THREADS / 2 ? 1 : 2) : 0;   // 0: both
+  const unsigned int rstep = split ? NARROW_THREADS / 2 : NARROW_THREADS;
+  for (unsigned int r = split ? threadIdx.x % (NARROW_THREADS / 2) : threadIdx.x; r < wtot; r += rstep) {
     State* __restrict__ nxt = (lev & 1) ? bufA : bufB;
     const uint64_t next_gidx = level_gidx + n;
     unsigned int lo = 0, hi = WP - 1;               // first parent whose inclusive offset > r
@@ -477,14 +485,17 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
       M::locate(ppl, t, slot, j);
       State x;
       M::apply(sp, slot, j, f, x);
-      store_state<M>(nxt, o, x);
-      if (keep_trace) {
-        parent[next_gidx + o] = level_gidx + i;
-        ord[next_gidx + o] = (uint8_t)t;
+      if (part != 2) {
+        store_state<M>(nxt, o, x);
+        if (keep_trace) {
+          parent[next_gidx + o] = level_gidx + i;
+          ord[next_gidx + o] = (uint8_t)t;
+        }
+        if (M::check(x, f.inv_mask) >= 0)
+          atomicMin(&ctl->err[pq], (i << 16) | ((uint64_t)t << 8) | E_INVARIANT);
+        atomicAdd(&sh_dist[M::slot_action(sp, slot)], 1u);
       }
-      if (M::check(x, f.inv_mask) >= 0)
-        atomicMin(&ctl->err[pq], (i << 16) | ((uint64_t)t << 8) | E_INVARIANT);
-      atomicAdd(&sh_dist[M::slot_action(sp, slot)], 1u);
+      if (part == 1) continue;
       // expand x for level L + 1 while it is in registers: its errors,
       // per-action counts and its successors' table entries (key: its index
       // o in level L + 1) are level L + 1's, kept only if that level runs
@@ -512,6 +523,7 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
         if (xs < NX_LDS) {
           sh_xs[xs] = x;
           sh_xc[xs] = px.counts;
+          sh_xf[xs] = M::fp_fold(x);
           sh_xo[xs] = (unsigned int)o;
           sh_xt[xs] = (unsigned int)tx;
         } else if (!lt_enter_succ<M>(lt_next, sc->hidx[qq], x, px, tx, (unsigned int)o, f)) {   // LDS full: this lane
@@ -577,7 +589,7 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
           M::locate(pxx, t, sl2, j2);
           State y;
           M::apply(xx, sl2, j2, f, y, who2);
-          fpx[q] = M::fingerprint_succ(xx, M::fp_fold(xx), y, who2);
+          fpx[q] = M::fingerprint_succ(xx, sh_xf[lo], y, who2);
           kx[q] = (sh_xo[lo] << 5) | (unsigned int)t;
         }
       }
