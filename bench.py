@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--fp-load", type=float, default=0.5, choices=[0.5, 0.75],
                     help="fpset workload: table load after the inserts")
     ap.add_argument("--sharded", action="store_true",
-                    help="use the sharded (multi-GPU) stages even at N=1 (run under torch.distributed.run)")
+                    help="use the sharded (multi-GPU) stages even at N=1 (started under torch.distributed.run)")
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks (gloo, no GPU) and report what each saw: a CPU test of "
                          "the --gpus N self-launch")
@@ -344,7 +344,8 @@ def bench_fpset(args):
 
 
 def relaunch(args) -> int:
-    """`python bench.py --gpus N` without a torch.distributed launcher: start
+    """`python bench.py --gpus N` (or `--sharded` at N=1) without a
+    torch.distributed launcher: start
     N ranks under torch.distributed.run as a CHILD process (nothing here has
     touched the GPU; no exec) and return its exit code."""
     import socket
@@ -383,17 +384,29 @@ def golden_check(workload: str, res: dict) -> str:
     return src
 
 
+def _json_stdout():
+    """The bench's one JSON line goes to the original stdout; everything else
+    written to file descriptor 1 from here on (RCCL prints its version banner
+    there at communicator init, in every rank) goes to stderr, so stdout
+    carries exactly one line."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.sharded) and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
+    jout = _json_stdout()
     if args.gpus != world and world != 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.launcher_check:
         out = launcher_check(args)
         if out is not None:
-            print(json.dumps(out), flush=True)
+            print(json.dumps(out), file=jout, flush=True)
         return
     if args.workload == "fpset":
         if args.gpus > 1 or args.sharded:
@@ -416,7 +429,7 @@ def main():
             out = bench_single(args, kw, desc)
         if args.gpus == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=jout, flush=True)
 
 
 if __name__ == "__main__":
