@@ -116,13 +116,41 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
 }
 
 // Records per owner from the owner-major exclusive scan of cnt[world][n].
+// Owner totals (world > 1; 0 at world 1) into tot and straight into pinned
+// host memory, with the level head (error key, overflow flags): what the
+// host reads after expand, with no copy launches.
+__device__ __forceinline__ void head_to_host(const Counters* __restrict__ C, unsigned long long* __restrict__ h) {
+  h[0] = C->err_key;
+  h[1] = C->chunk_base;
+  h[2] = C->overflow;
+  h[3] = C->batch_used;
+  h[4] = C->cand_total;
+  h[5] = C->level_new;
+}
+// Level head reset at the start of expand (one launch instead of two fills).
+__global__ void k_head_reset(Counters* __restrict__ C) {
+  if (threadIdx.x == 0) {
+    C->err_key = ~0ull;
+    C->chunk_base = 0;
+    C->overflow = 0;
+    C->batch_used = 0;
+  }
+}
 __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
-                               uint64_t n, uint32_t world, uint64_t* __restrict__ tot) {
+                               uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
+                               const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                               unsigned long long* __restrict__ host_head) {
   const uint32_t o = threadIdx.x;
-  if (o >= world) return;
-  const uint64_t end = (o + 1 < world) ? (uint64_t)off[(uint64_t)(o + 1) * n]
-                                       : (uint64_t)off[(uint64_t)world * n - 1] + cnt[(uint64_t)world * n - 1];
-  tot[o] = end - off[(uint64_t)o * n];
+  if (o == 0) head_to_host(C, host_head);
+  if (o >= 16) return;
+  uint64_t v = 0;
+  if (world > 1 && o < world) {
+    const uint64_t end = (o + 1 < world) ? (uint64_t)off[(uint64_t)(o + 1) * n]
+                                         : (uint64_t)off[(uint64_t)world * n - 1] + cnt[(uint64_t)world * n - 1];
+    v = end - off[(uint64_t)o * n];
+  }
+  tot[o] = v;
+  host_tot[o] = v;
 }
 
 // Record flags: 0 = out, 1 = candidate, 2 = inserted its fp, 3 = displacer.
@@ -192,12 +220,17 @@ __global__ void k_shard_base(const uint32_t* __restrict__ offsets, const uint32_
 }
 
 // cand_total = sum of the next_cand stripes (one lane per stripe)
-__global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C) {
+// (then the level head straight into pinned host memory, host_head)
+__global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C,
+                                                   unsigned long long* __restrict__ host_head) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
   unsigned long long v = C->s[threadIdx.x].next_cand;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  if (threadIdx.x == 0) C->cand_total = v;
+  if (threadIdx.x == 0) {
+    C->cand_total = v;
+    head_to_host(C, host_head);
+  }
 }
 
 // The winners among this rank's own successors (newmask), in parent order.
@@ -386,8 +419,7 @@ class ShardT final : public ShardBase {
   // Claims this rank's own successors of the level; counts the rest per owner.
   int expand(uint64_t* counts, uint64_t* err_key) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
-    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
-    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->chunk_base, 0, 3 * 8, st_));
+    hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
     for (int o = 0; o < world_; ++o) counts[o] = 0;
     send_total_ = 0;
     *err_key = init_err_;
@@ -440,14 +472,10 @@ class ShardT final : public ShardBase {
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
       KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
-      hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
-                         d_owner_base_);
-    } else {
-      KC_HIP_TRY(hipMemsetAsync(d_owner_base_, 0, 16 * sizeof(uint64_t), st_));
     }
+    hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
+                       d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_));
     KC_HIP_TRY(hipGetLastError());
-    KC_HIP_TRY(hipMemcpyAsync(h_owner_base_, d_owner_base_, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, st_));
-    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
     if (cfg_.timing) {
       float ms = 0;
@@ -612,9 +640,9 @@ class ShardT final : public ShardBase {
     if (n)
       hipLaunchKernelGGL(k_shard_emit_rec<M>, dim3(rgrid), dim3(256), 0, st_, in, n, isnew_, ioff_,
                          flags_, next_, pkeys_, next_gidx, d_ctr_);
-    hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_);
+    hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_,
+                       reinterpret_cast<unsigned long long*>(h_ctr_));
     KC_HIP_TRY(hipGetLastError());
-    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
     if (h_ctr_->overflow || h_ctr_->batch_used) {
       set_error("kc_shard_insert: table full or claim protocol violation");
