@@ -24,6 +24,8 @@
 // emulated ranks, and RCCL itself at world 1.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+
+#include <cstring>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -173,6 +175,7 @@ class RcclComm final : public Comm {
   }
   ~RcclComm() override {
     if (buf_) (void)hipFree(buf_);
+    if (hbuf_) (void)hipHostFree(hbuf_);
     if (comm_ && rccl()) (void)rccl()->comm_destroy(comm_);
   }
   int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
@@ -183,11 +186,12 @@ class RcclComm final : public Comm {
     const size_t L = rows[0].size(), R = (size_t)s_->world();
     KC_TRY(scratch(L * (R + 1)));
     hipStream_t st = s_->stream();
-    KC_HIP_TRY(hipMemcpyAsync(buf_, rows[0].data(), L * 8, hipMemcpyHostToDevice, st));
+    memcpy(hbuf_, rows[0].data(), L * 8);
+    KC_HIP_TRY(hipMemcpyAsync(buf_, hbuf_, L * 8, hipMemcpyHostToDevice, st));
     KC_NCCL_TRY(rccl()->all_gather(buf_, buf_ + L, L, ncclUint64, comm_, st));
-    out.resize(L * R);
-    KC_HIP_TRY(hipMemcpyAsync(out.data(), buf_ + L, L * R * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipMemcpyAsync(hbuf_ + L, buf_ + L, L * R * 8, hipMemcpyDeviceToHost, st));
     KC_HIP_TRY(hipStreamSynchronize(st));
+    out.assign(hbuf_ + L, hbuf_ + L + L * R);
     return 0;
   }
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
@@ -216,10 +220,12 @@ class RcclComm final : public Comm {
     if (trivial_) return 0;
     KC_TRY(scratch(1));
     hipStream_t st = s_->stream();
-    KC_HIP_TRY(hipMemcpyAsync(buf_, v, 8, hipMemcpyHostToDevice, st));
+    hbuf_[0] = *v;
+    KC_HIP_TRY(hipMemcpyAsync(buf_, hbuf_, 8, hipMemcpyHostToDevice, st));
     KC_NCCL_TRY(rccl()->broadcast(buf_, buf_, 1, ncclUint64, root, comm_, st));
-    KC_HIP_TRY(hipMemcpyAsync(v, buf_, 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipMemcpyAsync(hbuf_, buf_, 8, hipMemcpyDeviceToHost, st));
     KC_HIP_TRY(hipStreamSynchronize(st));
+    *v = hbuf_[0];
     return 0;
   }
   int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
@@ -230,27 +236,34 @@ class RcclComm final : public Comm {
     const size_t L = v[0].size();
     KC_TRY(scratch(L));
     hipStream_t st = s_->stream();
-    KC_HIP_TRY(hipMemcpyAsync(buf_, v[0].data(), L * 8, hipMemcpyHostToDevice, st));
+    memcpy(hbuf_, v[0].data(), L * 8);
+    KC_HIP_TRY(hipMemcpyAsync(buf_, hbuf_, L * 8, hipMemcpyHostToDevice, st));
     KC_NCCL_TRY(rccl()->all_reduce(buf_, buf_, L, ncclUint64, ncclSum, comm_, st));
-    out.resize(L);
-    KC_HIP_TRY(hipMemcpyAsync(out.data(), buf_, L * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipMemcpyAsync(hbuf_, buf_, L * 8, hipMemcpyDeviceToHost, st));
     KC_HIP_TRY(hipStreamSynchronize(st));
+    out.assign(hbuf_, hbuf_ + L);
     return 0;
   }
 
  private:
+  // device scratch for the small collectives and a pinned host mirror, so
+  // their host <-> device copies are asynchronous DMA (no pageable staging)
   int scratch(size_t words) {
     if (words <= cap_) return 0;
     if (buf_) KC_HIP_TRY(hipFree(buf_));
+    if (hbuf_) KC_HIP_TRY(hipHostFree(hbuf_));
     buf_ = nullptr;
+    hbuf_ = nullptr;
     cap_ = std::max<size_t>(words, 256);
     KC_HIP_TRY(hipMalloc(&buf_, cap_ * 8));
+    KC_HIP_TRY(hipHostMalloc(&hbuf_, cap_ * 8));
     return 0;
   }
   ShardBase* s_;
   bool trivial_ = false;
   ncclComm_t comm_ = nullptr;
   uint64_t* buf_ = nullptr;
+  uint64_t* hbuf_ = nullptr;
   size_t cap_ = 0;
 };
 
