@@ -208,10 +208,24 @@ def test_native_enlarged_prefix(fixtures):
     assert r["act_gen"] == fx["act_gen"]
 
 
-def test_native_rccl_world1(fixtures, monkeypatch):
+@pytest.mark.parametrize("devrow", ["1", "0"])
+def test_native_rccl_world1(fixtures, monkeypatch, devrow):
     # the RCCL communicator path (one rank: every collective runs, nothing
-    # moves; KC_RCCL_FORCE=1 keeps the world-1 collectives on RCCL)
+    # moves; KC_RCCL_FORCE=1 keeps the world-1 collectives on RCCL), with the
+    # all-gather row written by the shard's kernels in device memory (the
+    # N-GPU default) and with host rows (KC_DEVROW=0)
     monkeypatch.setenv("KC_RCCL_FORCE", "1")
+    monkeypatch.setenv("KC_DEVROW", devrow)
+    for key, kw, kind in (("variant5", dict(variant=5), "invariant"),   # Init state: key 0x12
+                          ("ns0", dict(ns=0), "deadlock"),
+                          ("variant3", dict(variant=3), "assertion")):
+        mc = NativeShardedChecker(ModelConfig(**kw), 0, 1)
+        try:
+            r = mc.run()
+            assert r["error"] == kind
+            assert (r["error_level"], r["trace_len"]) == (fixtures[key]["err_level"], fixtures[key]["trace_len"])
+        finally:
+            mc.close()
     mc = NativeShardedChecker(ModelConfig(), 0, 1)
     try:
         r = mc.run()

@@ -19,6 +19,14 @@ class ShardBase {
   virtual int set_stream(hipStream_t st) = 0;
   virtual int init(uint64_t* n_local) = 0;
   virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
+  // expand() split around a device-side all-gather row (the native loop over
+  // RCCL): expand_dev enqueues the level's claims and writes d_row[0..world)
+  // = owner totals, d_row[world] = status_new, d_row[world + 1] = status_err
+  // (on level 1 an Init-state invariant key instead, as the loop would), with
+  // no host sync; expand_done, after the caller's stream sync, reports what
+  // expand() reports.
+  virtual int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) = 0;
+  virtual int expand_done(uint64_t* counts, uint64_t* err_key) = 0;
   virtual uint64_t record_bytes() const = 0;
   virtual int pack(void* send) = 0;
   virtual int insert(const void* recv, uint64_t n, uint64_t* n_new, uint64_t* err_key) = 0;

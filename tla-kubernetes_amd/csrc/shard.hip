@@ -136,21 +136,39 @@ __global__ void k_head_reset(Counters* __restrict__ C) {
     C->batch_used = 0;
   }
 }
+// row != nullptr (ShardBase::expand_dev): the all-gather row too, in device
+// memory: totals, status_new, status_err (level 1: an Init-state invariant
+// key, 0x12, found by expand takes the status slot, as Group::run does).
 __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                                uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
                                const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
-                               unsigned long long* __restrict__ host_head) {
+                               unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
+                               uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err,
+                               uint64_t rank) {
   const uint32_t o = threadIdx.x;
-  if (o == 0) head_to_host(C, host_head);
+  if (o == 0) {
+    head_to_host(C, host_head);
+    if (row) {
+      uint64_t se = status_err;
+      if (level1) {
+        uint64_t e = init_err;
+        if (C->err_key != ~0ull) e = min(e, (rank << 60) | (uint64_t)C->err_key);
+        if (e != ~0ull && (e & 0xFF) == 0x12) se = e;
+      }
+      row[world] = status_new;
+      row[world + 1] = se;
+    }
+  }
   if (o >= 16) return;
   uint64_t v = 0;
-  if (world > 1 && o < world) {
+  if (world > 1 && o < world && n > 0) {
     const uint64_t end = (o + 1 < world) ? (uint64_t)off[(uint64_t)(o + 1) * n]
                                          : (uint64_t)off[(uint64_t)world * n - 1] + cnt[(uint64_t)world * n - 1];
     v = end - off[(uint64_t)o * n];
   }
   tot[o] = v;
   host_tot[o] = v;
+  if (row && o < world) row[o] = v;
 }
 
 // Record flags: 0 = out, 1 = candidate, 2 = inserted its fp, 3 = displacer.
@@ -418,13 +436,28 @@ class ShardT final : public ShardBase {
 
   // Claims this rank's own successors of the level; counts the rest per owner.
   int expand(uint64_t* counts, uint64_t* err_key) override {
+    KC_TRY(expand_dev(0, ~0ull, false, nullptr));
+    if (!dev_empty_) KC_HIP_TRY(hipStreamSynchronize(st_));
+    return expand_done(counts, err_key);
+  }
+  int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
-    for (int o = 0; o < world_; ++o) counts[o] = 0;
     send_total_ = 0;
-    *err_key = init_err_;
+    dev_init_err_ = init_err_;
     init_err_ = ~0ull;
-    if (n_ == 0) return 0;
+    dev_empty_ = n_ == 0;
+    if (n_ == 0) {
+      // nothing to claim; a device row still gets its status words
+      if (d_row)
+        hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, (uint64_t)0, (uint32_t)world_,
+                           d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                           d_row, status_new, status_err, (int)level1, dev_init_err_, (uint64_t)rank_);
+      dev_empty_ = d_row == nullptr;
+      dev_zero_ = true;
+      return 0;
+    }
+    dev_zero_ = false;
     if (n_ >= (1ull << 32)) {
       set_error("kc_shard_expand: frontier wider than 2^32 states");
       return -ENOMEM;
@@ -474,9 +507,16 @@ class ShardT final : public ShardBase {
       KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
     }
     hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
-                       d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_));
+                       d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                       d_row, status_new, status_err, (int)level1, dev_init_err_, (uint64_t)rank_);
     KC_HIP_TRY(hipGetLastError());
-    KC_HIP_TRY(hipStreamSynchronize(st_));
+    return 0;
+  }
+  // after the stream sync that follows expand_dev
+  int expand_done(uint64_t* counts, uint64_t* err_key) override {
+    for (int o = 0; o < world_; ++o) counts[o] = 0;
+    *err_key = dev_init_err_;
+    if (dev_zero_) return 0;
     if (cfg_.timing) {
       float ms = 0;
       KC_HIP_TRY(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
@@ -750,6 +790,10 @@ class ShardT final : public ShardBase {
   uint64_t n_ = 0, next_n_ = 0, send_total_ = 0, gen_init_ = 0;
   uint64_t cand_ = 0, next_cand_ = 0, cand_total_ = 0;   // successors of the frontier
   uint64_t init_err_ = ~0ull;
+  // expand_dev -> expand_done: the Init-state key taken, nothing launched
+  // that needs a sync, no claims this level
+  uint64_t dev_init_err_ = ~0ull;
+  bool dev_empty_ = false, dev_zero_ = false;
   int level_ = 0;
   std::vector<uint64_t> level_base_;
   hipEvent_t ev_[2] = {nullptr, nullptr};

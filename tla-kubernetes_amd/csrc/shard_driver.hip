@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <rccl/rccl.h>
 
@@ -124,6 +125,17 @@ class Comm {
   virtual int broadcast(int root, uint64_t* v) = 0;
   // v[i] = the vector of local shard i; out = the element-wise sum over ranks
   virtual int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) = 0;
+  // Device-row all-gather (one local shard; RcclComm with real collectives):
+  // row_buffer(L) is where the shard's kernels write its row of L words;
+  // all_gather_dev gathers it on the shard's stream, syncs, and returns the
+  // rank-major rows.  nullptr: not supported, use all_gather.
+  virtual uint64_t* row_buffer(size_t L) { (void)L; return nullptr; }
+  virtual int all_gather_dev(size_t L, std::vector<uint64_t>& out) {
+    (void)L;
+    (void)out;
+    set_error("all_gather_dev: not supported by this communicator");
+    return -EINVAL;
+  }
 };
 
 class LocalComm final : public Comm {
@@ -188,6 +200,19 @@ class RcclComm final : public Comm {
     hipStream_t st = s_->stream();
     memcpy(hbuf_, rows[0].data(), L * 8);
     KC_HIP_TRY(hipMemcpyAsync(buf_, hbuf_, L * 8, hipMemcpyHostToDevice, st));
+    KC_NCCL_TRY(rccl()->all_gather(buf_, buf_ + L, L, ncclUint64, comm_, st));
+    KC_HIP_TRY(hipMemcpyAsync(hbuf_ + L, buf_ + L, L * R * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    out.assign(hbuf_ + L, hbuf_ + L + L * R);
+    return 0;
+  }
+  uint64_t* row_buffer(size_t L) override {
+    if (trivial_ || scratch(L * ((size_t)s_->world() + 1))) return nullptr;
+    return buf_;
+  }
+  int all_gather_dev(size_t L, std::vector<uint64_t>& out) override {
+    const size_t R = (size_t)s_->world();
+    hipStream_t st = s_->stream();
     KC_NCCL_TRY(rccl()->all_gather(buf_, buf_ + L, L, ncclUint64, comm_, st));
     KC_HIP_TRY(hipMemcpyAsync(hbuf_ + L, buf_ + L, L * R * 8, hipMemcpyDeviceToHost, st));
     KC_HIP_TRY(hipStreamSynchronize(st));
@@ -274,6 +299,8 @@ class Group {
  public:
   Group(std::vector<ShardBase*> local, std::unique_ptr<Comm> comm, const kc_model_config& cfg)
       : local_(std::move(local)), comm_(std::move(comm)), cfg_(cfg) {
+    const char* dr = getenv("KC_DEVROW");     // KC_DEVROW=0: host rows + expand's own sync (A/B)
+    dev_row_off_ = dr && dr[0] == '0';
     world_ = local_[0]->world();
     cfg_.spill_dir = nullptr;
     for (auto* s : local_) s->set_async_pack(true);
@@ -328,6 +355,7 @@ class Group {
   std::vector<std::vector<uint64_t>> trace_;
   std::vector<uint64_t> sent_local_;   // records each local shard sent to other ranks
   uint64_t sent_ = 0;                  // all ranks (after run)
+  bool dev_row_off_ = false;
 };
 
 int Group::run(kc_result* res) {
@@ -352,7 +380,22 @@ int Group::run(kc_result* res) {
   std::vector<std::vector<uint64_t>> Mx(R, std::vector<uint64_t>(R, 0));
   for (;;) {
     const bool last = cfg_.max_levels && level >= cfg_.max_levels;
-    for (size_t i = 0; i < nl; ++i) {
+    // one local shard over RCCL: its kernels write the all-gather row in
+    // device memory and the gather's sync is the level's first (expand has
+    // none of its own)
+    uint64_t* d_row = (nl == 1 && !last && !dev_row_off_) ? comm_->row_buffer((size_t)R + 2) : nullptr;
+    if (d_row) {
+      std::fill(counts[0].begin(), counts[0].end(), 0);
+      KC_HIP_TRY(hipSetDevice(local_[0]->device()));
+      KC_TRY(local_[0]->expand_dev(status_new[0], status_err[0], level == 1, d_row));
+      KC_TRY(comm_->all_gather_dev((size_t)R + 2, all));
+      KC_TRY(local_[0]->expand_done(counts[0].data(), &e1[0]));
+      if (level == 1 && e1[0] != NONE && (e1[0] & 0xFF) == 0x12) {
+        status_err[0] = e1[0];       // (k_owner_totals put it in the row already)
+        e1[0] = NONE;
+      }
+    }
+    for (size_t i = 0; i < nl && !d_row; ++i) {
       std::fill(counts[i].begin(), counts[i].end(), 0);
       e1[i] = NONE;
       if (!last) {
@@ -369,7 +412,7 @@ int Group::run(kc_result* res) {
       rows[i].push_back(status_new[i]);
       rows[i].push_back(status_err[i]);
     }
-    KC_TRY(comm_->all_gather(rows, all));
+    if (!d_row) KC_TRY(comm_->all_gather(rows, all));
     uint64_t total = 0;
     err = NONE;
     for (int r = 0; r < R; ++r) {
