@@ -66,6 +66,21 @@ def test_multi_chunk_and_rehash_paths(model1):
     assert r.fpset_slots > 64
 
 
+@pytest.mark.parametrize("env", [{"KC_TSCAN_REG": "0"}, {"KC_TSCAN": "0"}, {"KC_HEADCOPY": "1"}])
+def test_wide_level_variants(model1, monkeypatch, env):
+    # every level on the wide path (chunk_states turns the narrow kernel
+    # off) with: the tile scan's loop path (levels wider than 65,536 tiles
+    # take it; forced here), the per-parent hipcub scan, and the copy +
+    # reset read-back of the level head
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = run(chunk_states=1 << 20)
+    assert (r.distinct, r.generated, r.depth) == (model1.distinct, model1.generated, model1.depth)
+    assert r.level_width == model1.level_width
+    assert r.act_gen == model1.act_gen and r.act_dist == model1.act_dist
+    assert r.outdeg_hist == model1.outdeg_hist
+
+
 def test_seeded_assertion_bug_trace(fixtures):
     # NC=2 clients sharing Secret/foo: C4 Assert (KubeAPI.tla:639-640) fails at depth 10
     fx = fixtures["nc2"]

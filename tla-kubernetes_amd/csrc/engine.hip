@@ -129,6 +129,10 @@ class EngineT final : public EngineBase {
     if (sp) claim_args_.spread = (uint32_t)atoi(sp);
     const char* ts = getenv("KC_TSCAN");
     tscan_ = !(ts && ts[0] == '0');
+    const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
+    if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
+    const char* tr = getenv("KC_TSCAN_REG");
+    tscan_reg_ = !(tr && tr[0] == '0');
     const char* eo = getenv("KC_EMIT_OCC");
     if (eo) emit_occ_ = atoi(eo);
     const char* hc = getenv("KC_HEADCOPY");
@@ -351,7 +355,7 @@ class EngineT final : public EngineBase {
         });
         if (tscan_) {
           timed(KK_SCAN, [&] {
-            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_);
+            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
           });
         } else {
         size_t tmp_bytes = 0;
@@ -773,7 +777,7 @@ class EngineT final : public EngineBase {
                        cfg_.check_deadlock, 0u, d_ns_, d_nsc_, d_ctr_, d_ntrace_);
     for (;;) {
       timed(KK_NARROW, [&] {
-        for (int k = 0; k < NARROW_BATCH; ++k, ++lev)
+        for (int k = 0; k < narrow_batch_; ++k, ++lev)
           hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
                              cfg_.check_deadlock, parent_, ord_, cfg_.keep_trace, lev, d_ns_, d_nsc_, cs_.t,
                              cs_.nslots, d_ctr_, d_ntrace_);
@@ -1096,6 +1100,8 @@ class EngineT final : public EngineBase {
   // NP=2 with events on every kernel: 165.7 ms both off, 163.9 direct head,
   // 162.5 both on; profiles/r02o_ab1.txt.)
   bool tscan_ = false, headcopy_ = false;
+  int narrow_batch_ = NARROW_BATCH;
+  int tscan_reg_ = 1;   // KC_TSCAN_REG=0: k_tile_scan's loop path (levels > 65,536 tiles) at any width
   int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;
   uint64_t ttot_cap_ = 0, toff_cap_ = 0;

@@ -518,7 +518,7 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
 // (T <= 65,536 tiles) stay in registers, all their loads in flight at once.
 constexpr int TSCAN_THREADS = 1024;
 static __global__ void __launch_bounds__(TSCAN_THREADS)
-k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off) {
+k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off, int reg_ok) {
   __shared__ unsigned int sh_w[TSCAN_THREADS / 64];
   const uint32_t G = (T + 3) / 4, per = (G + TSCAN_THREADS - 1) / TSCAN_THREADS;
   const uint32_t b = threadIdx.x * per, e = min(G, b + per);
@@ -532,7 +532,7 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
     return v;
   };
   constexpr uint32_t TS_REG = 16;
-  const bool inreg = per <= TS_REG;
+  const bool inreg = reg_ok && per <= TS_REG;   // (reg_ok = 0: KC_TSCAN_REG=0, tests the loop path)
   uint4 rv[TS_REG];
   unsigned int sum = 0;
   if (inreg) {
