@@ -459,16 +459,17 @@ __device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_
 // PASS 1 with tile_total (the engine's default): also the tile's new-state count
 // (popcount of its newmask words after pass A, plus this pass's winners),
 // the input of k_tile_scan.
+// (The body takes the tile index, so the sharded insert can run it in one
+// launch with the records' settle pass.)
 template <int PASS>
-static __global__ void __launch_bounds__(CLAIM_TILE)
-k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
-             uint32_t level, const unsigned int* __restrict__ rcount,
-             const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
-             uint32_t* __restrict__ tile_total = nullptr) {
+__device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs,
+                                            uint64_t nbuckets, uint32_t level, const unsigned int* __restrict__ rcount,
+                                            const unsigned long long* __restrict__ rec_fp,
+                                            unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask,
+                                            Counters* __restrict__ C, uint32_t rank, uint32_t* __restrict__ tile_total) {
   __shared__ unsigned int sh_tot[CLAIM_TILE / 64];
-  const unsigned int cnt = rcount[blockIdx.x];
-  const uint64_t tile0 = (uint64_t)blockIdx.x * CLAIM_TILE;
+  const unsigned int cnt = rcount[tile];
+  const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
   unsigned reads = 0, newc = 0;
   if (PASS == 1 && tile_total) {
     // read before any of this pass's bit sets (the barrier orders them)
@@ -476,7 +477,7 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
     __syncthreads();
   }
   for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
-    const uint64_t r = (uint64_t)blockIdx.x * CLAIM_RCAP + k;
+    const uint64_t r = (uint64_t)tile * CLAIM_RCAP + k;
     const unsigned int lk = rec_lk[r];
     if (PASS == 1 && !(lk & CAND_DISPLACER)) continue;
     const unsigned long long fp = rec_fp[r];
@@ -506,9 +507,18 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
       unsigned int t = 0;
 #pragma unroll
       for (int w = 0; w < CLAIM_TILE / 64; ++w) t += sh_tot[w];
-      tile_total[blockIdx.x] = t;
+      tile_total[tile] = t;
     }
   }
+}
+template <int PASS>
+static __global__ void __launch_bounds__(CLAIM_TILE)
+k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+             uint32_t level, const unsigned int* __restrict__ rcount,
+             const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ tile_total = nullptr) {
+  settle_tile<PASS>(blockIdx.x, n, base, cs, nbuckets, level, rcount, rec_fp, rec_lk, newmask, C, rank, tile_total);
 }
 
 // Exclusive prefix sum of the tiles' new-state counts (engine default; one

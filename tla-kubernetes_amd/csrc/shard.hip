@@ -201,13 +201,12 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
 // newmask bit, the displacer is flagged); PASS 1: inserters and displacers
 // win iff the stored claim is still theirs.
 template <class M, int PASS>
-__global__ void __launch_bounds__(256)
-k_rec_settle(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
-             uint64_t nslots, uint32_t level, uint32_t rank,
-             const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
-             uint32_t* __restrict__ newmask, uint64_t nlocal, uint32_t* __restrict__ isnew,
-             Counters* __restrict__ C) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __restrict__ in, uint64_t n,
+                                           ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
+                                           uint32_t rank, const unsigned long long* __restrict__ rfp,
+                                           unsigned int* __restrict__ flag, uint32_t* __restrict__ newmask,
+                                           uint64_t nlocal, uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+  const uint64_t i = blk * 256 + threadIdx.x;
   if (i >= n) return;
   const unsigned int fl = flag[i];
   if (PASS == 0) {
@@ -223,6 +222,22 @@ k_rec_settle(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restric
     }
     isnew[i] = w;
   }
+}
+// One settle pass over this rank's own claim tiles (blocks [0, tiles)) and
+// the received records (the blocks after them), in one launch: the passes
+// of the two commute (atomicMax claims; a displaced candidate has no bit).
+template <class M, int PASS>
+__global__ void __launch_bounds__(256)
+k_settle_both(uint32_t tiles, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
+              uint32_t rank, const unsigned int* __restrict__ rcount, const unsigned long long* __restrict__ rec_fp,
+              unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask, const Record<M>* __restrict__ in,
+              uint64_t n, const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
+              uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+  static_assert(CLAIM_TILE == 256, "one block size for both halves");
+  if (blockIdx.x < tiles)
+    settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank, nullptr);
+  else
+    rec_settle<M, PASS>(blockIdx.x - tiles, in, n, cs, nslots, level, rank, rfp, flag, newmask, n_local, isnew, C);
 }
 
 // chunk_base = this rank's own new states (the records' emit base);
@@ -635,23 +650,16 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL(k_rec_claim<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
                          succ_level, rfp_, flag_, d_ctr_);
     }
-    // settle pass A (local tiles, records), then pass B
-    if (n_)
-      hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, n_, (uint64_t)0,
-                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_,
-                         (uint32_t)rank_);
-    if (n)
-      hipLaunchKernelGGL((k_rec_settle<M, 0>), dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t,
-                         cs_.nslots, succ_level, (uint32_t)rank_, rfp_, flag_, newmask_, n_, isnew_,
-                         d_ctr_);
-    if (n_)
-      hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, n_, (uint64_t)0,
-                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_,
-                         (uint32_t)rank_);
-    if (n)
-      hipLaunchKernelGGL((k_rec_settle<M, 1>), dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t,
-                         cs_.nslots, succ_level, (uint32_t)rank_, rfp_, flag_, newmask_, n_, isnew_,
-                         d_ctr_);
+    // settle pass A (local tiles and records in one launch), then pass B
+    const unsigned lt = n_ ? tiles : 0u, sgrid = lt + (n ? rgrid : 0u);
+    if (sgrid) {
+      hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
+                         succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
+                         isnew_, d_ctr_);
+      hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
+                         succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
+                         isnew_, d_ctr_);
+    }
     // positions: this rank's own winners first, then the records'
     size_t tmp_bytes = 0;
     if (n_) {
