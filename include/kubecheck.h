@@ -208,6 +208,16 @@ typedef struct {
   uint64_t frontier_segment_states;   /* 0 = 2^22 */
   const char *spill_dir;
   int trace_host;
+  /* Seen-set spill (single-GPU engine; TLC's OffHeapDiskFPSet role,
+   * MC.out:5).  seen_hbm_bytes > 0 caps the HBM the seen-set uses: a fixed
+   * hot ClaimSet (<= half of it), scratch, and the HBM directories and
+   * filters of the cold tier.  When the hot table fills, its fingerprints are
+   * flushed into sorted runs in pinned host RAM (up to seen_host_bytes,
+   * 0 = unlimited), then in files in spill_dir; every level's new states are
+   * checked against the runs on the GPU.  Results are identical to the
+   * unbounded seen-set's. */
+  uint64_t seen_hbm_bytes;
+  uint64_t seen_host_bytes;
 } kc_model_config;
 
 typedef struct {
@@ -237,6 +247,18 @@ typedef struct {
   uint64_t frontier_spilled_bytes;   /* frontier bytes written to host RAM or disk */
   uint64_t frontier_reloaded_bytes;  /* ... and read back into HBM */
   uint64_t frontier_peak_hbm_bytes;  /* peak HBM held by the frontier queue */
+  /* seen-set spill (cfg.seen_hbm_bytes > 0) */
+  uint64_t seen_flushes;        /* hot-table flushes into the cold tier */
+  uint64_t seen_cold_fps;       /* fingerprints in cold runs at the end */
+  uint64_t seen_cold_runs;      /* cold runs at the end (host + disk) */
+  uint64_t seen_cold_queries;   /* new-to-the-hot-table fingerprints checked against the cold tier */
+  uint64_t seen_cold_hits;      /* ... found there (states already seen) */
+  uint64_t seen_merges;         /* run merges */
+  uint64_t seen_filter_tests;   /* (query, run) pairs tested by a run's Bloom filter */
+  uint64_t seen_filter_passed;  /* ... that the filter let through to the run */
+  uint64_t seen_disk_bytes;     /* cold-run bytes written to spill files */
+  uint64_t seen_peak_hbm_bytes; /* peak HBM of the seen-set (hot table + scratch + cold metadata) */
+  double seen_seconds;          /* host wall time in chunk planning, flushes and cold checks */
 } kc_result;
 
 typedef struct kc_engine kc_engine;
@@ -345,6 +367,16 @@ int kc_group_run(kc_group *g, kc_result *res);
 int kc_group_trace_tuple(kc_group *g, int i, uint64_t *out);
 /* Records this group's ranks sent to other ranks in the last run (global). */
 uint64_t kc_group_records_sent(const kc_group *g);
+/* The all-to-all of rank `me` as issued to RCCL (and replayed by the
+ * one-process emulation): for each peer in rank order, its sends then its
+ * receives, each cut into pieces of <= piece_records records (the native loop
+ * uses 256 MiB / record bytes, or KC_PIECE_BYTES).  Mx = world x world
+ * record counts (row = source rank).  out[4k..4k+3] = peer, 1 send / 0 receive,
+ * offset and count in records (offsets into the destination-grouped send /
+ * source-grouped receive buffer); fills at most `cap` transfers and returns
+ * how many there are.  Host only (no GPU): the CPU tests check every rank's
+ * plan pairs with its peers' for world 1..9. */
+int kc_exchange_plan(int world, int me, const uint64_t *Mx, uint64_t piece_records, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------- Spec (host) */
 /* Words of the canonical tuple for a model: 1 + 19 * (nc + np + ns). */

@@ -256,3 +256,40 @@ def test_native_enlarged_full_emulated(fixtures, R):
     assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r["level_width"] == fx["level_width"]
     assert r["act_gen"] == fx["act_gen"]
+
+
+def test_native_multipiece_emulated(fixtures, monkeypatch):
+    # the exchange cut into pieces of 85 records (KC_PIECE_BYTES=4096; the
+    # N-GPU default is 256 MiB): the emulated ranks replay every rank's
+    # RCCL plan (kc_exchange_plan) piece by piece, exact against the golden
+    monkeypatch.setenv("KC_PIECE_BYTES", "4096")
+    fx = fixtures["model1"]
+    r = native(3)
+    assert r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+    fx = fixtures["np2_40levels"]
+    r = native(5, np=2, max_levels=40)
+    assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"]
+
+
+@pytest.mark.parametrize("stage", [0, 1, 2])
+@pytest.mark.parametrize("devrow", ["1", "0"])
+def test_native_fault_stops_every_rank(monkeypatch, stage, devrow):
+    # a failure on one rank (KC_FAULT=rank:level:stage) travels in the
+    # all-gather row: every rank leaves the loop with an error at the next
+    # gather instead of waiting in a collective for the failed one
+    from kubecheck import KubecheckError
+    monkeypatch.setenv("KC_DEVROW", devrow)
+    monkeypatch.setenv("KC_FAULT", f"2:7:{stage}")
+    with pytest.raises(KubecheckError) as e:
+        native(4)
+    assert "injected fault" in str(e.value) and e.value.code == -5
+    monkeypatch.setenv("KC_FAULT", f"0:7:{stage}")
+    monkeypatch.setenv("KC_RCCL_FORCE", "1")
+    mc = NativeShardedChecker(ModelConfig(), 0, 1)
+    try:
+        with pytest.raises(KubecheckError) as e:
+            mc.run()
+        assert "injected fault" in str(e.value)
+    finally:
+        mc.close()

@@ -1,0 +1,510 @@
+// coldset.hip — the seen-set's cold tier (coldset.h): sorted fingerprint
+// runs in pinned host RAM or spill files, with HBM directories and Bloom
+// filters, probed by the GPU.  TLC's DiskFPSet keeps the same shape (an
+// in-memory table flushed into a sorted file with an index; MC.out:5
+// "OffHeapDiskFPSet"); here the lookups are batched GPU kernels over a
+// level's sorted new fingerprints, and the host only merges runs and moves
+// bytes to and from files.
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <thread>
+
+#include "coldset.h"
+#include "kc_common.h"
+
+namespace kc {
+
+namespace {
+
+constexpr int kBloomK = 6;            // bits per key, in one 512-bit block
+__device__ __forceinline__ uint64_t bloom_block(uint64_t k, uint64_t nblocks) {
+  return __umul64hi(k * 0x9e3779b97f4a7c15ull, nblocks);
+}
+__device__ __forceinline__ uint64_t bloom_hash(uint64_t k) {
+  uint64_t h = (k ^ (k >> 32)) * 0xd6e8feb86659fd93ull;
+  return h ^ (h >> 29);
+}
+
+__device__ __forceinline__ uint64_t dir_bucket(uint64_t k, int dbits) { return k >> (64 - dbits); }
+
+// dir[b] = first index whose bucket is >= b (b in [0, 2^dbits]); thread i
+// writes the buckets in (bucket(i-1), bucket(i)], thread n the tail.
+__global__ void k_run_dir(const uint64_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ dir, int dbits) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  const uint64_t nb = 1ull << dbits;
+  const uint64_t hi = i < n ? dir_bucket(keys[i], dbits) : nb;
+  const uint64_t lo = i > 0 ? dir_bucket(keys[i - 1], dbits) + 1 : 0;
+  for (uint64_t b = lo; b <= hi; ++b) dir[b] = i;
+}
+
+__global__ void k_bloom_add(const uint64_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ bloom,
+                            uint64_t nblocks) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = keys[i];
+  uint32_t* blk = bloom + bloom_block(k, nblocks) * 16;
+  uint64_t h = bloom_hash(k);
+  for (int j = 0; j < kBloomK; ++j, h >>= 9) atomicOr(&blk[(h >> 5) & 15], 1u << (h & 31));
+}
+
+// One query against one run, restricted to the run's indices [w0, w1) held
+// at win[j - w0].  The directory gives the key's bucket [lo, hi); keys in a
+// bucket are uniform over its key range, so the search starts at the
+// interpolated position and reads whole aligned 8-key lines (one 64-B
+// request each over the host link) until the key's place is bracketed:
+// about 1.2 lines per lookup.
+__device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict__ win, uint64_t w0, uint64_t w1,
+                                         const uint64_t* __restrict__ dir, int dbits) {
+  const uint64_t b = dir_bucket(k, dbits);
+  const uint64_t blo = dir[b], bhi = dir[b + 1];
+  const uint64_t lo = blo > w0 ? blo : w0, hi = bhi < w1 ? bhi : w1;
+  if (lo >= hi) return false;
+  // interpolation inside the bucket: the key's bits below the bucket bits
+  const uint64_t frac = (k << dbits) >> 32;                     // 32-bit fraction
+  uint64_t pos = blo + (((bhi - blo) * frac) >> 32);
+  pos = pos < lo ? lo : (pos >= hi ? hi - 1 : pos);
+  uint64_t a = pos & ~7ull;
+  if (a < lo) a = lo;
+  for (;;) {
+    uint64_t e = (a | 7ull) + 1;
+    if (e > hi) e = hi;
+    uint64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = a + u < e ? win[a + u - w0] : ~0ull;
+    if (k < v[0]) {
+      if (a == lo) return false;
+      a = (a - 1) & ~7ull;
+      if (a < lo) a = lo;
+      continue;
+    }
+    uint64_t last = v[0];
+#pragma unroll
+    for (int u = 1; u < 8; ++u) last = a + u < e ? v[u] : last;
+    if (k > last) {
+      if (e >= hi) return false;
+      a = e;
+      continue;
+    }
+    bool hit = false;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) hit |= v[u] == k;
+    return hit;
+  }
+}
+
+// stat[0]: filter tests (query x run), stat[1]: those it passed
+__global__ void k_cold_probe(const uint64_t* __restrict__ q, uint64_t m, uint8_t* __restrict__ found,
+                             const uint64_t* __restrict__ win, uint64_t w0, uint64_t w1,
+                             const uint64_t* __restrict__ dir, int dbits, const uint32_t* __restrict__ bloom,
+                             uint64_t nblocks, unsigned long long* __restrict__ hits,
+                             unsigned long long* __restrict__ stat) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool hit = false, tested = false, passed = false;
+  if (i < m && !found[i]) {
+    const uint64_t k = q[i];
+    bool maybe = true;
+    if (bloom) {
+      tested = true;
+      const uint32_t* blk = bloom + bloom_block(k, nblocks) * 16;
+      uint64_t h = bloom_hash(k);
+#pragma unroll
+      for (int j = 0; j < kBloomK; ++j, h >>= 9) maybe &= (blk[(h >> 5) & 15] >> (h & 31)) & 1u;
+      passed = maybe;
+    }
+    if (maybe && run_find(k, win, w0, w1, dir, dbits)) {
+      hit = true;
+      found[i] = 1;
+    }
+  }
+  const unsigned long long bh = __ballot(hit), bt = __ballot(tested), bp = __ballot(passed);
+  if ((threadIdx.x & 63) == 0) {
+    if (bh) atomicAdd(hits, (unsigned long long)__popcll(bh));
+    if (bt) atomicAdd(&stat[0], (unsigned long long)__popcll(bt));
+    if (bp) atomicAdd(&stat[1], (unsigned long long)__popcll(bp));
+  }
+}
+
+// qa[w] = first sorted query >= bound[w] (w = 0..nw)
+__global__ void k_window_ranges(const uint64_t* __restrict__ q, uint64_t m, const uint64_t* __restrict__ bound,
+                                uint64_t nw, uint64_t* __restrict__ qa) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w > nw) return;
+  if (w == nw) {
+    qa[w] = m;
+    return;
+  }
+  const uint64_t b = bound[w];
+  uint64_t lo = 0, hi = m;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (q[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  qa[w] = lo;
+}
+
+unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+ColdSet::~ColdSet() {
+  clear();
+  if (d_qa_) (void)hipFree(d_qa_);
+  if (h_qa_) (void)hipHostFree(h_qa_);
+  for (int s = 0; s < 2; ++s) {
+    if (stage_[s]) (void)hipHostFree(stage_[s]);
+    if (stage_ev_[s]) (void)hipEventDestroy(stage_ev_[s]);
+  }
+  if (d_stat_) (void)hipFree(d_stat_);
+}
+
+int ColdSet::init(const Config& c) {
+  static uint64_t ids = 0;
+  cfg_ = c;
+  if (cfg_.window_keys < 64) cfg_.window_keys = 64;
+  cfg_.window_keys &= ~7ull;
+  if (cfg_.merge_threads < 1) cfg_.merge_threads = 1;
+  id_ = ++ids;
+  if (!d_stat_) {
+    KC_HIP_TRY(hipMalloc(&d_stat_, 16));
+    KC_HIP_TRY(hipMemset(d_stat_, 0, 16));
+  }
+  return 0;
+}
+
+void ColdSet::free_meta(ColdRun& r) {
+  if (r.d_wkeys) (void)hipFree(r.d_wkeys);
+  r.d_wkeys = nullptr;
+  r.nw = r.wkeys = 0;
+  if (r.d_dir) (void)hipFree(r.d_dir);
+  if (r.d_bloom) (void)hipFree(r.d_bloom);
+  meta_used_ -= r.meta_bytes;
+  r.d_dir = nullptr;
+  r.d_bloom = nullptr;
+  r.meta_bytes = 0;
+  r.nblocks = 0;
+}
+
+void ColdSet::free_run(ColdRun& r) {
+  free_meta(r);
+  if (r.host) {
+    (void)hipHostFree(r.host);
+    host_used_ -= r.bytes();
+  }
+  if (!r.path.empty()) {
+    unlink(r.path.c_str());
+    disk_used_ -= r.bytes();
+  }
+  keys_ -= r.n;
+  r = ColdRun{};
+}
+
+void ColdSet::clear() {
+  (void)hipDeviceSynchronize();
+  for (auto& r : runs_) free_run(r);
+  runs_.clear();
+  if (d_stat_) (void)hipMemset(d_stat_, 0, 16);
+  merges_ = merged_keys_ = disk_written_ = disk_read_ = windows_skipped_ = 0;
+  peak_meta_ = meta_used_;
+}
+
+// Directory (mandatory) and filter (as the HBM budget allows) of run r from
+// its keys (device memory or pinned host RAM: the kernels read either).
+int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
+  int dbits = 1;
+  while ((1ull << (dbits + 1)) * 16 <= r.n && dbits < 40) ++dbits;
+  const uint64_t dir_bytes = ((1ull << dbits) + 1) * 8;
+  if (cfg_.meta_hbm_bytes && meta_used_ + dir_bytes > cfg_.meta_hbm_bytes) {
+    set_error("seen-set: HBM budget for cold-run directories exhausted (%llu + %llu > %llu B); raise seen_hbm_bytes",
+              (unsigned long long)meta_used_, (unsigned long long)dir_bytes,
+              (unsigned long long)cfg_.meta_hbm_bytes);
+    return -ENOMEM;
+  }
+  KC_HIP_TRY(hipMalloc(&r.d_dir, dir_bytes));
+  r.dbits = dbits;
+  r.meta_bytes = dir_bytes;
+  meta_used_ += dir_bytes;
+  hipLaunchKernelGGL(k_run_dir, dim3(grid_of(r.n + 1)), dim3(256), 0, st, keys, r.n, r.d_dir, dbits);
+  // filter bits per key: the target, or what the budget has left
+  uint64_t bits = (uint64_t)cfg_.bloom_bits;
+  if (cfg_.meta_hbm_bytes && r.n) {
+    const uint64_t left = cfg_.meta_hbm_bytes - meta_used_;
+    bits = std::min<uint64_t>(bits, left * 8 / r.n);
+  }
+  if (bits >= 4 && r.n) {
+    r.nblocks = std::max<uint64_t>(1, r.n * bits / 512);
+    const uint64_t fb = r.nblocks * 64;
+    KC_HIP_TRY(hipMalloc(&r.d_bloom, fb));
+    KC_HIP_TRY(hipMemsetAsync(r.d_bloom, 0, fb, st));
+    r.meta_bytes += fb;
+    meta_used_ += fb;
+    hipLaunchKernelGGL(k_bloom_add, dim3(grid_of(r.n)), dim3(256), 0, st, keys, r.n, r.d_bloom, r.nblocks);
+  }
+  KC_HIP_TRY(hipGetLastError());
+  peak_meta_ = std::max(peak_meta_, meta_used_);
+  return 0;
+}
+
+int ColdSet::add_run(const uint64_t* d_sorted, uint64_t n, hipStream_t st) {
+  if (n == 0) return 0;
+  ColdRun r;
+  r.n = n;
+  KC_HIP_TRY(hipHostMalloc(&r.host, n * 8));
+  host_used_ += r.bytes();
+  keys_ += n;
+  KC_HIP_TRY(hipMemcpyAsync(r.host, d_sorted, n * 8, hipMemcpyDeviceToHost, st));
+  const int rc = build_meta(r, d_sorted, st);
+  runs_.push_back(r);                   // owned (and freed) by runs_ from here on
+  KC_TRY(rc);
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  // size-tiered compaction: a binary counter of run sizes
+  while (runs_.size() >= 2) {
+    const ColdRun &a = runs_[runs_.size() - 2], &b = runs_.back();
+    if (!a.host || !b.host) break;
+    if (!(a.n * 2 <= b.n * 3 || runs_.size() > 12)) break;
+    KC_TRY(merge_last_two(st));
+  }
+  while (cfg_.host_bytes && host_used_ > cfg_.host_bytes) {
+    bool any = false;
+    for (const auto& x : runs_) any |= x.host != nullptr;
+    if (!any) break;
+    KC_TRY(evict_oldest_host(st));
+  }
+  return 0;
+}
+
+int ColdSet::merge_last_two(hipStream_t st) {
+  ColdRun& a = runs_[runs_.size() - 2];
+  ColdRun& b = runs_.back();
+  ColdRun c;
+  c.n = a.n + b.n;
+  KC_HIP_TRY(hipHostMalloc(&c.host, c.n * 8));
+  host_used_ += c.bytes();
+  // the key space cut into T equal ranges, each merged by its own thread
+  // (the runs are uniform, so the ranges carry equal work)
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cfg_.merge_threads, c.n / 65536 + 1));
+  std::vector<uint64_t> ia(T + 1), ib(T + 1);
+  ia[0] = ib[0] = 0;
+  ia[T] = a.n;
+  ib[T] = b.n;
+  for (int t = 1; t < T; ++t) {
+    const uint64_t s = (uint64_t)(((unsigned __int128)t << 64) / (unsigned)T);
+    ia[t] = std::lower_bound(a.host, a.host + a.n, s) - a.host;
+    ib[t] = std::lower_bound(b.host, b.host + b.n, s) - b.host;
+  }
+  const uint64_t *pa = a.host, *pb = b.host;
+  uint64_t* pc = c.host;
+  auto work = [&](int t) {
+    std::merge(pa + ia[t], pa + ia[t + 1], pb + ib[t], pb + ib[t + 1], pc + ia[t] + ib[t]);
+  };
+  try {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  } catch (...) {
+    (void)hipHostFree(c.host);
+    host_used_ -= c.bytes();
+    set_error("seen-set: cannot start merge threads");
+    return -ENOMEM;
+  }
+  merges_ += 1;
+  merged_keys_ += c.n;
+  const uint64_t na = a.n, nb = b.n;
+  free_run(runs_.back());
+  runs_.pop_back();
+  free_run(runs_.back());
+  runs_.pop_back();
+  keys_ += c.n;
+  const int rc = build_meta(c, c.host, st);
+  runs_.push_back(c);
+  KC_TRY(rc);
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  (void)na;
+  (void)nb;
+  return 0;
+}
+
+int ColdSet::evict_oldest_host(hipStream_t st) {
+  (void)st;
+  for (auto& r : runs_) {
+    if (!r.host) continue;
+    if (cfg_.dir.empty()) {
+      set_error("seen-set: host budget %llu B exhausted and no spill directory",
+                (unsigned long long)cfg_.host_bytes);
+      return -ENOMEM;
+    }
+    char name[80];
+    snprintf(name, sizeof name, "/kcfp-%d-%llu-%llu.run", (int)getpid(), (unsigned long long)id_,
+             (unsigned long long)++file_seq_);
+    const std::string path = cfg_.dir + name;
+    const int fd = open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0600);
+    if (fd < 0) {
+      set_error("seen-set: cannot create spill file %s", path.c_str());
+      return -EIO;
+    }
+    const char* p = reinterpret_cast<const char*>(r.host);
+    uint64_t left = r.bytes(), off = 0;
+    while (left) {
+      const ssize_t w = pwrite(fd, p + off, std::min<uint64_t>(left, 1ull << 30), (off_t)off);
+      if (w <= 0) {
+        close(fd);
+        unlink(path.c_str());
+        set_error("seen-set: short write to spill file %s", path.c_str());
+        return -EIO;
+      }
+      left -= (uint64_t)w;
+      off += (uint64_t)w;
+    }
+    if (close(fd) != 0) {
+      unlink(path.c_str());
+      set_error("seen-set: cannot close spill file %s", path.c_str());
+      return -EIO;
+    }
+    // window boundary keys (HBM; a few per GiB of run)
+    r.wkeys = cfg_.window_keys;
+    r.nw = (r.n + r.wkeys - 1) / r.wkeys;
+    std::vector<uint64_t> wk(r.nw + 1);
+    wk[0] = 0;
+    for (uint64_t w = 1; w < r.nw; ++w) wk[w] = r.host[w * r.wkeys];
+    wk[r.nw] = ~0ull;
+    KC_HIP_TRY(hipMalloc(&r.d_wkeys, (r.nw + 1) * 8));
+    KC_HIP_TRY(hipMemcpy(r.d_wkeys, wk.data(), (r.nw + 1) * 8, hipMemcpyHostToDevice));
+    (void)hipHostFree(r.host);
+    r.host = nullptr;
+    host_used_ -= r.bytes();
+    r.path = path;
+    disk_used_ += r.bytes();
+    disk_written_ += r.bytes();
+    return 0;
+  }
+  return 0;
+}
+
+int ColdSet::staging(uint64_t keys) {
+  if (keys <= stage_keys_) return 0;
+  for (int s = 0; s < 2; ++s) {
+    if (stage_[s]) (void)hipHostFree(stage_[s]);
+    stage_[s] = nullptr;
+  }
+  stage_keys_ = 0;
+  for (int s = 0; s < 2; ++s) {
+    KC_HIP_TRY(hipHostMalloc(&stage_[s], keys * 8));
+    if (!stage_ev_[s]) KC_HIP_TRY(hipEventCreateWithFlags(&stage_ev_[s], hipEventDisableTiming));
+  }
+  stage_keys_ = keys;
+  return 0;
+}
+
+int ColdSet::read_window(const ColdRun& r, uint64_t w0, uint64_t w1, uint64_t* dst) {
+  const int fd = open(r.path.c_str(), O_RDONLY);
+  if (fd < 0) {
+    set_error("seen-set: spill file %s missing", r.path.c_str());
+    return -EIO;
+  }
+  char* p = reinterpret_cast<char*>(dst);
+  uint64_t left = (w1 - w0) * 8, off = 0;
+  while (left) {
+    const ssize_t g = pread(fd, p + off, std::min<uint64_t>(left, 1ull << 30), (off_t)(w0 * 8 + off));
+    if (g <= 0) {
+      close(fd);
+      set_error("seen-set: short read from spill file %s", r.path.c_str());
+      return -EIO;
+    }
+    left -= (uint64_t)g;
+    off += (uint64_t)g;
+  }
+  close(fd);
+  disk_read_ += (w1 - w0) * 8;
+  return 0;
+}
+
+int ColdSet::probe(const uint64_t* d_q, uint64_t m, uint8_t* d_found, unsigned long long* d_hits, hipStream_t st) {
+  if (m == 0) return 0;
+  for (size_t k = runs_.size(); k-- > 0;) {            // newest first
+    const ColdRun& r = runs_[k];
+    if (r.host) {
+      hipLaunchKernelGGL(k_cold_probe, dim3(grid_of(m)), dim3(256), 0, st, d_q, m, d_found, r.host, 0ull, r.n,
+                         r.d_dir, r.dbits, r.d_bloom, r.nblocks, d_hits, d_stat_);
+      continue;
+    }
+    // disk run: stream the windows holding at least one query's key range
+    // through two pinned buffers (read one while the GPU probes the other);
+    // each window's launch covers just its queries
+    KC_TRY(staging(r.wkeys));
+    if (qa_cap_ < r.nw + 1) {
+      if (d_qa_) (void)hipFree(d_qa_);
+      if (h_qa_) (void)hipHostFree(h_qa_);
+      d_qa_ = nullptr;
+      h_qa_ = nullptr;
+      qa_cap_ = 0;
+      KC_HIP_TRY(hipMalloc(&d_qa_, (r.nw + 1) * 8));
+      KC_HIP_TRY(hipHostMalloc(&h_qa_, (r.nw + 1) * 8));
+      qa_cap_ = r.nw + 1;
+    }
+    hipLaunchKernelGGL(k_window_ranges, dim3(grid_of(r.nw + 1)), dim3(256), 0, st, d_q, m, r.d_wkeys, r.nw, d_qa_);
+    KC_HIP_TRY(hipMemcpyAsync(h_qa_, d_qa_, (r.nw + 1) * 8, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    int s = 0;
+    for (uint64_t w = 0; w < r.nw; ++w) {
+      const uint64_t qa = h_qa_[w], qb = h_qa_[w + 1];
+      if (qb <= qa) {
+        ++windows_skipped_;
+        continue;
+      }
+      const uint64_t w0 = w * r.wkeys, w1 = std::min(r.n, w0 + r.wkeys);
+      KC_HIP_TRY(hipEventSynchronize(stage_ev_[s]));  // the kernel that last read this buffer is done
+      KC_TRY(read_window(r, w0, w1, stage_[s]));
+      hipLaunchKernelGGL(k_cold_probe, dim3(grid_of(qb - qa)), dim3(256), 0, st, d_q + qa, qb - qa, d_found + qa,
+                         stage_[s], w0, w1, r.d_dir, r.dbits, r.d_bloom, r.nblocks, d_hits, d_stat_);
+      KC_HIP_TRY(hipEventRecord(stage_ev_[s], st));
+      s ^= 1;
+    }
+  }
+  KC_HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+void ColdSet::stats(ColdStats* s) const {
+  *s = ColdStats{};
+  s->runs = runs_.size();
+  for (const auto& r : runs_) s->runs_disk += r.host ? 0 : 1;
+  s->keys = keys_;
+  s->host_bytes = host_used_;
+  s->disk_bytes = disk_used_;
+  s->meta_bytes = meta_used_;
+  s->peak_meta_bytes = peak_meta_;
+  s->merges = merges_;
+  s->merged_keys = merged_keys_;
+  s->disk_written = disk_written_;
+  s->disk_read = disk_read_;
+  s->windows_skipped = windows_skipped_;
+  unsigned long long st[2] = {0, 0};
+  if (d_stat_ && hipMemcpy(st, d_stat_, 16, hipMemcpyDeviceToHost) == hipSuccess) {
+    s->filter_tests = st[0];
+    s->filter_passed = st[1];
+  }
+}
+
+int ColdSet::all_keys(std::vector<uint64_t>& out) {
+  out.clear();
+  out.reserve(keys_);
+  std::vector<uint64_t> buf;
+  for (const auto& r : runs_) {
+    const size_t at = out.size();
+    if (r.host) {
+      out.insert(out.end(), r.host, r.host + r.n);
+    } else {
+      buf.resize(r.n);
+      KC_TRY(read_window(r, 0, r.n, buf.data()));
+      out.insert(out.end(), buf.begin(), buf.end());
+    }
+    std::inplace_merge(out.begin(), out.begin() + at, out.end());
+  }
+  return 0;
+}
+
+}  // namespace kc

@@ -20,9 +20,11 @@
 #include <vector>
 
 #include "../../include/kubecheck.h"
+#include "coldset.h"
 #include "engine.h"
 #include "engine_kernels.h"
 #include "engine_narrow.h"
+#include "engine_spill.h"
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
@@ -124,11 +126,15 @@ class EngineT final : public EngineBase {
     narrow_on_ = cfg.chunk_states == 0 && !(nw && nw[0] == '0') && !ablate_;
     // frontiers in the StateQueue (spill mode): the chunked wide path only
     queued_ = cfg.frontier_hbm_bytes > 0;
-    if (queued_) narrow_on_ = false;    // k_claim tile order (engine_kernels.h spread_tile; KC_TILE_SPREAD=0: block order)
+    if (queued_) narrow_on_ = false;
+    // seen-set spill: a fixed-size hot ClaimSet + the cold tier (coldset.h);
+    // the chunked wide path with tile offsets only
+    spill_ = cfg.seen_hbm_bytes > 0;
+    if (spill_) narrow_on_ = false;    // k_claim tile order (engine_kernels.h spread_tile; KC_TILE_SPREAD=0: block order)
     const char* sp = getenv("KC_TILE_SPREAD");
     if (sp) claim_args_.spread = (uint32_t)atoi(sp);
     const char* ts = getenv("KC_TSCAN");
-    tscan_ = !(ts && ts[0] == '0');
+    tscan_ = spill_ || !(ts && ts[0] == '0');
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
@@ -191,7 +197,9 @@ class EngineT final : public EngineBase {
     // the seen-set allocation is kept across runs (cleared each run), like a
     // TLC FPSet pre-sized with -fpmem; it grows by rehash when needed
     const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
-    if (cs_.t && cs_.capacity() >= fp_slots) {
+    if (spill_) {
+      KC_TRY(spill_setup());
+    } else if (cs_.t && cs_.capacity() >= fp_slots) {
       KC_TRY(cs_.clear(st_));
     } else {
       KC_TRY(cs_.init(fp_slots, st_));
@@ -228,6 +236,7 @@ class EngineT final : public EngineBase {
       }
     }
     cs_.count = ni;
+    hot_count_ = ni;
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
     res->init = ni;
     res->generated = ni;
@@ -304,7 +313,7 @@ class EngineT final : public EngineBase {
       KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
       const uint64_t next_gidx = level_gidx + n;
       if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + cand + 1, true));
-      KC_TRY(cs_.reserve(cand, st_));
+      if (!spill_) KC_TRY(cs_.reserve(cand, st_));
       {
         const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
         KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
@@ -318,8 +327,10 @@ class EngineT final : public EngineBase {
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
       const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
-      for (uint64_t start = 0; start < n; start += chunk) {
-        const uint64_t cn = std::min(chunk, n - start);
+      for (uint64_t start = 0, cn = 0; start < n; start += cn) {
+        cn = std::min(chunk, n - start);
+        // seen-set spill: a chunk whose insertions fit the hot table (may flush it)
+        if (spill_) KC_TRY(spill_cut(cur_ + start, cn, &cn));
         ++res->levels_chunks;
         const unsigned grid = (unsigned)((cn + 255) / 256);
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
@@ -368,6 +379,7 @@ class EngineT final : public EngineBase {
         });
         KC_HIP_TRY(scan_err);
         }
+        if (spill_) KC_TRY(spill_check(cur_ + start, cn, tiles));
         const uint32_t* toff = tscan_ ? toff_ : nullptr;
         if (ablate_) {
           // cut-down k_emit variants on scratch counters, before the real
@@ -422,7 +434,7 @@ class EngineT final : public EngineBase {
         return -ENOMEM;
       }
       const uint64_t n_new = c.chunk_base;
-      cs_.count += n_new;
+      cs_.count = spill_ ? hot_count_ : cs_.count + n_new;
       res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
       if (c.err_key != ~0ull) {
         KC_TRY(report_error(res, c.err_key, level, level_gidx, n));
@@ -479,6 +491,7 @@ class EngineT final : public EngineBase {
   // minimum adjacent gap (MC.out:42 "based on the actual fingerprints").
   int check_fps(uint64_t* min_gap, double* prob) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
+    if (spill_) return check_fps_spill(min_gap, prob);
     const uint64_t cnt = std::max<uint64_t>(cs_.count, 2);
     unsigned long long *a = nullptr, *b = nullptr, *d_n = nullptr;
     void* tmp = nullptr;
@@ -522,6 +535,29 @@ class EngineT final : public EngineBase {
     if (rc) return rc;
     *min_gap = gap;
     *prob = (n > 1 && gap && gap != ~0ull) ? 1.0 / (double)gap : 0.0;
+    return 0;
+  }
+  // the same over hot + cold tiers, on the host (cold keys are mixed
+  // fingerprints: unmixed, merged with the hot table's, sorted)
+  int check_fps_spill(uint64_t* min_gap, double* prob) {
+    std::vector<uint64_t> keys;
+    KC_TRY(cold_.all_keys(keys));
+    uint64_t* hk = reinterpret_cast<uint64_t*>(sp_arena_);
+    KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
+    hipLaunchKernelGGL(k_claimset_keys, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_, cs_.t,
+                       cs_.nslots, hk, hot_limit_, d_spctr_ + 1);
+    KC_HIP_TRY(hipMemcpyAsync(h_spctr_, d_spctr_, 16, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const uint64_t c = std::min<uint64_t>(h_spctr_[1], hot_limit_);
+    const size_t at = keys.size();
+    keys.resize(at + c);
+    if (c) KC_HIP_TRY(hipMemcpy(keys.data() + at, hk, c * 8, hipMemcpyDeviceToHost));
+    for (auto& k : keys) k = cold_unkey(k);
+    std::sort(keys.begin(), keys.end());
+    uint64_t gap = ~0ull;
+    for (size_t i = 1; i < keys.size(); ++i) gap = std::min<uint64_t>(gap, keys[i] - keys[i - 1]);
+    *min_gap = gap;
+    *prob = (keys.size() > 1 && gap && gap != ~0ull) ? 1.0 / (double)gap : 0.0;
     return 0;
   }
   int trace_tuple(int i, uint64_t* out) const override {
@@ -693,6 +729,23 @@ class EngineT final : public EngineBase {
     res->fpset_probes = h_ctr_->probes() + narrow_probes_;
     for (int b = 0; b < OUTDEG_BINS; ++b) res->outdeg_hist[b] = h_ctr_->outdeg(b);
     res->batch_inserts = h_ctr_->settles();
+    if (spill_) {
+      ColdStats cst;
+      cold_.stats(&cst);
+      unsigned long long hits = 0;
+      if (hipMemcpy(&hits, d_spctr_, 8, hipMemcpyDeviceToHost) != hipSuccess) set_error("kubecheck: spill counter readback");
+      res->seen_flushes = sp_flushes_;
+      res->seen_cold_fps = cst.keys;
+      res->seen_cold_queries = sp_queries_;
+      res->seen_cold_hits = hits;
+      res->seen_cold_runs = cst.runs;
+      res->seen_disk_bytes = cst.disk_written;
+      res->seen_peak_hbm_bytes = cs_.nslots * sizeof(ClaimEntry) + sp_arena_bytes_ + cst.peak_meta_bytes;
+      res->seen_filter_tests = cst.filter_tests;
+      res->seen_filter_passed = cst.filter_passed;
+      res->seen_merges = cst.merges;
+      res->seen_seconds = sp_seconds_;
+    }
     if (q_) {
       kc_squeue_stats qs;
       q_->stats(&qs);
@@ -713,6 +766,11 @@ class EngineT final : public EngineBase {
       parent_ = nullptr;
       ord_ = nullptr;
     }
+    if (sp_arena_) (void)hipFree(sp_arena_);
+    if (sp_tsum_) (void)hipFree(sp_tsum_);
+    if (d_spctr_) (void)hipFree(d_spctr_);
+    if (h_tsum_) (void)hipHostFree(h_tsum_);
+    if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
                     (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_})
       if (p) (void)hipFree(p);
@@ -816,6 +874,185 @@ class EngineT final : public EngineBase {
     }
     return 0;
   }
+
+  // ---- seen-set spill (cfg.seen_hbm_bytes > 0; engine_spill.h, coldset.h).
+  // HBM budget B: the hot ClaimSet takes the largest power-of-two table of
+  // <= B/2 bytes and holds <= 1/2 load (hot_limit_); one scratch arena serves
+  // the flush (the hot keys; the sort borrows the cleared-to-be table) and
+  // the per-chunk queries (keys, locations, found flags, sort space; at most
+  // q_max_ per chunk); the rest is the cold runs' directories and filters.
+  int spill_setup() {
+    if (!cs_.t) {
+      const uint64_t B = cfg_.seen_hbm_bytes;
+      uint64_t ns = 1ull << 12;
+      while (ns * 2 * sizeof(ClaimEntry) <= B / 2) ns *= 2;
+      KC_TRY(cs_.init(ns, st_));
+      hot_limit_ = ns / 2;
+      q_max_ = std::max<uint64_t>(CLAIM_TILE * 32, hot_limit_ / 3) / 256 * 256;
+      size_t tmp = 0;
+      {
+        hipcub::DoubleBuffer<uint64_t> k(nullptr, nullptr);
+        hipcub::DoubleBuffer<uint32_t> v(nullptr, nullptr);
+        KC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, v, (int)q_max_, 0, 64, st_));
+      }
+      sp_qtmp_bytes_ = tmp;
+      const uint64_t qbytes = q_max_ * (8 + 8 + 4 + 4 + 1) + tmp + 1024;
+      sp_arena_bytes_ = std::max<uint64_t>(hot_limit_ * 8, qbytes);
+      KC_HIP_TRY(hipMalloc(&sp_arena_, sp_arena_bytes_));
+      KC_HIP_TRY(hipMalloc(&d_spctr_, 64));
+      KC_HIP_TRY(hipHostMalloc(&h_spctr_, 64));
+      const uint64_t used = ns * sizeof(ClaimEntry) + sp_arena_bytes_;
+      if (used + (1ull << 20) > B) {
+        set_error("kubecheck: seen_hbm_bytes %llu too small (hot table + scratch need %llu B)",
+                  (unsigned long long)B, (unsigned long long)used);
+        return -EINVAL;
+      }
+      ColdSet::Config cc;
+      cc.device = cfg_.device;
+      cc.meta_hbm_bytes = B - used;
+      cc.host_bytes = cfg_.seen_host_bytes;
+      cc.dir = cfg_.spill_dir ? cfg_.spill_dir : "";
+      const char* wk = getenv("KC_COLD_WINDOW");      // disk-run staging window (keys); tests shrink it
+      if (wk && atoll(wk) > 0) cc.window_keys = (uint64_t)atoll(wk);
+      const char* bb = getenv("KC_COLD_BLOOM_BITS");  // filter bits per key (0 = no filters; A/B)
+      if (bb) cc.bloom_bits = atoi(bb);
+      KC_TRY(cold_.init(cc));
+    } else {
+      KC_TRY(cs_.clear(st_));
+    }
+    cold_.clear();
+    hot_count_ = 0;
+    sp_flushes_ = sp_queries_ = 0;
+    sp_seconds_ = 0;
+    KC_HIP_TRY(hipMemsetAsync(d_spctr_, 0, 64, st_));
+    return 0;
+  }
+
+  // Cut [cur, cur + len) to a chunk whose successors (an upper bound on its
+  // hot-table insertions) fit both the table's room and q_max_; flush the
+  // hot table into the cold tier first when the room alone would make the
+  // chunk less than half as long as q_max_ allows.
+  int spill_cut(const State* cur, uint64_t len, uint64_t* cut) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t plan_len = std::min<uint64_t>(len, std::max<uint64_t>(CLAIM_TILE, q_max_ / 2 / 256 * 256));
+    const uint64_t tiles = (plan_len + 255) / 256;
+    KC_TRY(grow_buffer(sp_tsum_, sp_tsum_cap_, tiles, false, st_));
+    KC_TRY(grow_host_buffer(h_tsum_, h_tsum_cap_, tiles, st_));
+    hipLaunchKernelGGL(k_tile_succ<M>, dim3((unsigned)tiles), dim3(256), 0, st_, cur, plan_len, flags_, sp_tsum_);
+    KC_HIP_TRY(hipMemcpyAsync(h_tsum_, sp_tsum_, tiles * 4, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    auto pick = [&](uint64_t cap) {
+      uint64_t acc = 0, c = 0;
+      for (uint64_t t = 0; t < tiles; ++t) {
+        if (acc + h_tsum_[t] > cap) break;
+        acc += h_tsum_[t];
+        c = std::min(plan_len, (t + 1) * 256);
+      }
+      return c;
+    };
+    const uint64_t room = hot_limit_ > hot_count_ ? hot_limit_ - hot_count_ : 0;
+    uint64_t c = pick(std::min(room, q_max_));
+    if (c < plan_len && c < pick(q_max_) / 2 && hot_count_ > 0) {
+      KC_TRY(spill_flush());
+      c = pick(q_max_);
+    }
+    if (c == 0) {
+      set_error("kubecheck: a 256-parent tile has %u successors, more than the seen-set's hot table takes per chunk "
+                "(%llu); raise seen_hbm_bytes", h_tsum_[0], (unsigned long long)q_max_);
+      return -ENOMEM;
+    }
+    *cut = c;
+    sp_seconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+  }
+
+  // Hot table -> one sorted cold run; the table starts over empty.
+  int spill_flush() {
+    uint64_t* keys = reinterpret_cast<uint64_t*>(sp_arena_);
+    KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
+    hipLaunchKernelGGL(k_claimset_keys, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_, cs_.t,
+                       cs_.nslots, keys, hot_limit_, d_spctr_ + 1);
+    KC_HIP_TRY(hipMemcpyAsync(h_spctr_, d_spctr_, 16, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const uint64_t c = h_spctr_[1];
+    if (c > hot_limit_) {
+      set_error("kubecheck: hot seen-set holds %llu > %llu fingerprints", (unsigned long long)c,
+                (unsigned long long)hot_limit_);
+      return -EIO;
+    }
+    if (c) {
+      // sort in place, borrowing the hot table (cleared right after) as the
+      // alternate buffer and temporary storage
+      uint64_t* alt = reinterpret_cast<uint64_t*>(cs_.t);
+      const uint64_t tab = cs_.nslots * sizeof(ClaimEntry);
+      const uint64_t off = (c * 8 + 255) / 256 * 256;
+      hipcub::DoubleBuffer<uint64_t> kb(keys, alt);
+      size_t tb = 0;
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, kb, (int)c, 0, 64, st_));
+      if (off + tb > tab) {
+        set_error("kubecheck: seen-set flush sort needs %llu B > %llu", (unsigned long long)(off + tb),
+                  (unsigned long long)tab);
+        return -ENOMEM;
+      }
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(reinterpret_cast<uint8_t*>(cs_.t) + off, tb, kb, (int)c, 0, 64, st_));
+      KC_TRY(cold_.add_run(kb.Current(), c, st_));
+    }
+    KC_TRY(cs_.clear(st_));
+    hot_count_ = 0;
+    ++sp_flushes_;
+    return 0;
+  }
+
+  // After the chunk's claim + settle + tile scan: its winners w.r.t. the hot
+  // tier are checked against the cold tier; those found lose (k_spill_apply)
+  // and the tile offsets are recomputed.
+  int spill_check(const State* cur, uint64_t cn, unsigned tiles) {
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t* a = sp_arena_;
+    uint64_t* qk = reinterpret_cast<uint64_t*>(a);
+    uint64_t* qk2 = qk + q_max_;
+    uint32_t* ql = reinterpret_cast<uint32_t*>(qk2 + q_max_);
+    uint32_t* ql2 = ql + q_max_;
+    uint8_t* found = reinterpret_cast<uint8_t*>(ql2 + q_max_);
+    uint8_t* tmp = found + (q_max_ + 255) / 256 * 256;
+    hipLaunchKernelGGL(k_spill_queries<M>, dim3(tiles), dim3(256), 0, st_, cur, cn, flags_, newmask_, toff_, qk, ql);
+    KC_HIP_TRY(hipMemcpyAsync(h_spctr_ + 2, toff_ + tiles, 4, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const uint64_t m = (uint32_t)h_spctr_[2];
+    if (m > q_max_) {
+      set_error("kubecheck: chunk has %llu new fingerprints > %llu", (unsigned long long)m,
+                (unsigned long long)q_max_);
+      return -EIO;
+    }
+    hot_count_ += m;
+    sp_queries_ += m;
+    if (m && !cold_.empty()) {
+      hipcub::DoubleBuffer<uint64_t> kb(qk, qk2);
+      hipcub::DoubleBuffer<uint32_t> vb(ql, ql2);
+      size_t tb = sp_qtmp_bytes_;
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kb, vb, (int)m, 0, 64, st_));
+      KC_HIP_TRY(hipMemsetAsync(found, 0, m, st_));
+      KC_TRY(cold_.probe(kb.Current(), m, found, d_spctr_, st_));
+      hipLaunchKernelGGL(k_spill_apply, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st_, kb.Current(),
+                         vb.Current(), found, m, newmask_, ttot_, cs_.t, cs_.nslots, d_ctr_);
+      hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
+      KC_HIP_TRY(hipGetLastError());
+    }
+    sp_seconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+  }
+
+  bool spill_ = false;
+  ColdSet cold_;
+  uint64_t hot_limit_ = 0, q_max_ = 0, hot_count_ = 0;
+  uint8_t* sp_arena_ = nullptr;
+  uint64_t sp_arena_bytes_ = 0;
+  size_t sp_qtmp_bytes_ = 0;
+  uint32_t *sp_tsum_ = nullptr, *h_tsum_ = nullptr;
+  uint64_t sp_tsum_cap_ = 0, h_tsum_cap_ = 0;
+  unsigned long long *d_spctr_ = nullptr, *h_spctr_ = nullptr;   // [0] cold hits, [1] flush count
+  uint64_t sp_flushes_ = 0, sp_queries_ = 0;
+  double sp_seconds_ = 0;
 
   // the trace file (parent index + ordinal per state) in HBM, or in pinned
   // host RAM with cfg.trace_host (kernels store into it directly)

@@ -22,8 +22,8 @@ class ShardBase {
   // expand() split around a device-side all-gather row (the native loop over
   // RCCL): expand_dev enqueues the level's claims and writes d_row[0..world)
   // = owner totals, d_row[world] = status_new, d_row[world + 1] = status_err
-  // (on level 1 an Init-state invariant key instead, as the loop would), with
-  // no host sync; expand_done, after the caller's stream sync, reports what
+  // (on level 1 an Init-state invariant key instead, as the loop would),
+  // d_row[world + 2] = 1 if the claims overflowed (else 0), with no host sync; expand_done, after the caller's stream sync, reports what
   // expand() reports.
   virtual int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) = 0;
   virtual int expand_done(uint64_t* counts, uint64_t* err_key) = 0;
@@ -47,6 +47,14 @@ class ShardBase {
                      std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
                      int* err_inv) = 0;
 };
+
+// One transfer of a rank's all-to-all (shard_driver.hip exchange_plan).
+struct Xfer {
+  int peer;
+  int send;          // 1 = send to peer, 0 = receive from peer
+  uint64_t off, n;   // records: offset into the send / receive buffer, count
+};
+std::vector<Xfer> exchange_plan(const std::vector<std::vector<uint64_t>>& Mx, int me, uint64_t piece);
 
 }  // namespace kc
 

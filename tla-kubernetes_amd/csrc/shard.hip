@@ -138,7 +138,8 @@ __global__ void k_head_reset(Counters* __restrict__ C) {
 }
 // row != nullptr (ShardBase::expand_dev): the all-gather row too, in device
 // memory: totals, status_new, status_err (level 1: an Init-state invariant
-// key, 0x12, found by expand takes the status slot, as Group::run does).
+// key, 0x12, found by expand takes the status slot, as Group::run does), and
+// the failure word.
 __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                                uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
                                const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
@@ -157,6 +158,10 @@ __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t*
       }
       row[world] = status_new;
       row[world + 1] = se;
+      // failure word: a full table or an over-wide state found by this
+      // level's claims, so every rank leaves the loop together (the host
+      // overwrites it with its own failure code, if any)
+      row[world + 2] = (C->overflow || C->batch_used) ? 1ull : 0ull;
     }
   }
   if (o >= 16) return;

@@ -49,6 +49,15 @@ constexpr uint64_t NONE = ~0ull;
 constexpr uint64_t KEY44 = (1ull << 44) - 1;
 constexpr uint64_t PIECE_BYTES = 256ull << 20;   // largest single send/recv of the exchange
 
+// Largest single transfer of the exchange in bytes: PIECE_BYTES, or
+// KC_PIECE_BYTES from the environment (tests shrink it so a small model runs
+// the multi-piece path).
+uint64_t piece_bytes() {
+  const char* e = getenv("KC_PIECE_BYTES");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (uint64_t)v : PIECE_BYTES;
+}
+
 // ---------------------------------------------------------------- RCCL
 // Resolved at run time: torch ships its own librccl.so.1; when it is loaded
 // already, dlopen returns that copy (one RCCL per process).
@@ -108,6 +117,34 @@ const RcclApi* rccl() {
     }                                                                                     \
   } while (0)
 
+}  // namespace
+
+// ---------------------------------------------------------------- exchange plan
+// The all-to-all of one rank `me` as the transfers RCCL is given, in order:
+// for each peer, its send pieces, then its receive pieces; each piece at most
+// `piece` records.  Offsets are in records: into the send buffer grouped by
+// destination rank and the receive buffer grouped by source rank.  RCCL pairs
+// the k-th send from s to d with the k-th receive at d from s, so both sides
+// must cut a pair (s, d) into the same pieces: both cut Mx[s][d] here.
+// RcclComm issues this plan; LocalComm executes the same plan with device
+// copies, pairing pieces exactly as RCCL does (so emulated ranks test it).
+std::vector<Xfer> exchange_plan(const std::vector<std::vector<uint64_t>>& Mx, int me, uint64_t piece) {
+  std::vector<Xfer> out;
+  const int R = (int)Mx.size();
+  if (piece == 0) piece = 1;
+  uint64_t soff = 0, roff = 0;
+  for (int peer = 0; peer < R; ++peer) {
+    const uint64_t ns = Mx[me][peer], nr = Mx[peer][me];
+    for (uint64_t k = 0; k < ns; k += piece) out.push_back({peer, 1, soff + k, std::min(piece, ns - k)});
+    for (uint64_t k = 0; k < nr; k += piece) out.push_back({peer, 0, roff + k, std::min(piece, nr - k)});
+    soff += ns;
+    roff += nr;
+  }
+  return out;
+}
+
+namespace {
+
 // ---------------------------------------------------------------- Comm
 // Collectives over the ranks; every call is made by the driver on behalf of
 // all the shards this process holds (LocalComm: every rank; RcclComm: one).
@@ -125,11 +162,15 @@ class Comm {
   virtual int broadcast(int root, uint64_t* v) = 0;
   // v[i] = the vector of local shard i; out = the element-wise sum over ranks
   virtual int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) = 0;
-  // Device-row all-gather (one local shard; RcclComm with real collectives):
-  // row_buffer(L) is where the shard's kernels write its row of L words;
-  // all_gather_dev gathers it on the shard's stream, syncs, and returns the
-  // rank-major rows.  nullptr: not supported, use all_gather.
-  virtual uint64_t* row_buffer(size_t L) { (void)L; return nullptr; }
+  // Device-row all-gather: row_buffer(i, L) is where local shard i's kernels
+  // write its row of L words; all_gather_dev gathers every local shard's row
+  // (on their streams), syncs, and returns the rank-major rows.  nullptr:
+  // not supported, use all_gather.
+  virtual uint64_t* row_buffer(size_t i, size_t L) {
+    (void)i;
+    (void)L;
+    return nullptr;
+  }
   virtual int all_gather_dev(size_t L, std::vector<uint64_t>& out) {
     (void)L;
     (void)out;
@@ -141,25 +182,67 @@ class Comm {
 class LocalComm final : public Comm {
  public:
   explicit LocalComm(std::vector<ShardBase*> shards) : s_(std::move(shards)) {}
+  ~LocalComm() override {
+    if (rows_) (void)hipFree(rows_);
+    if (hrows_) (void)hipHostFree(hrows_);
+  }
   int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
     out.clear();
     for (const auto& r : rows) out.insert(out.end(), r.begin(), r.end());
     return 0;
   }
+  // one device row per emulated rank, gathered by copies (the rows the
+  // kernels write in the RCCL path, k_owner_totals, are exercised here)
+  uint64_t* row_buffer(size_t i, size_t L) override {
+    const size_t need = s_.size() * L;
+    if (need > rows_cap_) {
+      if (rows_) (void)hipFree(rows_);
+      if (hrows_) (void)hipHostFree(hrows_);
+      rows_ = nullptr;
+      hrows_ = nullptr;
+      rows_cap_ = 0;
+      if (hipMalloc(&rows_, need * 8) != hipSuccess || hipHostMalloc(&hrows_, need * 8) != hipSuccess) return nullptr;
+      rows_cap_ = need;
+    }
+    return rows_ + i * L;
+  }
+  int all_gather_dev(size_t L, std::vector<uint64_t>& out) override {
+    for (size_t i = 0; i < s_.size(); ++i)
+      KC_HIP_TRY(hipMemcpyAsync(hrows_ + i * L, rows_ + i * L, L * 8, hipMemcpyDeviceToHost, s_[i]->stream()));
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
+    out.assign(hrows_, hrows_ + s_.size() * L);
+    return 0;
+  }
+  // every rank's exchange plan, its pieces paired as RCCL pairs them: the
+  // k-th send from src to dst with the k-th receive at dst from src
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx,
                  uint64_t rb, const std::vector<void*>& recv) override {
     const int R = (int)s_.size();
+    const uint64_t piece = std::max<uint64_t>(1, piece_bytes() / rb);
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every pack is done
+    std::vector<std::vector<Xfer>> plan(R);
+    for (int r = 0; r < R; ++r) plan[r] = exchange_plan(Mx, r, piece);
     for (int dst = 0; dst < R; ++dst) {
-      uint64_t roff = 0;
       for (int src = 0; src < R; ++src) {
-        uint64_t soff = 0;
-        for (int d = 0; d < dst; ++d) soff += Mx[src][d];
-        const uint64_t n = Mx[src][dst];
-        if (n)
-          KC_HIP_TRY(hipMemcpyAsync((char*)recv[dst] + roff * rb, (const char*)send[src] + soff * rb, n * rb,
-                                    hipMemcpyDeviceToDevice, s_[dst]->stream()));
-        roff += n;
+        std::vector<const Xfer*> sends, recvs;
+        for (const auto& x : plan[src])
+          if (x.send && x.peer == dst) sends.push_back(&x);
+        for (const auto& x : plan[dst])
+          if (!x.send && x.peer == src) recvs.push_back(&x);
+        if (sends.size() != recvs.size()) {
+          set_error("exchange plan: %zu sends from rank %d to %d but %zu receives", sends.size(), src, dst,
+                    recvs.size());
+          return -EIO;
+        }
+        for (size_t k = 0; k < sends.size(); ++k) {
+          if (sends[k]->n != recvs[k]->n) {
+            set_error("exchange plan: piece %zu of %d->%d: %llu sent, %llu received", k, src, dst,
+                      (unsigned long long)sends[k]->n, (unsigned long long)recvs[k]->n);
+            return -EIO;
+          }
+          KC_HIP_TRY(hipMemcpyAsync((char*)recv[dst] + recvs[k]->off * rb, (const char*)send[src] + sends[k]->off * rb,
+                                    sends[k]->n * rb, hipMemcpyDeviceToDevice, s_[dst]->stream()));
+        }
       }
     }
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
@@ -175,6 +258,9 @@ class LocalComm final : public Comm {
 
  private:
   std::vector<ShardBase*> s_;
+  uint64_t* rows_ = nullptr;
+  uint64_t* hrows_ = nullptr;
+  size_t rows_cap_ = 0;
 };
 
 class RcclComm final : public Comm {
@@ -206,8 +292,8 @@ class RcclComm final : public Comm {
     out.assign(hbuf_ + L, hbuf_ + L + L * R);
     return 0;
   }
-  uint64_t* row_buffer(size_t L) override {
-    if (trivial_ || scratch(L * ((size_t)s_->world() + 1))) return nullptr;
+  uint64_t* row_buffer(size_t i, size_t L) override {
+    if (i != 0 || trivial_ || scratch(L * ((size_t)s_->world() + 1))) return nullptr;
     return buf_;
   }
   int all_gather_dev(size_t L, std::vector<uint64_t>& out) override {
@@ -221,22 +307,16 @@ class RcclComm final : public Comm {
   }
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
                  const std::vector<void*>& recv) override {
-    const int R = s_->world(), me = s_->rank();
     const uint64_t rw = rb / 8;                       // records are whole 8-byte words
-    const uint64_t piece = std::max<uint64_t>(1, PIECE_BYTES / rb);   // records per piece
+    const uint64_t piece = std::max<uint64_t>(1, piece_bytes() / rb);   // records per piece
     hipStream_t st = s_->stream();
+    const std::vector<Xfer> plan = exchange_plan(Mx, s_->rank(), piece);
     KC_NCCL_TRY(rccl()->group_start());
-    uint64_t soff = 0, roff = 0;
-    for (int peer = 0; peer < R; ++peer) {
-      const uint64_t ns = Mx[me][peer], nr = Mx[peer][me];
-      for (uint64_t k = 0; k < ns; k += piece)
-        KC_NCCL_TRY(rccl()->send((const uint64_t*)send[0] + (soff + k) * rw, std::min(piece, ns - k) * rw,
-                                 ncclUint64, peer, comm_, st));
-      for (uint64_t k = 0; k < nr; k += piece)
-        KC_NCCL_TRY(rccl()->recv((uint64_t*)recv[0] + (roff + k) * rw, std::min(piece, nr - k) * rw,
-                                 ncclUint64, peer, comm_, st));
-      soff += ns;
-      roff += nr;
+    for (const auto& x : plan) {
+      if (x.send)
+        KC_NCCL_TRY(rccl()->send((const uint64_t*)send[0] + x.off * rw, x.n * rw, ncclUint64, x.peer, comm_, st));
+      else
+        KC_NCCL_TRY(rccl()->recv((uint64_t*)recv[0] + x.off * rw, x.n * rw, ncclUint64, x.peer, comm_, st));
     }
     KC_NCCL_TRY(rccl()->group_end());
     return 0;                                          // stream-ordered before insert
@@ -301,6 +381,10 @@ class Group {
       : local_(std::move(local)), comm_(std::move(comm)), cfg_(cfg) {
     const char* dr = getenv("KC_DEVROW");     // KC_DEVROW=0: host rows + expand's own sync (A/B)
     dev_row_off_ = dr && dr[0] == '0';
+    // fault injection for the failure-path tests: KC_FAULT=rank:level:stage
+    // (stage 0 expand, 1 pack, 2 insert) fails that rank's stage with -EIO
+    const char* fl = getenv("KC_FAULT");
+    if (fl && sscanf(fl, "%d:%d:%d", &fault_rank_, &fault_level_, &fault_stage_) != 3) fault_rank_ = -1;
     world_ = local_[0]->world();
     cfg_.spill_dir = nullptr;
     for (auto* s : local_) s->set_async_pack(true);
@@ -310,6 +394,7 @@ class Group {
     recv_cap_.assign(local_.size(), 0);
   }
   ~Group() {
+    if (h_fail_) (void)hipHostFree(h_fail_);
     for (size_t i = 0; i < local_.size(); ++i) {
       (void)hipSetDevice(local_[i]->device());
       if (send_[i]) (void)hipFree(send_[i]);
@@ -326,10 +411,23 @@ class Group {
       if (s->rank() == rank) return s;
     return nullptr;
   }
+  // every rank takes part in the broadcast; a failed lookup on the owner
+  // travels as NONE, so all ranks fail together
   int query_parent(int rank, int level, uint64_t idx, uint64_t* key) {
     uint64_t v = 0;
-    if (ShardBase* s = owner_local(rank)) KC_TRY(s->parent_key(level, idx, &v));
+    std::string why;
+    if (ShardBase* s = owner_local(rank)) {
+      if (s->parent_key(level, idx, &v) < 0) {
+        why = last_error();
+        v = NONE;
+      }
+    }
     KC_TRY(comm_->broadcast(rank, &v));
+    if (v == NONE) {
+      set_error("kc_group_run: trace walk failed on rank %d at level %d index %llu%s%s", rank, level,
+                (unsigned long long)idx, why.empty() ? "" : ": ", why.c_str());
+      return -EIO;
+    }
     *key = v;
     return 0;
   }
@@ -345,6 +443,7 @@ class Group {
     return 0;
   }
   int error_trace(uint64_t err, int level, kc_result* res);
+  int group_failed(int rank, uint64_t word, const std::vector<int>& fail, const std::string& msg);
 
   std::vector<ShardBase*> local_;
   std::unique_ptr<Comm> comm_;
@@ -356,8 +455,18 @@ class Group {
   std::vector<uint64_t> sent_local_;   // records each local shard sent to other ranks
   uint64_t sent_ = 0;                  // all ranks (after run)
   bool dev_row_off_ = false;
+  uint64_t* h_fail_ = nullptr;         // pinned: failure words copied into device rows
+  int fault_rank_ = -1, fault_level_ = 0, fault_stage_ = 0;
 };
 
+// Failure handling: no rank may leave the loop alone, or its peers would
+// wait in a collective for it forever (RCCL driven directly has no
+// watchdog).  A rank that fails records the code and keeps taking part in
+// the collectives; the failure travels in the all-gather row (word R + 2;
+// claims that overflow set it on the device) and every rank stops at the
+// next gather with an error.  A failure after the gather (pack, insert)
+// sends zeroed records for the rest of the level; the error walk and the
+// final reduction carry a failure flag the same way.
 int Group::run(kc_result* res) {
   memset(res, 0, sizeof *res);
   res->err_action = res->err_self = res->err_invariant = -1;
@@ -367,11 +476,28 @@ int Group::run(kc_result* res) {
   const auto t0 = std::chrono::steady_clock::now();
   const size_t nl = local_.size();
   const int R = world_;
+  const size_t L = (size_t)R + 3;            // row: owner counts | new states | error key | failure
+  std::vector<int> fail(nl, 0);
+  std::string fail_msg;
+  auto note = [&](size_t i, int rc) {
+    if (rc < 0 && !fail[i]) {
+      fail[i] = rc;
+      if (fail_msg.empty()) fail_msg = last_error();
+    }
+  };
+  auto inject = [&](size_t i, int level, int stage) {
+    if (local_[i]->rank() == fault_rank_ && level == fault_level_ && stage == fault_stage_ && !fail[i]) {
+      set_error("kc_group_run: injected fault (KC_FAULT) on rank %d at level %d, stage %d", fault_rank_, level, stage);
+      note(i, -EIO);
+    }
+  };
+  auto fail_word = [&](size_t i) -> uint64_t { return fail[i] ? (1ull << 32) | (uint64_t)(uint32_t)(-fail[i]) : 0ull; };
   std::vector<uint64_t> status_new(nl), status_err(nl, NONE), e1(nl, NONE);
   for (size_t i = 0; i < nl; ++i) {
-    KC_HIP_TRY(hipSetDevice(local_[i]->device()));
-    KC_TRY(local_[i]->init(&status_new[i]));
+    note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
+    if (!fail[i]) note(i, local_[i]->init(&status_new[i]));
   }
+  if (!h_fail_) KC_HIP_TRY(hipHostMalloc(&h_fail_, 16 * 8));
   std::vector<uint64_t> widths;
   int level = 1;
   uint64_t err = NONE;
@@ -380,43 +506,66 @@ int Group::run(kc_result* res) {
   std::vector<std::vector<uint64_t>> Mx(R, std::vector<uint64_t>(R, 0));
   for (;;) {
     const bool last = cfg_.max_levels && level >= cfg_.max_levels;
-    // one local shard over RCCL: its kernels write the all-gather row in
-    // device memory and the gather's sync is the level's first (expand has
-    // none of its own)
-    uint64_t* d_row = (nl == 1 && !last && !dev_row_off_) ? comm_->row_buffer((size_t)R + 2) : nullptr;
-    if (d_row) {
-      std::fill(counts[0].begin(), counts[0].end(), 0);
-      KC_HIP_TRY(hipSetDevice(local_[0]->device()));
-      KC_TRY(local_[0]->expand_dev(status_new[0], status_err[0], level == 1, d_row));
-      KC_TRY(comm_->all_gather_dev((size_t)R + 2, all));
-      KC_TRY(local_[0]->expand_done(counts[0].data(), &e1[0]));
-      if (level == 1 && e1[0] != NONE && (e1[0] & 0xFF) == 0x12) {
-        status_err[0] = e1[0];       // (k_owner_totals put it in the row already)
-        e1[0] = NONE;
-      }
+    // device rows (every local shard's kernels write its all-gather row, so
+    // the gather's sync is the level's first: expand has none of its own)
+    std::vector<uint64_t*> d_rows(nl, nullptr);
+    bool dev = !last && !dev_row_off_;
+    for (size_t i = 0; i < nl && dev; ++i) {
+      d_rows[i] = comm_->row_buffer(i, L);
+      dev = d_rows[i] != nullptr;
     }
-    for (size_t i = 0; i < nl && !d_row; ++i) {
-      std::fill(counts[i].begin(), counts[i].end(), 0);
-      e1[i] = NONE;
-      if (!last) {
+    if (dev) {
+      for (size_t i = 0; i < nl; ++i) {
+        std::fill(counts[i].begin(), counts[i].end(), 0);
+        e1[i] = NONE;
         KC_HIP_TRY(hipSetDevice(local_[i]->device()));
-        KC_TRY(local_[i]->expand(counts[i].data(), &e1[i]));
+        inject(i, level, 0);
+        if (!fail[i]) note(i, local_[i]->expand_dev(status_new[i], status_err[i], level == 1, d_rows[i]));
+        if (fail[i]) {          // the row says so, whatever else it holds
+          h_fail_[i % 16] = fail_word(i);
+          KC_HIP_TRY(hipMemcpyAsync(d_rows[i] + R + 2, &h_fail_[i % 16], 8, hipMemcpyHostToDevice,
+                                    local_[i]->stream()));
+        }
+      }
+      KC_TRY(comm_->all_gather_dev(L, all));
+      for (size_t i = 0; i < nl; ++i) {
+        if (fail[i]) continue;
+        note(i, local_[i]->expand_done(counts[i].data(), &e1[i]));
         if (level == 1 && e1[i] != NONE && (e1[i] & 0xFF) == 0x12) {
-          // an Init state violates an invariant: level 1's error, ahead of
-          // any level-2 error (distributed.py does the same)
-          status_err[i] = e1[i];
+          status_err[i] = e1[i];       // (k_owner_totals put it in the row already)
           e1[i] = NONE;
         }
       }
-      rows[i] = counts[i];
-      rows[i].push_back(status_new[i]);
-      rows[i].push_back(status_err[i]);
+    } else {
+      for (size_t i = 0; i < nl; ++i) {
+        std::fill(counts[i].begin(), counts[i].end(), 0);
+        e1[i] = NONE;
+        if (!last) inject(i, level, 0);
+        if (!last && !fail[i]) {
+          KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+          note(i, local_[i]->expand(counts[i].data(), &e1[i]));
+          if (level == 1 && e1[i] != NONE && (e1[i] & 0xFF) == 0x12) {
+            // an Init state violates an invariant: level 1's error, ahead of
+            // any level-2 error (distributed.py does the same)
+            status_err[i] = e1[i];
+            e1[i] = NONE;
+          }
+        }
+        rows[i] = counts[i];
+        rows[i].push_back(status_new[i]);
+        rows[i].push_back(status_err[i]);
+        rows[i].push_back(fail_word(i));
+      }
+      KC_TRY(comm_->all_gather(rows, all));
     }
-    if (!d_row) KC_TRY(comm_->all_gather(rows, all));
+    for (int r = 0; r < R; ++r) {
+      const uint64_t w = all[(size_t)r * L + R + 2];
+      if (w) return group_failed(r, w, fail, fail_msg);
+    }
     uint64_t total = 0;
     err = NONE;
     for (int r = 0; r < R; ++r) {
-      const uint64_t* row = all.data() + (size_t)r * (R + 2);
+      const uint64_t* row = all.data() + (size_t)r * L;
       for (int d = 0; d < R; ++d) Mx[r][d] = row[d];
       total += row[R];
       err = std::min(err, row[R + 1]);
@@ -436,10 +585,17 @@ int Group::run(kc_result* res) {
       }
       sent_local_[i] += ns - Mx[me][me];
       const uint64_t rb = local_[i]->record_bytes();
+      // (without its buffers a rank cannot take part in the exchange at all)
       KC_TRY(buffer(send_, send_cap_, i, std::max<uint64_t>(ns, 1) * rb));
       KC_TRY(buffer(recv_, recv_cap_, i, std::max<uint64_t>(nr, 1) * rb));
       KC_HIP_TRY(hipSetDevice(local_[i]->device()));
-      KC_TRY(local_[i]->pack(send_[i]));
+      // (a rank cannot reach pack already failed: the gather above would
+      // have stopped every rank; a failed pack means a broken device, and
+      // its records are zeroed)
+      const bool pre = fail[i] != 0;
+      if (!pre) note(i, local_[i]->pack(send_[i]));
+      if (fail[i] && !pre && ns) KC_HIP_TRY(hipMemsetAsync(send_[i], 0, ns * rb, local_[i]->stream()));
+      inject(i, level, 1);      // (a failure found after a complete pack)
     }
     std::vector<void*> sv(send_.begin(), send_.end()), rv(recv_.begin(), recv_.end());
     KC_TRY(comm_->all_to_all(sv, Mx, local_[0]->record_bytes(), rv));
@@ -449,10 +605,11 @@ int Group::run(kc_result* res) {
       for (int s = 0; s < R; ++s) nr += Mx[s][me];
       uint64_t n_new = 0, e2 = NONE;
       KC_HIP_TRY(hipSetDevice(local_[i]->device()));
-      KC_TRY(local_[i]->insert(recv_[i], nr, &n_new, &e2));
-      status_new[i] = n_new;
-      status_err[i] = std::min(e1[i], e2);
-      KC_TRY(local_[i]->advance());
+      inject(i, level, 2);
+      if (!fail[i]) note(i, local_[i]->insert(recv_[i], nr, &n_new, &e2));
+      if (!fail[i]) note(i, local_[i]->advance());
+      status_new[i] = fail[i] ? 0 : n_new;
+      status_err[i] = fail[i] ? NONE : std::min(e1[i], e2);
     }
     ++level;
     if ((int)widths.size() >= KC_MAX_LEVELS) {
@@ -460,20 +617,23 @@ int Group::run(kc_result* res) {
       return -ENOMEM;
     }
   }
-  // global totals (the same on every rank)
+  // global totals (the same on every rank), with a failure count
   std::vector<std::vector<uint64_t>> mine(nl);
   for (size_t i = 0; i < nl; ++i) {
     kc_result r;
-    KC_TRY(local_[i]->result(&r));
+    memset(&r, 0, sizeof r);
+    if (!fail[i]) note(i, local_[i]->result(&r));
     for (int a = 0; a < KC_NACTIONS; ++a) mine[i].push_back(r.act_gen[a]);
     for (int a = 0; a < KC_NACTIONS; ++a) mine[i].push_back(r.act_dist[a]);
     mine[i].push_back(r.init);
     mine[i].push_back(r.generated);
     mine[i].push_back(r.distinct);
     mine[i].push_back(sent_local_[i]);
+    mine[i].push_back(fail[i] ? 1 : 0);
   }
   std::vector<uint64_t> tot;
   KC_TRY(comm_->all_reduce_sum(mine, tot));
+  if (tot[2 * KC_NACTIONS + 4]) return group_failed(-1, 0, fail, fail_msg);
   for (int a = 0; a < KC_NACTIONS; ++a) {
     res->act_gen[a] = tot[a];
     res->act_dist[a] = tot[KC_NACTIONS + a];
@@ -491,6 +651,27 @@ int Group::run(kc_result* res) {
   res->collision_optimistic = d * (g - d) / 18446744073709551616.0;
   res->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return 0;
+}
+
+// Every rank leaves with an error: its own message where one of its shards
+// failed, otherwise the failing rank and what its failure word says.
+int Group::group_failed(int rank, uint64_t word, const std::vector<int>& fail, const std::string& msg) {
+  for (size_t i = 0; i < fail.size(); ++i) {
+    if (fail[i]) {
+      set_error("%s", msg.c_str());
+      return fail[i];
+    }
+  }
+  if (rank < 0) {
+    set_error("kc_group_run: a peer rank failed");
+    return -EIO;
+  }
+  if (word >> 32) {
+    set_error("kc_group_run: rank %d failed (errno %d)", rank, (int)(word & 0xffffffffu));
+    return -(int)(word & 0xffffffffu);
+  }
+  set_error("kc_group_run: rank %d: successor overflow or full table", rank);
+  return -ENOMEM;
 }
 
 // Walk the parent keys back across ranks (TLC's trace file), then replay
@@ -594,5 +775,23 @@ int kc_group_trace_tuple(kc_group* g, int i, uint64_t* out) {
 }
 
 uint64_t kc_group_records_sent(const kc_group* g) { return g ? g->impl->records_sent() : 0; }
+
+int kc_exchange_plan(int world, int me, const uint64_t* Mx, uint64_t piece_records, uint64_t* out, int cap) {
+  if (world < 1 || me < 0 || me >= world || !Mx || cap < 0 || (cap > 0 && !out)) {
+    set_error("kc_exchange_plan: bad argument");
+    return -EINVAL;
+  }
+  std::vector<std::vector<uint64_t>> M(world, std::vector<uint64_t>(world));
+  for (int s = 0; s < world; ++s)
+    for (int d = 0; d < world; ++d) M[s][d] = Mx[(size_t)s * world + d];
+  const std::vector<Xfer> plan = exchange_plan(M, me, piece_records);
+  for (size_t k = 0; k < plan.size() && (int)k < cap; ++k) {
+    out[4 * k] = (uint64_t)plan[k].peer;
+    out[4 * k + 1] = (uint64_t)plan[k].send;
+    out[4 * k + 2] = plan[k].off;
+    out[4 * k + 3] = plan[k].n;
+  }
+  return (int)plan.size();
+}
 
 }  // extern "C"

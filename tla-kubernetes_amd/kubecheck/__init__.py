@@ -61,6 +61,11 @@ class ModelConfig:
     frontier_segment_states: int = 0   # parents per chunk / states per segment (0 = 2^22)
     spill_dir: Optional[str] = None
     trace_host: bool = False    # the trace file (9 B per state) in pinned host RAM
+    # seen-set spill (TLC's OffHeapDiskFPSet role): > 0 caps the seen-set's HBM;
+    # older fingerprints go to sorted runs in pinned host RAM (seen_host_bytes,
+    # 0 = unlimited), then to files in spill_dir
+    seen_hbm_bytes: int = 0
+    seen_host_bytes: int = 0
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()
@@ -105,6 +110,7 @@ class CheckResult:
     frontier_spilled_bytes: int = 0
     frontier_reloaded_bytes: int = 0
     frontier_peak_hbm_bytes: int = 0
+    seen: Dict[str, float] = field(default_factory=dict)   # seen-set spill statistics (seen_* fields)
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -130,7 +136,8 @@ def _result(r: KcResult) -> CheckResult:
         batch_inserts=r.batch_inserts, levels_chunks=r.levels_chunks,
         outdeg_hist=[int(x) for x in r.outdeg_hist],
         frontier_spilled_bytes=r.frontier_spilled_bytes, frontier_reloaded_bytes=r.frontier_reloaded_bytes,
-        frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes)
+        frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes,
+        seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")})
 
 
 class ModelChecker:

@@ -35,6 +35,7 @@ class KcModelConfig(C.Structure):
         ("verbose", C.c_int), ("timing", C.c_int), ("invariants", C.c_int),
         ("frontier_hbm_bytes", C.c_uint64), ("frontier_host_bytes", C.c_uint64),
         ("frontier_segment_states", C.c_uint64), ("spill_dir", C.c_char_p), ("trace_host", C.c_int),
+        ("seen_hbm_bytes", C.c_uint64), ("seen_host_bytes", C.c_uint64),
     ]
 
 
@@ -52,6 +53,10 @@ class KcResult(C.Structure):
         ("levels_chunks", C.c_uint64), ("outdeg_hist", C.c_uint64 * 16),
         ("frontier_spilled_bytes", C.c_uint64), ("frontier_reloaded_bytes", C.c_uint64),
         ("frontier_peak_hbm_bytes", C.c_uint64),
+        ("seen_flushes", C.c_uint64), ("seen_cold_fps", C.c_uint64), ("seen_cold_runs", C.c_uint64),
+        ("seen_cold_queries", C.c_uint64), ("seen_cold_hits", C.c_uint64), ("seen_merges", C.c_uint64),
+        ("seen_filter_tests", C.c_uint64), ("seen_filter_passed", C.c_uint64),
+        ("seen_disk_bytes", C.c_uint64), ("seen_peak_hbm_bytes", C.c_uint64), ("seen_seconds", C.c_double),
     ]
 
 
@@ -143,6 +148,7 @@ SIGNATURES = [
     ("kc_group_run", C.c_int, [_P, C.POINTER(KcResult)]),
     ("kc_group_trace_tuple", C.c_int, [_P, C.c_int, _U64P]),
     ("kc_group_records_sent", C.c_uint64, [_P]),
+    ("kc_exchange_plan", C.c_int, [C.c_int, C.c_int, _U64P, C.c_uint64, _U64P, C.c_int]),
     ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_init", C.c_int, [C.POINTER(KcModelConfig), _U64P, C.c_int]),
