@@ -195,7 +195,9 @@ typedef struct {
   int timing;              /* 1 = time every kernel launch with HIP events,
                               2 = only k_claim (the roofline kernel) */
   int invariants;          /* MC.cfg INVARIANT list: bit 0 TypeOK, bit 1
-                              OnlyOneVersion (default 3; 0 = check none) */
+                              OnlyOneVersion (default 3; 0 = check none), bit 2
+                              the build-defined NoLostUpdate (with its lostUpdate
+                              history variable; models of <= 3 actors) */
   /* Frontier spill (single-GPU engine).  frontier_hbm_bytes > 0 keeps the
    * frontiers in a kc_squeue with that HBM budget: levels run in chunks of
    * <= frontier_segment_states parents, read from the queue's head and
@@ -259,6 +261,8 @@ typedef struct {
   uint64_t seen_disk_bytes;     /* cold-run bytes written to spill files */
   uint64_t seen_peak_hbm_bytes; /* peak HBM of the seen-set (hot table + scratch + cold metadata) */
   double seen_seconds;          /* host wall time in chunk planning, flushes and cold checks */
+  uint64_t cand_overflow_records;  /* settle candidates beyond their tile's segment (overflow list) */
+  uint64_t cand_buffer_peak_bytes; /* HBM of the candidate-record buffers (tile segments + overflow list) */
 } kc_result;
 
 typedef struct kc_engine kc_engine;

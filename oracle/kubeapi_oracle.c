@@ -54,6 +54,9 @@ typedef uint8_t oval;
 #define OV_HASVV(o) (((o) >> 2) & 1u)
 #define OV_SPEC(o) (((o) >> 3) & 1u)
 #define OV_VV(o) (((o) >> 4) & 0xFu)
+/* lostUpdate, the history variable of the build-defined NoLostUpdate, kept
+ * in bit 63 of kstate.api (see check_invariants) */
+#define KO_LOST_UPDATE (1ull << 63)
 static inline oval ov_bare(int id) { return (oval)(OV_DEF | (id << 1)); }
 static inline oval ov_make(int id, int hasvv, int spec, int vv) {
   return (oval)(OV_DEF | (id << 1) | (hasvv << 2) | (spec << 3) | (vv << 4));
@@ -447,16 +450,21 @@ static void a_APIStart(const model *m, const kstate *s, int self, emitter *e) {
       break;
     case OP_Update: {                                             /* :732-739 */
       br(e, KO_B_API_UPDATE);
-      int ok = 0;
+      int ok = 0, read = 0;
       uint64_t x = same;
       while (x) {
         int u = __builtin_ctzll(x); x &= x - 1;
+        if (tla_HasRead(ov_of_u(m, u), c)) read = 1;
         if (m->cfg.variant == 1 || tla_HasRead(ov_of_u(m, u), c)) ok = 1;
       }
       if (ok) {
         br(e, KO_B_API_UPDATE_OK);
         t.api = (s->api & ~same) | (1ull << u_of(m, tla_Write(o)));
         t.rq_status[c] = ST_Ok;
+        /* lostUpdate' = TRUE: the history variable of the build-defined
+         * NoLostUpdate (see check_invariants) — an Update applied although
+         * its writer read no stored version (possible only in variant 1) */
+        if (m->cfg.lost_update && !read) t.api |= KO_LOST_UPDATE;
       } else { br(e, KO_B_API_UPDATE_ERR); t.rq_status[c] = ST_Error; }
       break;
     }
@@ -475,7 +483,7 @@ static void a_APIStart(const model *m, const kstate *s, int self, emitter *e) {
     uint64_t km = (k == K_Secret) ? m->idmask[ID_SECRET] : (k == K_PVC) ? m->idmask[ID_PVC] : 0;
     /* variant 4 (seeded bug): the reply lists objects of every kind, which
      * violates IsValidListRequest's o.k = r.kind (:435), i.e. TypeOK */
-    t.lr_objs[c] = m->cfg.variant == 4 ? s->api : (s->api & km);
+    t.lr_objs[c] = m->cfg.variant == 4 ? (s->api & m->allmask) : (s->api & km);
     t.lr_status[c] = ST_Ok;
     uint64_t nw = s->api & ~km, x = s->api & km;
     while (x) {
@@ -535,18 +543,26 @@ static int init_states(const model *m, kstate *out) {
  * Returns -1 if both hold, else the index of the first violated invariant
  * in MC.cfg order (0 TypeOK, 1 OnlyOneVersion). */
 static int check_invariants_all(const model *m, const kstate *s);
-/* the invariants the config lists (MC.cfg:13-15); -1 = all hold */
+/* the invariants the config lists (MC.cfg:13-15); -1 = all hold.
+ * NoLostUpdate (index 2, build-defined; SURVEY §8(d) config 5's second
+ * variant) == ~lostUpdate, a history variable kept as bit 63 of api (free:
+ * apiState has |U| <= 32 bits with at most 3 readers) that APIStart sets
+ * when it applies an Update whose writer has not read any stored version of
+ * the object (KubeAPI.tla:733 without HasRead: variant 1 only). */
 static int check_invariants(const model *m, const kstate *s) {
-  int mask = 3 & ~m->cfg.skip_inv;
-  if (!mask) return -1;
-  kstate t = *s;
-  int r = check_invariants_all(m, &t);
-  if (r == 0 && !(mask & 1)) {               /* TypeOK fails but is not checked */
-    for (int id = 0; id < 2; id++)
-      if (popc64(s->api & m->idmask[id]) > 1) return (mask & 2) ? 1 : -1;
-    return -1;
+  int mask = 3 & ~m->cfg.skip_inv, r = -1;
+  if (mask) {
+    kstate t = *s;
+    r = check_invariants_all(m, &t);
+    if (r == 0 && !(mask & 1)) {               /* TypeOK fails but is not checked */
+      r = -1;
+      for (int id = 0; id < 2; id++)
+        if (popc64(s->api & m->idmask[id]) > 1) r = (mask & 2) ? 1 : -1;
+    } else if (r == 1 && !(mask & 2)) {
+      r = -1;
+    }
   }
-  if (r == 1 && !(mask & 2)) return -1;
+  if (r < 0 && m->cfg.lost_update && (s->api & KO_LOST_UPDATE)) r = 2;
   return r;
 }
 static int check_invariants_all(const model *m, const kstate *s) {
@@ -571,6 +587,7 @@ static int check_invariants_all(const model *m, const kstate *s) {
     if (popc64(s->api & m->idmask[id]) > 1) return 1;
   return -1;
 }
+
 
 /* --------------------------------------------------------- fingerprints */
 static inline uint64_t mix64(uint64_t z) {
@@ -755,7 +772,7 @@ static const char *STN[] = {"?", "\"Pending\"", "\"Ok\"", "\"Error\""};
 static const char *KN[] = {"defaultInitValue", "\"Secret\"", "\"PVC\""};
 static void put_state(const model *m, sbuf *b, const kstate *s) {
   char nb[32]; int first;
-  sb_put(b, "/\\ apiState = "); put_uset(m, b, s->api);
+  sb_put(b, "/\\ apiState = "); put_uset(m, b, s->api & m->allmask);
   sb_put(b, "\n/\\ requests = "); first = 1;
   for (int c = 0; c < m->P; c++) if (s->rq_present[c]) {
     sb_put(b, "%s\"%s\" :> [op |-> %s, obj |-> ", first ? "(" : " @@ ", pname(m, c, nb), OPN[s->rq_op[c]]);
@@ -780,6 +797,7 @@ static void put_state(const model *m, sbuf *b, const kstate *s) {
   sb_put(b, ")\n/\\ shouldReconcile = (");
   for (int p = 0; p < m->cfg.nc; p++) sb_put(b, "%s\"%s\" :> %s", p ? " @@ " : "", pname(m, p, nb), s->sr[p] ? "TRUE" : "FALSE");
   sb_put(b, ")\n");
+  if (m->cfg.lost_update) sb_put(b, "/\\ lostUpdate = %s\n", (s->api & KO_LOST_UPDATE) ? "TRUE" : "FALSE");
 }
 
 /* ------------------------------------------------------------------ BFS */
@@ -880,7 +898,7 @@ void *ko_run(const ko_config *cfg, ko_result *res) {
       pv_get(&cur, m, i, &scur);
       const kstate *s = &scur;
       /* per-distinct-state coverage sums (MC.out:1029-1080) */
-      int na = popc64(s->api);
+      int na = popc64(s->api & m->allmask);
       res->cov_api += na; res->cov_api2 += (uint64_t)na * na;
       for (int c = 0; c < m->P; c++) {
         res->cov_req += s->rq_present[c];

@@ -71,6 +71,8 @@ typedef struct {
   int progress;            /* print per-level progress to stderr */
   int skip_inv;            /* invariants NOT in the .cfg's INVARIANT list:
                               bit 0 TypeOK, bit 1 OnlyOneVersion (0 = check both) */
+  int lost_update;         /* 1: also check the build-defined NoLostUpdate, with its
+                              lostUpdate history variable (kubeapi_oracle.c) */
 } ko_config;
 
 enum { KO_OK = 0, KO_ERR_ASSERT = 1, KO_ERR_INVARIANT = 2, KO_ERR_DEADLOCK = 3,
@@ -98,7 +100,7 @@ typedef struct {
   int err_kind;            /* KO_ERR_* */
   int err_action;          /* action id for assertion failures */
   int err_self;            /* process index */
-  int err_invariant;       /* 0 TypeOK, 1 OnlyOneVersion */
+  int err_invariant;       /* 0 TypeOK, 1 OnlyOneVersion, 2 NoLostUpdate */
   int err_level;           /* BFS level of the last state of the trace */
   int trace_len;           /* states in the counterexample */
   double seconds;

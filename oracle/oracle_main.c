@@ -13,7 +13,7 @@
 #include <string.h>
 
 int main(int argc, char **argv) {
-  ko_config cfg = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 128, 0, 0, 0};
+  ko_config cfg = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 128, 0, 0, 0, 0};
   int print_trace = 0, threads = 0;
   double budget = 1e30;
   for (int i = 1; i < argc; i++) {
@@ -27,6 +27,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "-maxlevels") && i + 1 < argc) cfg.max_levels = atoi(argv[++i]);
     else if (!strcmp(argv[i], "-maxdistinct") && i + 1 < argc) cfg.max_distinct = strtoull(argv[++i], 0, 10);
     else if (!strcmp(argv[i], "-variant") && i + 1 < argc) cfg.variant = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "-lostupdate")) cfg.lost_update = 1;
     else if (!strcmp(argv[i], "-trace")) print_trace = 1;
     else if (!strcmp(argv[i], "-fp64")) cfg.fp_bits = 64;
     else if (!strcmp(argv[i], "-fpsetlog2") && i + 1 < argc) cfg.fpset_log2 = atoi(argv[++i]);

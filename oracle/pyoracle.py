@@ -35,7 +35,7 @@ class KoConfig(C.Structure):
                 ("can_timeout", C.c_int), ("check_deadlock", C.c_int), ("keep_trace", C.c_int),
                 ("max_levels", C.c_int), ("max_distinct", C.c_uint64), ("variant", C.c_int),
                 ("fp_bits", C.c_int), ("fpset_log2", C.c_int), ("progress", C.c_int),
-                ("skip_inv", C.c_int)]
+                ("skip_inv", C.c_int), ("lost_update", C.c_int)]
 
 
 class KoResult(C.Structure):
@@ -87,9 +87,11 @@ def lib():
 
 def config(nc=1, np_=1, ns=1, can_fail=True, can_timeout=True, check_deadlock=True,
            keep_trace=True, max_levels=0, variant=0, fp_bits=128, invariants=3) -> KoConfig:
-    """invariants: bit 0 TypeOK, bit 1 OnlyOneVersion (the .cfg INVARIANT list)."""
+    """invariants: bit 0 TypeOK, bit 1 OnlyOneVersion (the .cfg INVARIANT list),
+    bit 2 the build-defined NoLostUpdate (with its lostUpdate history variable)."""
     return KoConfig(nc, np_, ns, int(can_fail), int(can_timeout), int(check_deadlock),
-                    int(keep_trace), max_levels, 0, variant, fp_bits, 0, 0, 3 & ~invariants)
+                    int(keep_trace), max_levels, 0, variant, fp_bits, 0, 0, 3 & ~invariants,
+                    1 if invariants & 4 else 0)
 
 
 def run(cfg: KoConfig) -> dict:

@@ -205,3 +205,35 @@ def test_check_fps_min_gap():
     # 163,408 fingerprints spread over [1, 2^63): the minimum gap is far below
     # the mean spacing and far above 0 (TLC reports 9.9E-10, MC.out:42)
     assert 0 < gap < 2**63 // 163408 and prob == pytest.approx(1 / gap)
+
+
+# --- the resourceVersion race as an INVARIANT bug (BASELINE configs[4],
+# SURVEY §8(d) config 5's second variant): variant 1 drops HasRead from
+# Update (KubeAPI.tla:733), and the build-defined NoLostUpdate (invariants
+# bit 2, with its lostUpdate history variable) catches the lost update
+@pytest.mark.parametrize("key,kw", [("variant1_lost_update", dict(variant=1)),
+                                    ("np2_variant1_lost_update", dict(np=2, variant=1))])
+@pytest.mark.parametrize("mode", ["hbm", "frontier_spill", "seen_spill", "chunked"])
+def test_lost_update_invariant(fixtures, key, kw, mode):
+    fx = fixtures[key]
+    extra = {"hbm": {}, "frontier_spill": dict(frontier_hbm_bytes=32 << 10, frontier_segment_states=256),
+             "seen_spill": dict(seen_hbm_bytes=4 << 20), "chunked": dict(chunk_states=512)}[mode]
+    with ModelChecker(ModelConfig(invariants=7, **kw, **extra)) as mc:
+        r = mc.run()
+    assert r.error == "invariant" and r.error_invariant == "NoLostUpdate" and fx["err_invariant"] == 2
+    assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
+    assert [list(map(int, t)) for t in r.trace] == fx["trace"]
+    assert "lostUpdate = TRUE" in r.trace_text.split("State %d:" % r.trace_len)[1]
+    k = min(len(r.level_width), len(fx["level_width"]))
+    assert r.level_width[:k] == fx["level_width"][:k]
+
+
+def test_lost_update_holds_as_written(fixtures):
+    # KubeAPI.tla as written keeps NoLostUpdate, and checking it (the ghost
+    # present) leaves Model_1's state space exactly as MC.out has it
+    fx = fixtures["model1_lost_update_checked"]
+    r = run(invariants=7)
+    assert r.complete and r.error is None
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"]) == (
+        163408, 577736, 124)
+    assert r.act_dist == fx["act_dist"]

@@ -293,3 +293,15 @@ def test_native_fault_stops_every_rank(monkeypatch, stage, devrow):
         assert "injected fault" in str(e.value)
     finally:
         mc.close()
+
+
+@pytest.mark.parametrize("R", [1, 2, 3])
+def test_native_lost_update_invariant(fixtures, R):
+    # NoLostUpdate (build-defined; variant 1 = Update without HasRead) through
+    # the sharded loop: same error, level and trace length as the oracle
+    fx = fixtures["variant1_lost_update"]
+    r = native(R, variant=1, invariants=7)
+    assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate"
+    assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
+    if R == 1:
+        assert r["trace"] == fx["trace"]

@@ -88,3 +88,26 @@ def test_tuple_outside_domain_rejected():
     bad[0] = 1 << 40                                          # apiState bit beyond |U|
     with pytest.raises(Exception):
         sp.successors(bad)
+
+
+def test_lost_update_ghost_matches_oracle(oracle, fixtures):
+    # variant 1 (Update without HasRead, KubeAPI.tla:733) with the
+    # build-defined NoLostUpdate: the lostUpdate history variable and its
+    # successors agree with the oracle state by state up to the level before
+    # the violation, and the oracle's counterexample replays through the
+    # product's spec, ending in the state that breaks NoLostUpdate
+    _, widths, failure = _bfs_compare(oracle, 1, 1, 1, max_levels=25, variant=1, invariants=7)
+    fx = fixtures["variant1_lost_update"]
+    assert widths == fx["level_width"][:25] and failure is None
+    sp = Spec(ModelConfig(variant=1, invariants=7))
+    tr = [np.array(t, dtype=np.uint64) for t in fx["trace"]]
+    for a, b in zip(tr, tr[1:]):
+        succ, _ = sp.successors(a)
+        assert any(np.array_equal(x, b) for _, x in succ)
+        assert sp.check_invariants(a) is None
+    assert sp.check_invariants(tr[-1]) == "NoLostUpdate"
+    assert int(tr[-1][0]) >> 63 == 1                          # lostUpdate: bit 63 of the apiState word
+    # without the check the ghost does not exist: the same Update leaves no trace
+    plain = Spec(ModelConfig(variant=1))
+    succ, _ = plain.successors(tr[-2])
+    assert all(int(x[0]) >> 63 == 0 for _, x in succ)

@@ -62,6 +62,6 @@ class EngineBase {
 std::unique_ptr<EngineBase> make_engine(const kc_model_config& cfg);
 const char* action_name(int a);
 // TLA+-style rendering of a canonical tuple (spec_abi.cpp)
-std::string format_tuple(const uint64_t* tuple, int nc, int np, int ns);
+std::string format_tuple(const uint64_t* tuple, int nc, int np, int ns, bool ghost = false);
 
 }  // namespace kc

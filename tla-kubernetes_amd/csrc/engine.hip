@@ -323,6 +323,7 @@ class EngineT final : public EngineBase {
         }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+        KC_TRY(cand_overflow(cand, level, n));
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
@@ -334,6 +335,7 @@ class EngineT final : public EngineBase {
         ++res->levels_chunks;
         const unsigned grid = (unsigned)((cn + 255) / 256);
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
+        KC_HIP_TRY(hipMemsetAsync(claim_args_.ovf.count, 0, 8, st_));
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
@@ -360,9 +362,13 @@ class EngineT final : public EngineBase {
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+          hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start,
+                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
                              tscan_ ? ttot_ : (uint32_t*)nullptr);
+          hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start,
+                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, tscan_ ? ttot_ : (uint32_t*)nullptr);
         });
         if (tscan_) {
           timed(KK_SCAN, [&] {
@@ -729,6 +735,8 @@ class EngineT final : public EngineBase {
     res->fpset_probes = h_ctr_->probes() + narrow_probes_;
     for (int b = 0; b < OUTDEG_BINS; ++b) res->outdeg_hist[b] = h_ctr_->outdeg(b);
     res->batch_inserts = h_ctr_->settles();
+    res->cand_overflow_records = h_ctr_->cand_ovf();
+    res->cand_buffer_peak_bytes = cand_buf_peak_;
     if (spill_) {
       ColdStats cst;
       cold_.stats(&cst);
@@ -766,6 +774,8 @@ class EngineT final : public EngineBase {
       parent_ = nullptr;
       ord_ = nullptr;
     }
+    for (void* p : {(void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_})
+      if (p) (void)hipFree(p);
     if (sp_arena_) (void)hipFree(sp_arena_);
     if (sp_tsum_) (void)hipFree(sp_tsum_);
     if (d_spctr_) (void)hipFree(d_spctr_);
@@ -874,6 +884,30 @@ class EngineT final : public EngineBase {
     }
     return 0;
   }
+
+  // The chunk's candidate overflow list (engine_kernels.h CandOvf), sized by
+  // the level's successor count `bound` (no chunk of the level has more), and
+  // the peak of the candidate buffers (verbose: per level).
+  int cand_overflow(uint64_t bound, int level, uint64_t n) {
+    bound = std::max<uint64_t>(bound, 1);
+    KC_TRY(grow_buffer_tight(ovf_fp_, ovf_fp_cap_, bound, st_));
+    KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
+    KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
+    if (!d_ovf_cnt_) KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
+    claim_args_.ovf = CandOvf{d_ovf_cnt_, ovf_fp_, ovf_lk_, ovf_tile_,
+                              std::min(ovf_fp_cap_, std::min(ovf_lk_cap_, ovf_tile_cap_))};
+    const uint64_t b = rcount_cap_ * 4 + rec_fp_cap_ * 8 + rec_lk_cap_ * 4 + ovf_fp_cap_ * 8 + ovf_lk_cap_ * 4 +
+                       ovf_tile_cap_ * 4;
+    cand_buf_peak_ = std::max(cand_buf_peak_, b);
+    if (cfg_.verbose)
+      fprintf(stderr, "kubecheck: level %d width %llu: candidate buffers %.1f MiB (%.1f B per parent)\n", level,
+              (unsigned long long)n, b / 1048576.0, n ? (double)b / (double)n : 0.0);
+    return 0;
+  }
+  unsigned long long* ovf_fp_ = nullptr;
+  unsigned int *ovf_lk_ = nullptr, *ovf_tile_ = nullptr;
+  uint64_t ovf_fp_cap_ = 0, ovf_lk_cap_ = 0, ovf_tile_cap_ = 0, cand_buf_peak_ = 0;
+  unsigned long long* d_ovf_cnt_ = nullptr;
 
   // ---- seen-set spill (cfg.seen_hbm_bytes > 0; engine_spill.h, coldset.h).
   // HBM budget B: the hot ClaimSet takes the largest power-of-two table of
@@ -1116,6 +1150,7 @@ class EngineT final : public EngineBase {
         }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+        KC_TRY(cand_overflow(cand, level, n));
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, cmax, false, st_));
       KC_TRY(grow_buffer(offsets_, off_cap_, cmax, false, st_));
@@ -1158,6 +1193,7 @@ class EngineT final : public EngineBase {
         const State* cur = reinterpret_cast<const State*>(p);
         ++res->levels_chunks;
         const unsigned tiles = (unsigned)((m + CLAIM_TILE - 1) / CLAIM_TILE);
+        KC_HIP_TRY(hipMemsetAsync(claim_args_.ovf.count, 0, 8, st_));
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur, m, start, flags_,
                              cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level, abl_mask_, rcount_, rec_fp_,
@@ -1166,8 +1202,12 @@ class EngineT final : public EngineBase {
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+          hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
+                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+          hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
+                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
         });
         size_t tmp_bytes = 0;
         const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
@@ -1366,7 +1406,7 @@ size_t EngineT<M>::trace_text(char* buf, size_t cap) const {
     s += "State " + std::to_string(i + 1) + ":\n";
     std::vector<uint64_t> t(M::TUPLE_WORDS);
     M::to_tuple(trace_[i], t.data());
-    s += format_tuple(t.data(), cfg_.nc, cfg_.np, cfg_.ns);
+    s += format_tuple(t.data(), cfg_.nc, cfg_.np, cfg_.ns, (cfg_.invariants & 4) != 0);
     s += "\n";
   }
   if (buf && cap) {

@@ -41,7 +41,8 @@ struct CtrStripe {                  // 1 KiB
   // CL_NEW) and CL_OLD outcomes by level distance (1, 2, 3, 4, 5-8, 9-16, 17+)
   unsigned long long claim_out[4];
   unsigned long long old_dist[8];
-  unsigned long long pad[128 - 2 * A_COUNT - 15 - OUTDEG_BINS];
+  unsigned long long cand_ovf;      // candidate records that went to the overflow list
+  unsigned long long pad[128 - 2 * A_COUNT - 16 - OUTDEG_BINS];
 };
 struct Counters {
   unsigned long long err_key;     // min error key of the level (~0 = none)
@@ -57,6 +58,7 @@ struct Counters {
   unsigned long long act_dist(int a) const { return sum(&CtrStripe::act_dist, a); }
   unsigned long long probes() const { return sum1(&CtrStripe::probes); }
   unsigned long long settles() const { return sum1(&CtrStripe::settles); }
+  unsigned long long cand_ovf() const { return sum1(&CtrStripe::cand_ovf); }
   unsigned long long next_cand() const { return sum1(&CtrStripe::next_cand); }
   unsigned long long outdeg(int b) const {
     unsigned long long t = 0;
@@ -143,19 +145,41 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 constexpr int CLAIM_TILE = 256;
 constexpr int CLAIM_LDS_BITS = 11;
 constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
-// Candidate records per tile (claimants whose claim may win): fp + tile-local
-// key (bit 31: set by settle pass A on a displacer).  A tile has at most
-// CLAIM_TILE * 32 successors, so the list cannot overflow.
-constexpr int CLAIM_RCAP = CLAIM_TILE * 32;
+// Candidate records (claimants whose claim may win): fp + tile-local key
+// (bit 31: set by settle pass A on a displacer).  Each tile keeps its first
+// CLAIM_RCAP in its own segment (12 B per parent); the rest of a busy tile's
+// go to one overflow list shared by the chunk, {fp, key, tile}, sized by the
+// chunk's successor count (an exact upper bound), so it cannot overflow
+// either.  (A segment of CLAIM_TILE * 32 per tile, the worst case, cost 384 B
+// per parent: 6 GB at NP=2's widest level for ~0.1 candidate per parent.)
+constexpr int CLAIM_RCAP = 256;
 constexpr unsigned int CAND_DISPLACER = 1u << 31;
+struct CandOvf {
+  unsigned long long* count = nullptr;   // records pushed (may exceed cap: then C->overflow)
+  unsigned long long* fp = nullptr;
+  unsigned int* lk = nullptr;
+  unsigned int* tile = nullptr;
+  uint64_t cap = 0;
+};
 
 __device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t tile,
                                                unsigned long long* __restrict__ rec_fp,
                                                unsigned int* __restrict__ rec_lk, uint64_t fp,
-                                               unsigned int lk) {
+                                               unsigned int lk, const CandOvf& ovf, Counters* __restrict__ C) {
   const unsigned int k = atomicAdd(sh_rc, 1u);
-  rec_fp[tile * CLAIM_RCAP + k] = fp;
-  rec_lk[tile * CLAIM_RCAP + k] = lk;
+  if (k < (unsigned)CLAIM_RCAP) {
+    rec_fp[tile * CLAIM_RCAP + k] = fp;
+    rec_lk[tile * CLAIM_RCAP + k] = lk;
+    return;
+  }
+  const unsigned long long g = ovf.count ? atomicAdd(ovf.count, 1ull) : ~0ull;
+  if (g < ovf.cap) {
+    ovf.fp[g] = fp;
+    ovf.lk[g] = lk;
+    ovf.tile[g] = (unsigned int)tile;
+  } else {
+    atomicAdd(&C->overflow, 1ull);
+  }
 }
 
 // The LDS table of the sharded variant is smaller (CLAIM_LDS_SH entries):
@@ -191,11 +215,14 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
 // exchange.  Claim keys carry the rank above the parent index.
 constexpr int CLAIM_RANK_SHIFT = 40;
 constexpr uint32_t CLAIM_SPREAD = 768;   // k_claim tile-order columns (spread_tile)
+// (k_claim's per-launch arguments beyond the engine's: owner sharding, the
+// tile order, and the candidate overflow list)
 struct ShardArgs {
   uint32_t world = 1, rank = 0;
   uint32_t spread = CLAIM_SPREAD; // tile order strided by `spread` (spread_tile); 0 = block order
   uint32_t* repmask = nullptr;   // [n]: remote representatives of each parent
   uint32_t* cnt = nullptr;       // [world][n]: remote representatives per owner and parent
+  CandOvf ovf;
 };
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
 // workgroups resident together (~1,536: 6 per CU) work on tiles spread over
@@ -332,7 +359,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         if (r == CL_NEW)
           atomicOr(&sh_cur[threadIdx.x], 1u << t);
         else if (r == CL_CUR)
-          push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t);
+          push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t, sh.ovf, C);
         else if (r == CL_FULL)
           atomicAdd(&C->overflow, 1ull);
       }
@@ -391,12 +418,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     if (r == CL_NEW)
       atomicOr(&sh_cur[lp], 1u << t);
     else if (r == CL_CUR)
-      push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk);
+      push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk, sh.ovf, C);
     else if (r == CL_FULL)
       atomicAdd(&C->overflow, 1ull);
   }
   __syncthreads();
-  if (threadIdx.x == 0) rcount[tile] = sh_rc;
+  if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
   if (live) newmask[i] = sh_cur[threadIdx.x];
   if (SH && live) {
     sh.repmask[i] = sh_rep[threadIdx.x];
@@ -461,6 +488,33 @@ __device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_
 // the input of k_tile_scan.
 // (The body takes the tile index, so the sharded insert can run it in one
 // launch with the records' settle pass.)
+// One candidate record of tile `tile`.  PASS 0 folds its claim into its
+// slot (a displacer flags itself in *lkp); PASS 1 a displacer whose claim is
+// still the stored one sets its newmask bit.  Returns 1 for a record it
+// processed (PASS 1: 2 for a winner), 0 for one PASS 1 skips.
+template <int PASS>
+__device__ __forceinline__ int settle_record(uint32_t tile, unsigned long long fp, unsigned int* lkp, uint64_t n,
+                                             uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+                                             uint32_t level, uint32_t* __restrict__ newmask, Counters* __restrict__ C,
+                                             uint32_t rank) {
+  const unsigned int lk = *lkp;
+  if (PASS == 1 && !(lk & CAND_DISPLACER)) return 0;
+  const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
+  const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
+  const uint64_t claim = make_claim(level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | ((base + tile0 + lp) << 8) | t);
+  if (PASS == 0) {
+    const unsigned long long prev = claimset_store_claim(cs, nbuckets, fp, claim);
+    if (prev < ~claim)                           // displaced ~prev (or found no claim)
+      settle_displace(prev, level, rank, base, n, newmask, C, lkp, lk | CAND_DISPLACER);
+    return 1;
+  }
+  if (~claimset_get(cs, nbuckets, fp) == claim) {
+    atomicOr(&newmask[tile0 + lp], 1u << t);     // a candidate's bit is never set before
+    return 2;
+  }
+  return 1;
+}
+
 template <int PASS>
 __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs,
                                             uint64_t nbuckets, uint32_t level, const unsigned int* __restrict__ rcount,
@@ -478,21 +532,9 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
   }
   for (unsigned int k = threadIdx.x; k < cnt; k += CLAIM_TILE) {
     const uint64_t r = (uint64_t)tile * CLAIM_RCAP + k;
-    const unsigned int lk = rec_lk[r];
-    if (PASS == 1 && !(lk & CAND_DISPLACER)) continue;
-    const unsigned long long fp = rec_fp[r];
-    const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
-    const uint64_t claim =
-        make_claim(level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | ((base + tile0 + lp) << 8) | t);
-    ++reads;
-    if (PASS == 0) {
-      const unsigned long long prev = claimset_store_claim(cs, nbuckets, fp, claim);
-      if (prev < ~claim)                         // displaced ~prev (or found no claim)
-        settle_displace(prev, level, rank, base, n, newmask, C, &rec_lk[r], lk | CAND_DISPLACER);
-    } else if (~claimset_get(cs, nbuckets, fp) == claim) {
-      atomicOr(&newmask[tile0 + lp], 1u << t);   // a candidate's bit is never set before
-      ++newc;
-    }
+    const int v = settle_record<PASS>(tile, rec_fp[r], &rec_lk[r], n, base, cs, nbuckets, level, newmask, C, rank);
+    reads += v ? 1u : 0u;
+    newc += v == 2 ? 1u : 0u;
   }
   unsigned long long rw = reads;
 #pragma unroll
@@ -511,6 +553,29 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
     }
   }
 }
+// The same passes over the chunk's overflow list (after k_settle_rec<PASS>:
+// a PASS-1 winner then adds itself to its tile's count).
+template <int PASS>
+static __global__ void __launch_bounds__(256)
+k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ tile_total) {
+  const unsigned long long c = *ovf.count;
+  const uint64_t cnt = c < ovf.cap ? c : ovf.cap;
+  if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&stripe(C).cand_ovf, (unsigned long long)cnt);
+  unsigned long long reads = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned int tile = ovf.tile[k];
+    const int v = settle_record<PASS>(tile, ovf.fp[k], &ovf.lk[k], n, base, cs, nbuckets, level, newmask, C, rank);
+    reads += v ? 1 : 0;
+    if (v == 2 && tile_total) atomicAdd(&tile_total[tile], 1u);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) reads += __shfl_down(reads, off, 64);
+  if ((threadIdx.x & 63) == 0 && reads) atomicAdd(&stripe(C).settles, reads);
+}
+constexpr unsigned SETTLE_OVF_GRID = 1024;
+
 template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,

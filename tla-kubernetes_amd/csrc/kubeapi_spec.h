@@ -73,12 +73,25 @@ enum ErrKind : int { E_NONE = 0, E_ASSERT = 1, E_INVARIANT = 2, E_DEADLOCK = 3 }
 //   4 = list replies ignore the kind filter (:747)      -> TypeOK (:433-435)
 //   5 = Init store already holds two Secret versions    -> Init violates
 //       (a pre-corrupted apiState, :456)                   OnlyOneVersion
+//
+// NoLostUpdate (build-defined, inv_mask bit 2; SURVEY §8(d) config 5's
+// second variant): the optimistic-concurrency guarantee HasRead gives Update
+// (:733) — no Update overwrites a version its writer has not read.  It needs
+// a history variable: lostUpdate (a ghost, FALSE in Init) becomes TRUE when
+// APIStart applies an Update whose writer has not read any stored version of
+// the object (only variant 1 can), and NoLostUpdate == ~lostUpdate.  The
+// ghost exists only in runs that check NoLostUpdate, and stays FALSE in
+// every reachable state of KubeAPI.tla as written, so those state spaces are
+// unchanged.  It is bit 63 of word 0 (apiState holds |U| <= 32 bits when
+// there are at most 3 actors; with 4 the invariant is unavailable).
 struct Flags {
   int can_fail;      // REQUESTS_CAN_FAIL
   int can_timeout;   // REQUESTS_CAN_TIMEOUT
   int variant;
-  int inv_mask = 3;  // invariants checked (MC.cfg INVARIANT): bit 0 TypeOK, bit 1 OnlyOneVersion
+  int inv_mask = 3;  // invariants checked (MC.cfg INVARIANT): bit 0 TypeOK, bit 1 OnlyOneVersion,
+                     // bit 2 NoLostUpdate (build-defined)
 };
+constexpr uint64_t GHOST_LOST = 1ull << 63;   // lostUpdate (word 0; see above)
 
 KC_HD constexpr int ceil_log2(int x) { return x <= 1 ? 0 : 1 + ceil_log2((x + 1) / 2); }
 
@@ -581,10 +594,15 @@ struct Model {
           break;
         case OP_Delete: nw = api & ~same; break;                // :729-731
         default: {                                              // Update :732-739
-          bool ok = false;
-          for (uint64_t x = same; x; x &= x - 1)
-            if (f.variant == 1 || ((u_vv(ctz(x)) >> c) & 1)) ok = true;   // HasRead
+          bool ok = false, read = false;
+          for (uint64_t x = same; x; x &= x - 1) {
+            const bool hr = (u_vv(ctz(x)) >> c) & 1;            // HasRead
+            read |= hr;
+            if (f.variant == 1 || hr) ok = true;
+          }
           if (ok) nw = (api & ~same) | (1ull << write_u(oc)); else st = ST_Error;
+          // lostUpdate' (the NoLostUpdate ghost): an Update applied unread
+          if (U < 64 && (f.inv_mask & 4) && ok && !read) nw |= GHOST_LOST;
         }
       }
       t.w[0] = nw;
@@ -616,9 +634,10 @@ struct Model {
   }
 
   // ------------------------------------------------------------ invariants
-  // Returns -1 if TypeOK (:776-781) and OnlyOneVersion (:787-789) hold, else
-  // the index of the first violated one in MC.cfg order (0 TypeOK, 1 OOV);
-  // only the invariants in `mask` (Flags::inv_mask) are evaluated.
+  // Returns -1 if TypeOK (:776-781), OnlyOneVersion (:787-789) and (bit 2)
+  // the build-defined NoLostUpdate hold, else the index of the first violated
+  // one in MC.cfg order (0 TypeOK, 1 OOV, 2 NoLostUpdate); only the
+  // invariants in `mask` (Flags::inv_mask) are evaluated.
   KC_HD static int check(const State& s, int mask = 3) {
     if (!mask) return -1;
     bool typeok = true;
@@ -637,6 +656,7 @@ struct Model {
     });
     if (!typeok && (mask & 1)) return 0;
     if ((mask & 2) && (popc(s.w[0] & id_mask(0)) > 1 || popc(s.w[0] & id_mask(1)) > 1)) return 1;
+    if (U < 64 && (mask & 4) && (s.w[0] & GHOST_LOST)) return 2;
     return -1;
   }
 
@@ -784,7 +804,7 @@ struct Model {
   // returns false if the tuple is outside the lowered domain
   static bool from_tuple(const uint64_t* o, State& s) {
     for (int i = 0; i < W; ++i) s.w[i] = 0;
-    if (o[0] & ~UMASK) return false;
+    if (o[0] & ~(UMASK | (U < 64 ? GHOST_LOST : 0ull))) return false;   // (lostUpdate: bit 63)
     s.w[0] = o[0];
     for (int p = 0; p < P; ++p) {
       const uint64_t* q = o + 1 + TUPLE_PER_PROC * p;

@@ -487,6 +487,17 @@ class ShardT final : public ShardBase {
     KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
     KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
     KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+    // candidates past a tile's segment: one overflow list, bounded by the
+    // level's successor count
+    {
+      const uint64_t bound = std::max<uint64_t>(cand_, 1);
+      KC_TRY(grow_buffer_tight(ovf_fp_, ovf_fp_cap_, bound, st_));
+      KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
+      KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
+      if (!d_ovf_cnt_) KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
+      ovf_ = CandOvf{d_ovf_cnt_, ovf_fp_, ovf_lk_, ovf_tile_, std::min(ovf_fp_cap_, std::min(ovf_lk_cap_, ovf_tile_cap_))};
+      KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
+    }
     KC_TRY(grow_buffer(newmask_, mask_cap_, n_, false, st_));
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
@@ -496,6 +507,7 @@ class ShardT final : public ShardBase {
     sh.rank = (uint32_t)rank_;
     sh.repmask = repmask_;
     sh.cnt = cnt_;
+    sh.ovf = ovf_;
     const size_t dyn = (size_t)(CLAIM_TILE + ((world_ + 3) / 4) * CLAIM_TILE) * sizeof(unsigned int);
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[0], st_));
     if (world_ == 1) {
@@ -504,7 +516,7 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL((k_claim<M, 0, false>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
-                         d_ctr_, ShardArgs{});
+                         d_ctr_, sh);
     } else {
       hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
@@ -661,9 +673,15 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
                          succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
                          isnew_, d_ctr_);
+      if (lt)
+        hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
+                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, (uint32_t*)nullptr);
       hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
                          succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
                          isnew_, d_ctr_);
+      if (lt)
+        hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
+                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, (uint32_t*)nullptr);
     }
     // positions: this rank's own winners first, then the records'
     size_t tmp_bytes = 0;
@@ -763,6 +781,7 @@ class ShardT final : public ShardBase {
     (void)hipSetDevice(cfg_.device);
     cs_.release();
     for (void* p : {(void*)cur_, (void*)next_, (void*)pkeys_, (void*)cnt_, (void*)off_,
+                    (void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_,
                     (void*)repmask_, (void*)newmask_, (void*)offsets_, (void*)rcount_, (void*)rec_fp_,
                     (void*)rec_lk_, (void*)rfp_, (void*)flag_, (void*)isnew_, (void*)ioff_,
                     (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_})
@@ -790,6 +809,11 @@ class ShardT final : public ShardBase {
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
   uint64_t rcount_cap_ = 0, rec_fp_cap_ = 0, rec_lk_cap_ = 0;
+  CandOvf ovf_{};
+  unsigned long long* ovf_fp_ = nullptr;
+  unsigned int *ovf_lk_ = nullptr, *ovf_tile_ = nullptr;
+  uint64_t ovf_fp_cap_ = 0, ovf_lk_cap_ = 0, ovf_tile_cap_ = 0;
+  unsigned long long* d_ovf_cnt_ = nullptr;
   // insert: per received record
   unsigned long long* rfp_ = nullptr;
   unsigned int* flag_ = nullptr;

@@ -94,13 +94,13 @@ struct Printer {
 
 }  // namespace
 
-std::string format_tuple(const uint64_t* t, int nc, int np, int ns) {
+std::string format_tuple(const uint64_t* t, int nc, int np, int ns, bool ghost) {
   Printer pr{nc, np, ns, nc + np, {}};
   const int P = nc + np + ns;
   auto q = [&](int p, int k) { return t[1 + 19 * p + k]; };
   std::string& s = pr.s;
   s += "/\\ apiState = ";
-  pr.uset(t[0]);
+  pr.uset(t[0] & ~GHOST_LOST);
   s += "\n/\\ requests = ";
   bool first = true;
   for (int p = 0; p < P; ++p) {
@@ -154,6 +154,8 @@ std::string format_tuple(const uint64_t* t, int nc, int np, int ns) {
     s += "\"" + pr.pn(p) + "\" :> " + (q(p, 4) ? "TRUE" : "FALSE");
   }
   s += ")\n";
+  // the history variable of the build-defined NoLostUpdate (kubeapi_spec.h)
+  if (ghost) s += std::string("/\\ lostUpdate = ") + ((t[0] & GHOST_LOST) ? "TRUE" : "FALSE") + "\n";
   return s;
 }
 

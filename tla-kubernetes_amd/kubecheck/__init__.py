@@ -111,6 +111,8 @@ class CheckResult:
     frontier_reloaded_bytes: int = 0
     frontier_peak_hbm_bytes: int = 0
     seen: Dict[str, float] = field(default_factory=dict)   # seen-set spill statistics (seen_* fields)
+    cand_overflow_records: int = 0
+    cand_buffer_peak_bytes: int = 0
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -137,7 +139,8 @@ def _result(r: KcResult) -> CheckResult:
         outdeg_hist=[int(x) for x in r.outdeg_hist],
         frontier_spilled_bytes=r.frontier_spilled_bytes, frontier_reloaded_bytes=r.frontier_reloaded_bytes,
         frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes,
-        seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")})
+        seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")},
+        cand_overflow_records=r.cand_overflow_records, cand_buffer_peak_bytes=r.cand_buffer_peak_bytes)
 
 
 class ModelChecker:

@@ -23,7 +23,7 @@ ACTIONS = [
 ]
 
 ERR_KINDS = {0: None, 1: "assertion", 2: "invariant", 3: "deadlock"}
-INVARIANTS = {0: "TypeOK", 1: "OnlyOneVersion"}
+INVARIANTS = {0: "TypeOK", 1: "OnlyOneVersion", 2: "NoLostUpdate"}
 
 
 class KcModelConfig(C.Structure):
@@ -57,6 +57,7 @@ class KcResult(C.Structure):
         ("seen_cold_queries", C.c_uint64), ("seen_cold_hits", C.c_uint64), ("seen_merges", C.c_uint64),
         ("seen_filter_tests", C.c_uint64), ("seen_filter_passed", C.c_uint64),
         ("seen_disk_bytes", C.c_uint64), ("seen_peak_hbm_bytes", C.c_uint64), ("seen_seconds", C.c_double),
+        ("cand_overflow_records", C.c_uint64), ("cand_buffer_peak_bytes", C.c_uint64),
     ]
 
 

@@ -27,6 +27,10 @@ import time
 from typing import Dict, List, Optional
 
 KNOWN_INVARIANTS = ("TypeOK", "OnlyOneVersion")          # KubeAPI.tla:776,787
+# build-defined (not in KubeAPI.tla): no Update overwrites a version its
+# writer has not read (the optimistic concurrency HasRead gives Update,
+# :733), with its lostUpdate history variable; run with -variant 1 it fails
+BUILD_INVARIANTS = ("NoLostUpdate",)
 KNOWN_CONSTANTS = ("REQUESTS_CAN_FAIL", "REQUESTS_CAN_TIMEOUT", "defaultInitValue")  # :4-6,374
 
 
@@ -88,9 +92,10 @@ def model_from_cfg(cfg: dict) -> dict:
     """Validate a parsed cfg against KubeAPI.tla and map it to ModelConfig kwargs."""
     if cfg["specification"] not in (None, "Spec"):
         raise CfgError(f"SPECIFICATION {cfg['specification']}: only Spec (KubeAPI.tla:765)")
-    bad = [x for x in cfg["invariants"] if x not in KNOWN_INVARIANTS]
+    bad = [x for x in cfg["invariants"] if x not in KNOWN_INVARIANTS + BUILD_INVARIANTS]
     if bad:
-        raise CfgError(f"unknown invariant(s) {bad}; KubeAPI.tla defines {KNOWN_INVARIANTS}")
+        raise CfgError(f"unknown invariant(s) {bad}; KubeAPI.tla defines {KNOWN_INVARIANTS}"
+                       f" (and the build {BUILD_INVARIANTS})")
     if cfg["properties"]:
         raise CfgError("temporal PROPERTY checking (liveness) is out of scope")
     kw = {}
@@ -104,7 +109,8 @@ def model_from_cfg(cfg: dict) -> dict:
         raise CfgError(f"unknown CONSTANT(s) {sorted(unknown)}")
     # the INVARIANT list selects the checks (an empty list checks none, as in TLC)
     kw["invariants"] = (1 if "TypeOK" in cfg["invariants"] else 0) | \
-        (2 if "OnlyOneVersion" in cfg["invariants"] else 0)
+        (2 if "OnlyOneVersion" in cfg["invariants"] else 0) | \
+        (4 if "NoLostUpdate" in cfg["invariants"] else 0)
     return kw
 
 

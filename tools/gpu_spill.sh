@@ -11,6 +11,9 @@ export TMPDIR=/tmp
 echo "== host_probe $(date +%T)"
 timeout -k 10 240 ./tools/microbench/host_probe > $O/host_probe.txt 2>&1 || { echo PROBE_FAIL; tail -20 $O/host_probe.txt; exit 1; }
 cat $O/host_probe.txt
+echo "== engine tests $(date +%T)"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py tests/test_tlc_cli.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/engine_tests.log 2>&1 || { echo ENGINE_FAIL; tail -60 $O/engine_tests.log; exit 1; }
+tail -3 $O/engine_tests.log
 echo "== shard tests $(date +%T)"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py -x -v -k "native" --timeout 300 --timeout-method thread > $O/shard_tests.log 2>&1 || { echo SHARD_FAIL; tail -60 $O/shard_tests.log; exit 1; }
 tail -5 $O/shard_tests.log

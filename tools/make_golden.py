@@ -152,6 +152,18 @@ def oracle_fixtures(with_np2: bool) -> dict:
     fx["variant2"]["err_invariant"] = r["err_invariant"]
     fx["variant2"]["trace"] = [[int(x) for x in t] for t in r["trace"]]
     fx["variant1"] = summary(O.run(O.config(variant=1)))  # Update without HasRead
+    # the lost update as an invariant violation (SURVEY §8(d) config 5's
+    # second variant): the build-defined NoLostUpdate (bit 2) with its
+    # lostUpdate history variable; KubeAPI.tla as written keeps it (the
+    # state space is Model_1's), variant 1 breaks it
+    for key, cfg in (("variant1_lost_update", O.config(variant=1, invariants=7)),
+                     ("np2_variant1_lost_update", O.config(np_=2, variant=1, invariants=7)),
+                     ("nc2np0_variant1_lost_update", O.config(nc=2, np_=0, variant=1, invariants=7))):
+        r = O.run(cfg)
+        fx[key] = summary(r)
+        fx[key]["err_invariant"] = r["err_invariant"]
+        fx[key]["trace"] = [[int(x) for x in t] for t in r["trace"]]
+    fx["model1_lost_update_checked"] = summary(O.run(O.config(invariants=7)))
     # seeded bugs that exercise the other error paths (kubeapi_spec.h Flags):
     # 3 = C2 Assert (KubeAPI.tla:598-599), 4 = TypeOK, 5 = Init violates
     # OnlyOneVersion; ns=0 (no API server) deadlocks (launch:16)
