@@ -160,14 +160,24 @@ def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     return None, None
 
 
-def host_cores() -> int:
-    """Threads for the CPU comparator: this process's CPUs, at most 16 (the
-    GPU box's CPU share per GPU; os.cpu_count() there shows the whole host)."""
+def host_cpu_info() -> dict:
+    """The host CPUs the comparator may use: this process's affinity set, the
+    machine's count, and the per-GPU share the GPU box grants (its
+    OMP_NUM_THREADS, 16: os.cpu_count() there shows the whole host, whose
+    other CPUs belong to the other GPUs' jobs)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+    return {"affinity_cpus": aff, "machine_cpus": os.cpu_count() or aff, "per_gpu_share": share,
+            "threads": max(1, min(share, aff))}
+
+
+def host_cores() -> int:
+    """Threads for the CPU comparator: this process's CPUs, capped at the
+    box's per-GPU CPU share (host_cpu_info)."""
+    return host_cpu_info()["threads"]
 
 
 def cpu_model() -> str:
@@ -187,13 +197,16 @@ def cpu_baseline(kw, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    threads = host_cores()
+    info = host_cpu_info()
+    threads = info["threads"]
     cfg = pyoracle.config(kw["nc"], kw["np"], kw["ns"], keep_trace=False)
     cfg.fpset_log2 = 22 if (kw["nc"], kw["np"], kw["ns"]) == (1, 1, 1) else 29
     r = pyoracle.bench_parallel(cfg, threads, seconds)
     what = "the whole model" if r["complete"] else f"{r['levels']} BFS levels from Init"
     out = {"value": round(r["rate"], 1), "unit": "distinct states/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model(),
+           "cpu_model": cpu_model(), "host_cpus": info,
+           "cores_note": f"{threads} threads = min(this process's {info['affinity_cpus']} affinity CPUs, the box's "
+                         f"per-GPU CPU share {info['per_gpu_share']}); the machine has {info['machine_cpus']}",
            "sample": f"oracle/kubeapi_oracle.c ko_bench_parallel: level-synchronous BFS of the same "
                      f"model on {threads} threads with a lock-free 64-bit fingerprint set, {what} "
                      f"({r['distinct']} distinct, {r['generated']} generated) in {r['seconds']:.1f} s"}
@@ -324,7 +337,7 @@ def bench_fpset(args):
     s.close()
     traffic, tsrc = pmc_traffic("fpset", "k_stress_insert")
     gbs = n * args.steps * 64 / tin / 1e9
-    return {
+    out = {
         "metric": "FPSet probe HBM GB/s (insert)", "value": round(gbs, 1), "unit": "GB/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(tin * 1e3 / args.steps, 3), "higher_is_better": True,
@@ -341,6 +354,31 @@ def bench_fpset(args):
                      "traffic_unit": "HBM bytes per launch (PMC, one launch = one batch)",
                      "traffic_source": tsrc},
     }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_fpset(args.fp_load)
+    return out
+
+
+def cpu_baseline_fpset(load: float) -> dict:
+    """The FPSet stress on the host: the same
+    open-addressing set shape in host RAM, filled by all the comparator's
+    threads with lock-free CAS inserts (oracle/fpset_cpu.c), on a bounded
+    sample of 2^28 fingerprints (a 4 GiB table at 50% load)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    info = host_cpu_info()
+    n = 1 << 28
+    r = pyoracle.fpset_stress_cpu(n, load, info["threads"])
+    if r["inserted"] != n or r["found"] != n // 2:
+        raise RuntimeError(f"fpset cpu comparator: {r}")
+    return {"value": round(r["inserts_per_s"] * 64 / 1e9, 2), "unit": "GB/s", "cores": info["threads"],
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus": info,
+            "inserts_per_s": round(r["inserts_per_s"], 1), "lookups_per_s": round(r["lookups_per_s"], 1),
+            "sample": f"oracle/fpset_cpu.c: {n} distinct fingerprints inserted by {info['threads']} threads "
+                      f"(lock-free CAS, linear probing) into a {r['slots'] * 8 >> 20} MiB host table to "
+                      f"{load:.0%} load in {r['insert_seconds']:.2f} s, then {n} lookups (half present) in "
+                      f"{r['lookup_seconds']:.2f} s; value = inserts/s x 64 B, the GPU line's unit"}
 
 
 def relaunch(args) -> int:

@@ -382,6 +382,14 @@ uint64_t kc_group_records_sent(const kc_group *g);
  * plan pairs with its peers' for world 1..9. */
 int kc_exchange_plan(int world, int me, const uint64_t *Mx, uint64_t piece_records, uint64_t *out, int cap);
 
+/* ----------------------------------------------- Seen-set spill (tests) */
+/* Host self-check of the cold tier's run search (coldset.hip run_find, the
+ * search every GPU lookup of a spilled fingerprint runs): n sorted random
+ * keys and their directory; every key must be found and absent keys not,
+ * whole-run and through staging windows.  Returns the number of wrong
+ * answers (0 expected).  No GPU needed. */
+int64_t kc_cold_find_selftest(uint64_t n, uint64_t seed);
+
 /* ---------------------------------------------------------- Spec (host) */
 /* Words of the canonical tuple for a model: 1 + 19 * (nc + np + ns). */
 int kc_spec_tuple_words(int nc, int np, int ns);

@@ -146,6 +146,17 @@ typedef struct {
 } ko_par_result;
 double ko_bench_parallel(const ko_config *cfg, int threads, double seconds_budget, ko_par_result *out);
 
+/* FPSet stress comparator on the host (fpset_cpu.c; bench.py cpu_baseline
+ * of the fpset workload): n distinct fingerprints inserted by `threads`
+ * threads into one open-addressing table sized for `load`, then n lookups
+ * (half present). */
+typedef struct {
+  uint64_t slots, inserted, duplicates, found;
+  int threads;
+  double insert_seconds, lookup_seconds, inserts_per_s, lookups_per_s;
+} ko_fpset_cpu_result;
+int ko_fpset_stress_cpu(uint64_t n, double load, int threads, uint64_t seed, ko_fpset_cpu_result *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,3 +171,22 @@ def bench_sample(cfg: KoConfig, seconds: float):
     done = C.c_uint64()
     rate = lib().ko_bench_sample(C.byref(cfg), seconds, C.byref(done))
     return rate, done.value
+
+
+class KoFpsetCpuResult(C.Structure):
+    _fields_ = [("slots", C.c_uint64), ("inserted", C.c_uint64), ("duplicates", C.c_uint64),
+                ("found", C.c_uint64), ("threads", C.c_int), ("insert_seconds", C.c_double),
+                ("lookup_seconds", C.c_double), ("inserts_per_s", C.c_double), ("lookups_per_s", C.c_double)]
+
+
+def fpset_stress_cpu(n: int, load: float, threads: int, seed: int = 0x5EED0000) -> dict:
+    """Host FPSet comparator (fpset_cpu.c): n distinct fingerprints inserted by
+    `threads` threads into one table at `load`, then n lookups (half present)."""
+    L = lib()
+    L.ko_fpset_stress_cpu.restype = C.c_int
+    L.ko_fpset_stress_cpu.argtypes = [C.c_uint64, C.c_double, C.c_int, C.c_uint64, C.POINTER(KoFpsetCpuResult)]
+    r = KoFpsetCpuResult()
+    rc = L.ko_fpset_stress_cpu(n, load, threads, seed, C.byref(r))
+    if rc != 0:
+        raise RuntimeError(f"ko_fpset_stress_cpu failed ({rc})")
+    return {f[0]: getattr(r, f[0]) for f in KoFpsetCpuResult._fields_}

@@ -101,7 +101,7 @@ def test_seen_spill_np2_prefix_disk(fixtures, tmp_path, monkeypatch):
     monkeypatch.setenv("KC_COLD_WINDOW", str(1 << 20))
     fx = fixtures["np2_full"]
     r, _ = _run(np=2, max_levels=55, keep_trace=False, seen_hbm_bytes=512 * MiB, seen_host_bytes=64 * MiB,
-                spill_dir=str(tmp_path))
+                spill_dir=str(tmp_path), verbose=1)
     ref, _ = _run(np=2, max_levels=55, keep_trace=False)
     _same(r, ref)
     assert r.level_width == fx["level_width"][:55]
@@ -115,7 +115,7 @@ def test_seen_spill_np2_full(fixtures):
     # natural size is a 2^31-slot, 32 GiB ClaimSet): older fingerprints in
     # sorted runs in pinned host RAM
     fx = fixtures["np2_full"]
-    r, _ = _run(np=2, keep_trace=False, seen_hbm_bytes=4 << 30)
+    r, _ = _run(np=2, keep_trace=False, seen_hbm_bytes=4 << 30, verbose=1)   # (a line per level)
     assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r.level_width == fx["level_width"]
     assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]

@@ -27,7 +27,7 @@ __device__ __forceinline__ uint64_t bloom_hash(uint64_t k) {
   return h ^ (h >> 29);
 }
 
-__device__ __forceinline__ uint64_t dir_bucket(uint64_t k, int dbits) { return k >> (64 - dbits); }
+__host__ __device__ __forceinline__ uint64_t dir_bucket(uint64_t k, int dbits) { return k >> (64 - dbits); }
 
 // dir[b] = first index whose bucket is >= b (b in [0, 2^dbits]); thread i
 // writes the buckets in (bucket(i-1), bucket(i)], thread n the tail.
@@ -56,7 +56,7 @@ __global__ void k_bloom_add(const uint64_t* __restrict__ keys, uint64_t n, uint3
 // interpolated position and reads whole aligned 8-key lines (one 64-B
 // request each over the host link) until the key's place is bracketed:
 // about 1.2 lines per lookup.
-__device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict__ win, uint64_t w0, uint64_t w1,
+__host__ __device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict__ win, uint64_t w0, uint64_t w1,
                                          const uint64_t* __restrict__ dir, int dbits) {
   const uint64_t b = dir_bucket(k, dbits);
   const uint64_t blo = dir[b], bhi = dir[b + 1];
@@ -68,14 +68,18 @@ __device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict_
   pos = pos < lo ? lo : (pos >= hi ? hi - 1 : pos);
   uint64_t a = pos & ~7ull;
   if (a < lo) a = lo;
-  for (;;) {
+  // walk lines away from the guess in ONE direction: a key that falls
+  // between two lines' ranges is absent (turning back would loop forever)
+  int way = 0;
+  for (uint64_t steps = 0; steps <= (hi - lo) / 8 + 2; ++steps) {
     uint64_t e = (a | 7ull) + 1;
     if (e > hi) e = hi;
     uint64_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = a + u < e ? win[a + u - w0] : ~0ull;
     if (k < v[0]) {
-      if (a == lo) return false;
+      if (a == lo || way > 0) return false;
+      way = -1;
       a = (a - 1) & ~7ull;
       if (a < lo) a = lo;
       continue;
@@ -84,7 +88,8 @@ __device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict_
 #pragma unroll
     for (int u = 1; u < 8; ++u) last = a + u < e ? v[u] : last;
     if (k > last) {
-      if (e >= hi) return false;
+      if (e >= hi || way < 0) return false;
+      way = 1;
       a = e;
       continue;
     }
@@ -93,6 +98,7 @@ __device__ __forceinline__ bool run_find(uint64_t k, const uint64_t* __restrict_
     for (int u = 0; u < 8; ++u) hit |= v[u] == k;
     return hit;
   }
+  return false;
 }
 
 // stat[0]: filter tests (query x run), stat[1]: those it passed
@@ -508,3 +514,52 @@ int ColdSet::all_keys(std::vector<uint64_t>& out) {
 }
 
 }  // namespace kc
+
+// Host self-check of the cold-run search (no GPU): n sorted random keys with
+// the directory the kernels build, every key found, absent keys (including
+// ones between two lines' ranges) not found, each through whole-run and
+// windowed views.  Returns the number of wrong answers (0 expected).
+extern "C" int64_t kc_cold_find_selftest(uint64_t n, uint64_t seed) {
+  using namespace kc;
+  std::vector<uint64_t> keys(n);
+  uint64_t x = seed | 1;
+  for (auto& k : keys) {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    k = cold_key(x);
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  n = keys.size();
+  int dbits = 1;
+  while ((1ull << (dbits + 1)) * 16 <= n && dbits < 40) ++dbits;
+  std::vector<uint64_t> dir((1ull << dbits) + 1);
+  for (uint64_t b = 0, i = 0; b <= (1ull << dbits); ++b) {
+    while (i < n && dir_bucket(keys[i], dbits) < b) ++i;
+    dir[b] = i;
+  }
+  int64_t bad = 0;
+  const uint64_t W = 64 + (n / 7 & ~7ull);      // windows of W keys (a multiple of 8)
+  auto find_any = [&](uint64_t k) {
+    if (run_find(k, keys.data(), 0, n, dir.data(), dbits)) return 1;
+    return 0;
+  };
+  auto find_win = [&](uint64_t k) {
+    int hits = 0;
+    for (uint64_t w0 = 0; w0 < n; w0 += W)
+      hits += run_find(k, keys.data() + w0, w0, std::min(n, w0 + W), dir.data(), dbits) ? 1 : 0;
+    return hits;
+  };
+  for (uint64_t i = 0; i < n; ++i) {
+    bad += find_any(keys[i]) != 1;
+    if (i % 7 == 0) bad += find_win(keys[i]) != 1;
+    // absent neighbours: just above this key (inside gaps, often between lines)
+    if (i + 1 < n && keys[i + 1] > keys[i] + 1) {
+      const uint64_t a = keys[i] + 1 + (keys[i + 1] - keys[i] - 1) / 2;
+      bad += find_any(a) != 0;
+      if (i % 7 == 0) bad += find_win(a) != 0;
+    }
+  }
+  bad += find_any(0) != (n && keys[0] == 0);
+  bad += find_any(~0ull) != (n && keys[n - 1] == ~0ull);
+  return bad;
+}

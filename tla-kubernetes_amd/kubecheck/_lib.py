@@ -150,6 +150,7 @@ SIGNATURES = [
     ("kc_group_trace_tuple", C.c_int, [_P, C.c_int, _U64P]),
     ("kc_group_records_sent", C.c_uint64, [_P]),
     ("kc_exchange_plan", C.c_int, [C.c_int, C.c_int, _U64P, C.c_uint64, _U64P, C.c_int]),
+    ("kc_cold_find_selftest", C.c_int64, [C.c_uint64, C.c_uint64]),
     ("kc_spec_tuple_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_state_words", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("kc_spec_init", C.c_int, [C.POINTER(KcModelConfig), _U64P, C.c_int]),
