@@ -261,6 +261,9 @@ typedef struct {
   uint64_t seen_disk_bytes;     /* cold-run bytes written to spill files */
   uint64_t seen_peak_hbm_bytes; /* peak HBM of the seen-set (hot table + scratch + cold metadata) */
   double seen_seconds;          /* host wall time in chunk planning, flushes and cold checks */
+  double seen_flush_seconds;    /* ... of it in flushes (sort, copy out, merges, files) */
+  double seen_merge_seconds;    /* ... of that in the host merges of runs */
+  double seen_check_seconds;    /* ... in the per-chunk cold checks (queries, sort, probe) */
   uint64_t cand_overflow_records;  /* settle candidates beyond their tile's segment (overflow list) */
   uint64_t cand_buffer_peak_bytes; /* HBM of the candidate-record buffers (tile segments + overflow list) */
 } kc_result;

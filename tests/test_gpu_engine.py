@@ -237,3 +237,13 @@ def test_lost_update_holds_as_written(fixtures):
     assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"]) == (
         163408, 577736, 124)
     assert r.act_dist == fx["act_dist"]
+
+
+def test_np3_prefix(fixtures):
+    # SURVEY §8(d) config 2's secondary model, NP=3 (4 actors: 80-B states,
+    # |U| = 64): its first 40 levels (50.8M states) against the oracle
+    fx = fixtures["np3_40levels"]
+    r = run(np=3, max_levels=40, keep_trace=False)
+    assert r.level_width == fx["level_width"]
+    assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    assert (r.distinct, r.generated) == (fx["distinct"], fx["generated"]) and not r.complete

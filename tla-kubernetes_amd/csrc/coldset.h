@@ -62,6 +62,7 @@ __host__ __device__ __forceinline__ uint64_t cold_unkey(uint64_t k) {
 struct ColdRun {
   uint64_t n = 0;                 // keys
   uint64_t* host = nullptr;       // pinned host RAM (device-readable), or nullptr on disk
+  uint64_t host_cap = 0;          // keys the pinned buffer holds (pooled: >= n)
   std::string path;               // the spill file when on disk
   uint64_t* d_dir = nullptr;      // HBM: 2^dbits + 1 entries
   int dbits = 1;
@@ -80,6 +81,9 @@ struct ColdStats {
   uint64_t host_bytes = 0, disk_bytes = 0, meta_bytes = 0, peak_meta_bytes = 0;
   uint64_t merges = 0, merged_keys = 0, disk_written = 0, disk_read = 0, windows_skipped = 0;
   uint64_t filter_tests = 0, filter_passed = 0;   // query x run pairs a filter saw / let through
+  // host wall time: pinning buffers, CPU merges, directory/filter builds
+  // (incl. the copy of a new run), writing runs to files
+  double pin_seconds = 0, merge_seconds = 0, meta_seconds = 0, evict_seconds = 0;
 };
 
 class ColdSet {
@@ -122,6 +126,12 @@ class ColdSet {
   int read_window(const ColdRun& r, uint64_t w0, uint64_t w1, uint64_t* dst);
   void free_run(ColdRun& r);
   int staging(uint64_t keys);
+  // pinned host buffers are pooled: pinning GBs of pages costs more than the
+  // merges that use them
+  int pin_get(uint64_t keys, uint64_t** p, uint64_t* cap);
+  void pin_put(uint64_t* p, uint64_t cap);
+  std::vector<std::pair<uint64_t*, uint64_t>> pool_;
+  double t_pin_ = 0, t_merge_ = 0, t_meta_ = 0, t_evict_ = 0;
 
   Config cfg_;
   std::vector<ColdRun> runs_;      // oldest first

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <thread>
 
 #include "coldset.h"
@@ -154,7 +155,39 @@ __global__ void k_window_ranges(const uint64_t* __restrict__ q, uint64_t m, cons
 
 unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
 }  // namespace
+
+// Best fit from the pool, else a fresh pinned buffer with 1/4 slack (the
+// size-tiered runs come in a few recurring sizes).
+int ColdSet::pin_get(uint64_t keys, uint64_t** p, uint64_t* cap) {
+  size_t best = pool_.size();
+  for (size_t i = 0; i < pool_.size(); ++i)
+    if (pool_[i].second >= keys && (best == pool_.size() || pool_[i].second < pool_[best].second)) best = i;
+  if (best < pool_.size()) {
+    *p = pool_[best].first;
+    *cap = pool_[best].second;
+    pool_.erase(pool_.begin() + best);
+    return 0;
+  }
+  const double t0 = now_s();
+  const uint64_t c = keys + keys / 4 + 1024;
+  KC_HIP_TRY(hipHostMalloc(p, c * 8));
+  *cap = c;
+  t_pin_ += now_s() - t0;
+  return 0;
+}
+// Back to the pool; the pool keeps its 4 largest buffers.
+void ColdSet::pin_put(uint64_t* p, uint64_t cap) {
+  if (!p) return;
+  pool_.push_back({p, cap});
+  std::sort(pool_.begin(), pool_.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+  while (pool_.size() > 4) {
+    (void)hipHostFree(pool_.back().first);
+    pool_.pop_back();
+  }
+}
 
 ColdSet::~ColdSet() {
   clear();
@@ -165,6 +198,8 @@ ColdSet::~ColdSet() {
     if (stage_ev_[s]) (void)hipEventDestroy(stage_ev_[s]);
   }
   if (d_stat_) (void)hipFree(d_stat_);
+  for (auto& b : pool_) (void)hipHostFree(b.first);
+  pool_.clear();
 }
 
 int ColdSet::init(const Config& c) {
@@ -197,7 +232,7 @@ void ColdSet::free_meta(ColdRun& r) {
 void ColdSet::free_run(ColdRun& r) {
   free_meta(r);
   if (r.host) {
-    (void)hipHostFree(r.host);
+    pin_put(r.host, r.host_cap);
     host_used_ -= r.bytes();
   }
   if (!r.path.empty()) {
@@ -214,6 +249,7 @@ void ColdSet::clear() {
   runs_.clear();
   if (d_stat_) (void)hipMemset(d_stat_, 0, 16);
   merges_ = merged_keys_ = disk_written_ = disk_read_ = windows_skipped_ = 0;
+  t_pin_ = t_merge_ = t_meta_ = t_evict_ = 0;
   peak_meta_ = meta_used_;
 }
 
@@ -258,14 +294,16 @@ int ColdSet::add_run(const uint64_t* d_sorted, uint64_t n, hipStream_t st) {
   if (n == 0) return 0;
   ColdRun r;
   r.n = n;
-  KC_HIP_TRY(hipHostMalloc(&r.host, n * 8));
+  KC_TRY(pin_get(n, &r.host, &r.host_cap));
   host_used_ += r.bytes();
   keys_ += n;
+  const double t0 = now_s();
   KC_HIP_TRY(hipMemcpyAsync(r.host, d_sorted, n * 8, hipMemcpyDeviceToHost, st));
   const int rc = build_meta(r, d_sorted, st);
   runs_.push_back(r);                   // owned (and freed) by runs_ from here on
   KC_TRY(rc);
   KC_HIP_TRY(hipStreamSynchronize(st));
+  t_meta_ += now_s() - t0;
   // size-tiered compaction: a binary counter of run sizes
   while (runs_.size() >= 2) {
     const ColdRun &a = runs_[runs_.size() - 2], &b = runs_.back();
@@ -287,8 +325,9 @@ int ColdSet::merge_last_two(hipStream_t st) {
   ColdRun& b = runs_.back();
   ColdRun c;
   c.n = a.n + b.n;
-  KC_HIP_TRY(hipHostMalloc(&c.host, c.n * 8));
+  KC_TRY(pin_get(c.n, &c.host, &c.host_cap));
   host_used_ += c.bytes();
+  const double t0 = now_s();
   // the key space cut into T equal ranges, each merged by its own thread
   // (the runs are uniform, so the ranges carry equal work)
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cfg_.merge_threads, c.n / 65536 + 1));
@@ -312,11 +351,13 @@ int ColdSet::merge_last_two(hipStream_t st) {
     work(0);
     for (auto& x : th) x.join();
   } catch (...) {
-    (void)hipHostFree(c.host);
+    pin_put(c.host, c.host_cap);
     host_used_ -= c.bytes();
     set_error("seen-set: cannot start merge threads");
     return -ENOMEM;
   }
+  const double t1 = now_s();
+  t_merge_ += t1 - t0;
   merges_ += 1;
   merged_keys_ += c.n;
   const uint64_t na = a.n, nb = b.n;
@@ -329,6 +370,7 @@ int ColdSet::merge_last_two(hipStream_t st) {
   runs_.push_back(c);
   KC_TRY(rc);
   KC_HIP_TRY(hipStreamSynchronize(st));
+  t_meta_ += now_s() - t1;
   (void)na;
   (void)nb;
   return 0;
@@ -336,6 +378,7 @@ int ColdSet::merge_last_two(hipStream_t st) {
 
 int ColdSet::evict_oldest_host(hipStream_t st) {
   (void)st;
+  const double t0 = now_s();
   for (auto& r : runs_) {
     if (!r.host) continue;
     if (cfg_.dir.empty()) {
@@ -379,12 +422,14 @@ int ColdSet::evict_oldest_host(hipStream_t st) {
     wk[r.nw] = ~0ull;
     KC_HIP_TRY(hipMalloc(&r.d_wkeys, (r.nw + 1) * 8));
     KC_HIP_TRY(hipMemcpy(r.d_wkeys, wk.data(), (r.nw + 1) * 8, hipMemcpyHostToDevice));
-    (void)hipHostFree(r.host);
+    pin_put(r.host, r.host_cap);
     r.host = nullptr;
+    r.host_cap = 0;
     host_used_ -= r.bytes();
     r.path = path;
     disk_used_ += r.bytes();
     disk_written_ += r.bytes();
+    t_evict_ += now_s() - t0;
     return 0;
   }
   return 0;
@@ -488,6 +533,10 @@ void ColdSet::stats(ColdStats* s) const {
   s->disk_written = disk_written_;
   s->disk_read = disk_read_;
   s->windows_skipped = windows_skipped_;
+  s->pin_seconds = t_pin_;
+  s->merge_seconds = t_merge_;
+  s->meta_seconds = t_meta_;
+  s->evict_seconds = t_evict_;
   unsigned long long st[2] = {0, 0};
   if (d_stat_ && hipMemcpy(st, d_stat_, 16, hipMemcpyDeviceToHost) == hipSuccess) {
     s->filter_tests = st[0];

@@ -753,6 +753,15 @@ class EngineT final : public EngineBase {
       res->seen_filter_passed = cst.filter_passed;
       res->seen_merges = cst.merges;
       res->seen_seconds = sp_seconds_;
+      res->seen_flush_seconds = sp_flush_seconds_;
+      res->seen_merge_seconds = cst.merge_seconds;
+      res->seen_check_seconds = sp_check_seconds_;
+      if (cfg_.verbose)
+        fprintf(stderr, "kubecheck seen-set spill: %.3f s host (flushes %.3f: pin %.3f merge %.3f meta+copy %.3f files %.3f;"
+                        " checks %.3f), %llu flushes, %llu runs, %llu merges\n",
+                sp_seconds_, sp_flush_seconds_, cst.pin_seconds, cst.merge_seconds, cst.meta_seconds, cst.evict_seconds,
+                sp_check_seconds_, (unsigned long long)sp_flushes_, (unsigned long long)cst.runs,
+                (unsigned long long)cst.merges);
     }
     if (q_) {
       kc_squeue_stats qs;
@@ -957,7 +966,9 @@ class EngineT final : public EngineBase {
     cold_.clear();
     hot_count_ = 0;
     sp_flushes_ = sp_queries_ = 0;
-    sp_seconds_ = 0;
+    sp_seconds_ = sp_flush_seconds_ = sp_check_seconds_ = 0;
+    const char* ss = getenv("KC_SPILL_SYNC");
+    sp_sync_check_ = ss && ss[0] == '1';
     KC_HIP_TRY(hipMemsetAsync(d_spctr_, 0, 64, st_));
     return 0;
   }
@@ -1002,6 +1013,7 @@ class EngineT final : public EngineBase {
 
   // Hot table -> one sorted cold run; the table starts over empty.
   int spill_flush() {
+    const auto t0 = std::chrono::steady_clock::now();
     uint64_t* keys = reinterpret_cast<uint64_t*>(sp_arena_);
     KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
     hipLaunchKernelGGL(k_claimset_keys, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_, cs_.t,
@@ -1034,6 +1046,7 @@ class EngineT final : public EngineBase {
     KC_TRY(cs_.clear(st_));
     hot_count_ = 0;
     ++sp_flushes_;
+    sp_flush_seconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return 0;
   }
 
@@ -1071,8 +1084,11 @@ class EngineT final : public EngineBase {
                          vb.Current(), found, m, newmask_, ttot_, cs_.t, cs_.nslots, d_ctr_);
       hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
       KC_HIP_TRY(hipGetLastError());
+      if (sp_sync_check_) KC_HIP_TRY(hipStreamSynchronize(st_));   // (KC_SPILL_SYNC=1: time the check itself)
     }
-    sp_seconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    sp_seconds_ += dt;
+    sp_check_seconds_ += dt;
     return 0;
   }
 
@@ -1086,7 +1102,8 @@ class EngineT final : public EngineBase {
   uint64_t sp_tsum_cap_ = 0, h_tsum_cap_ = 0;
   unsigned long long *d_spctr_ = nullptr, *h_spctr_ = nullptr;   // [0] cold hits, [1] flush count
   uint64_t sp_flushes_ = 0, sp_queries_ = 0;
-  double sp_seconds_ = 0;
+  double sp_seconds_ = 0, sp_flush_seconds_ = 0, sp_check_seconds_ = 0;
+  bool sp_sync_check_ = false;
 
   // the trace file (parent index + ordinal per state) in HBM, or in pinned
   // host RAM with cfg.trace_host (kernels store into it directly)

@@ -185,6 +185,11 @@ def oracle_fixtures(with_np2: bool) -> dict:
         path = os.path.join(GOLDEN, "np2_full.json")
         if os.path.exists(path):
             fx["np2_full"] = json.load(open(path))
+        # NP=3 (SURVEY §8(d) config 2 secondary): its first 40 levels, from
+        # `kubeapi_oracle -np 3 -notracestore -maxlevels 40` (112 s)
+        path = os.path.join(GOLDEN, "np3_40levels.json")
+        if os.path.exists(path):
+            fx["np3_40levels"] = json.load(open(path))
     return fx
 
 
