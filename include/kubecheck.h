@@ -151,7 +151,9 @@ typedef struct {
   uint64_t spilled_host_bytes, spilled_disk_bytes, reloaded_bytes, peak_hbm_bytes;  /* cumulative */
 } kc_squeue_stats;
 int kc_squeue_create2(const kc_squeue_config *cfg, kc_squeue **out);
-/* one HBM tier of `capacity_states`-state segments, no budget (round-1 API) */
+/* one HBM tier of `capacity_states`-state segments, no budget (round-1 API);
+ * capacity_states is also a hard bound on the queue's size: enqueue,
+ * enqueue_dev and reserve_dev past it fail with -ENOMEM ("StateQueue full") */
 int kc_squeue_create(int state_words, uint64_t capacity_states, int device, kc_squeue **out);
 void kc_squeue_destroy(kc_squeue *q);
 /* host buffers (synchronous) */
@@ -314,6 +316,10 @@ int kc_shard_create(const kc_model_config *cfg, int rank, int world, kc_shard **
 void kc_shard_destroy(kc_shard *s);
 /* Adopt (insert + enqueue) the Init states this rank owns. */
 int kc_shard_init(kc_shard *s, uint64_t *n_local);
+/* After kc_shard_init: the error key (low byte 0x12) of this rank's first
+ * Init state that violates an invariant, ~0 if none.  It is level 1's error
+ * and takes precedence over anything level 1's expansion reports. */
+int kc_shard_init_error(kc_shard *s, uint64_t *key_out);
 /* Run every stage on the caller's HIP stream (e.g. the one its RCCL
  * collectives use) instead of the shard's own: pack() then returns without a
  * host sync and insert() may read a recv buffer written earlier on that

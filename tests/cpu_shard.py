@@ -39,17 +39,23 @@ class CpuShard:
             if self.spec.check_invariants(t) is not None:
                 self.init_err = min(self.init_err, (self.rank << 60) | ((len(self.frontier) - 1) << 16) | 0x12)
         self.n_init = len(self.frontier)
+        self.init_key = self.init_err
         return len(self.frontier)
+
+    def init_error(self):
+        return self.init_key
 
     def expand(self):
         err, self.init_err = self.init_err, NONE_KEY
+        init_violated = err != NONE_KEY            # then it is THE error (HipShard does the same)
         local, per_owner = set(), [[] for _ in range(self.world)]
         for i, s in enumerate(self.frontier):
             succ, fail = self.spec.successors(s)
             if succ is None:
-                err = min(err, (self.rank << 60) | (i << 16) | 1)
+                if not init_violated:
+                    err = min(err, (self.rank << 60) | (i << 16) | 1)
                 continue
-            if not succ and self.cfg.check_deadlock:
+            if not succ and self.cfg.check_deadlock and not init_violated:
                 err = min(err, (self.rank << 60) | (i << 16) | 3)
             for t, (a, x) in enumerate(succ):
                 self.act_gen[ACTIONS.index(a)] += 1

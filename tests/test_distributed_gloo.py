@@ -135,3 +135,14 @@ def test_bench_self_launch_two_ranks():
     assert rep["world"] == 2 and rep["n_gpus"] == 2 and rep["master_addr"] == "127.0.0.1"
     assert sorted(r[0] for r in rep["ranks"]) == [0, 1] and all(r[1] == 2 for r in rep["ranks"])
     assert sorted(r[2] for r in rep["ranks"]) == [0, 1]
+
+
+@pytest.mark.parametrize("max_levels", [0, 1])
+def test_sharded_init_violation_is_level1(tmp_path, fixtures, max_levels):
+    # variant 5: an Init state violates OnlyOneVersion.  It is level 1's error
+    # even when level 1 is not expanded (max_levels=1), and ahead of anything
+    # level 1's expansion finds (it was min-merged with Assert
+    # keys and lost at max_levels=1)
+    r = run_sharded(tmp_path, 2, variant=5, max_levels=max_levels)
+    assert r["error"] == "invariant" and r["error_level"] == 1
+    assert r["trace_len"] == fixtures["variant5"]["trace_len"] == 1

@@ -305,3 +305,11 @@ def test_native_lost_update_invariant(fixtures, R):
     assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
     if R == 1:
         assert r["trace"] == fx["trace"]
+
+
+@pytest.mark.parametrize("R", [1, 3])
+def test_native_init_violation_max_levels_1(fixtures, R):
+    # an Init state's invariant violation (variant 5) is level 1's error even
+    # when level 1 is never expanded
+    r = native(R, variant=5, max_levels=1)
+    assert r["error"] == "invariant" and r["error_level"] == 1 and r["trace_len"] == 1

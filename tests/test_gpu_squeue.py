@@ -239,3 +239,18 @@ def test_engine_spill_np2_full(fixtures):
     assert r.complete and r.frontier_spilled_bytes > 0
     # (in-HBM, the two frontier buffers are sized by the successor count: GBs)
     assert r.frontier_peak_hbm_bytes < (3 << 29)
+
+
+def test_legacy_capacity_is_a_bound():
+    # kc_squeue_create(state_words, capacity_states, ...): the round-1
+    # constructor's capacity stays a hard bound: enqueues past it
+    # fail with -ENOMEM instead of growing the queue silently
+    W = 4
+    q = StateQueue(W, capacity=1024, device=0)
+    q.enqueue(np.arange(1000 * W, dtype=np.uint64).reshape(-1, W))
+    with pytest.raises(KubecheckError) as e:
+        q.enqueue(np.zeros((25, W), dtype=np.uint64))
+    assert e.value.code == -12 and "StateQueue full" in str(e.value)
+    q.enqueue(np.zeros((24, W), dtype=np.uint64))           # exactly to capacity
+    assert q.size() == 1024
+    q.close()

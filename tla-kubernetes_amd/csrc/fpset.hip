@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -407,7 +408,7 @@ using namespace kc;
 // Flat-combining state of the single-fingerprint put/contains (below).
 struct Combiner {
   struct Req { uint64_t fp; int op; uint64_t ticket; };
-  struct Res { uint8_t seen; int rc; };
+  struct Res { uint8_t seen; int rc; std::string msg; };   // msg: the combiner's error text (rc < 0)
   std::mutex mu;
   std::condition_variable cv;
   std::vector<Req> pending;
@@ -791,6 +792,8 @@ static int combine_one(kc_fpset* s, uint64_t fp, int op, uint8_t* result) {
     if (it != c.done.end()) {
       const int rc = it->second.rc;
       *result = it->second.seen;
+      // the combiner ran this request: its failure message, on this thread
+      if (rc < 0) set_error("%s", it->second.msg.c_str());
       c.done.erase(it);
       return rc;
     }
@@ -807,6 +810,7 @@ static int combine_one(kc_fpset* s, uint64_t fp, int op, uint8_t* result) {
     // same op go out as one batch each
     std::vector<uint8_t> seen(batch.size());
     std::vector<int> rcs(batch.size(), 0);
+    std::vector<std::string> msgs(batch.size());
     size_t a = 0;
     while (a < batch.size()) {
       size_t b = a;
@@ -814,18 +818,23 @@ static int combine_one(kc_fpset* s, uint64_t fp, int op, uint8_t* result) {
       while (b < batch.size() && batch[b].op == batch[a].op) fps.push_back(batch[b++].fp);
       const int rc = batch[a].op == 0 ? kc_fpset_put_batch(s, fps.data(), fps.size(), seen.data() + a)
                                       : kc_fpset_contains_batch(s, fps.data(), fps.size(), seen.data() + a);
-      for (size_t k = a; k < b; ++k) rcs[k] = rc;
+      const std::string m = rc < 0 ? std::string(last_error()) : std::string();
+      for (size_t k = a; k < b; ++k) {
+        rcs[k] = rc;
+        msgs[k] = m;
+      }
       a = b;
     }
     lk.lock();
     ++c.rounds;
-    for (size_t k = 0; k < batch.size(); ++k) c.done[batch[k].ticket] = {seen[k], rcs[k]};
+    for (size_t k = 0; k < batch.size(); ++k) c.done[batch[k].ticket] = {seen[k], rcs[k], std::move(msgs[k])};
     c.cv.notify_all();
   }
   c.busy = false;
   auto it = c.done.find(ticket);
   const int rc = it->second.rc;
   *result = it->second.seen;
+  if (rc < 0) set_error("%s", it->second.msg.c_str());
   c.done.erase(it);
   c.cv.notify_all();
   return rc;

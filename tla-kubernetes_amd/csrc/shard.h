@@ -18,6 +18,10 @@ class ShardBase {
   virtual int setup() = 0;
   virtual int set_stream(hipStream_t st) = 0;
   virtual int init(uint64_t* n_local) = 0;
+  // the error key of the first Init state (in this rank's order) that
+  // violates an invariant (low byte 0x12), ~0 if none: level 1's error,
+  // ahead of anything expansion finds (TLC checks Init before expanding)
+  virtual uint64_t init_error() const = 0;
   virtual int expand(uint64_t* counts, uint64_t* err_key) = 0;
   // expand() split around a device-side all-gather row (the native loop over
   // RCCL): expand_dev enqueues the level's claims and writes d_row[0..world)

@@ -151,11 +151,10 @@ __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t*
     head_to_host(C, host_head);
     if (row) {
       uint64_t se = status_err;
-      if (level1) {
-        uint64_t e = init_err;
-        if (C->err_key != ~0ull) e = min(e, (rank << 60) | (uint64_t)C->err_key);
-        if (e != ~0ull && (e & 0xFF) == 0x12) se = e;
-      }
+      // an Init state's invariant violation is level 1's error, whatever
+      // level 1's expansion found (an Assert of a lower-index Init state
+      // must not hide it)
+      if (level1 && init_err != ~0ull) se = init_err;
       row[world] = status_new;
       row[world + 1] = se;
       // failure word: a full table or an over-wide state found by this
@@ -432,6 +431,7 @@ class ShardT final : public ShardBase {
         init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
     }
     n_ = mine.size();
+    init_key_ = init_err_;
     level_ = 1;
     level_base_.assign(1, 0);
     gen_init_ = n_;
@@ -549,6 +549,7 @@ class ShardT final : public ShardBase {
     for (int o = 0; o < world_; ++o) counts[o] = 0;
     *err_key = dev_init_err_;
     if (dev_zero_) return 0;
+    const bool init_violated = dev_init_err_ != ~0ull;   // then it is THE error (see k_owner_totals)
     if (cfg_.timing) {
       float ms = 0;
       KC_HIP_TRY(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
@@ -564,12 +565,13 @@ class ShardT final : public ShardBase {
       counts[o] = h_owner_base_[o];
       send_total_ += counts[o];
     }
-    if (h_ctr_->err_key != ~0ull)
+    if (h_ctr_->err_key != ~0ull && !init_violated)
       *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_ctr_->err_key);
     return 0;
   }
 
   uint64_t record_bytes() const override { return sizeof(Rec); }
+  uint64_t init_error() const override { return init_key_; }
   hipStream_t stream() const override { return st_; }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
@@ -827,6 +829,7 @@ class ShardT final : public ShardBase {
   uint64_t n_ = 0, next_n_ = 0, send_total_ = 0, gen_init_ = 0;
   uint64_t cand_ = 0, next_cand_ = 0, cand_total_ = 0;   // successors of the frontier
   uint64_t init_err_ = ~0ull;
+  uint64_t init_key_ = ~0ull;       // init_error(): init_err_ as init() found it
   // expand_dev -> expand_done: the Init-state key taken, nothing launched
   // that needs a sync, no claims this level
   uint64_t dev_init_err_ = ~0ull;
@@ -870,6 +873,12 @@ void kc_shard_destroy(kc_shard* s) { delete s; }
 int kc_shard_init(kc_shard* s, uint64_t* n_local) {
   if (!s || !n_local) { set_error("kc_shard_init: NULL"); return -EINVAL; }
   return s->impl->init(n_local);
+}
+
+int kc_shard_init_error(kc_shard* s, uint64_t* key) {
+  if (!s || !key) { set_error("kc_shard_init_error: NULL"); return -EINVAL; }
+  *key = s->impl->init_error();
+  return 0;
 }
 int kc_shard_set_stream(kc_shard* s, void* stream) {
   if (!s) { set_error("kc_shard_set_stream: NULL"); return -EINVAL; }   // stream 0: the default stream

@@ -496,6 +496,9 @@ int Group::run(kc_result* res) {
   for (size_t i = 0; i < nl; ++i) {
     note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
     if (!fail[i]) note(i, local_[i]->init(&status_new[i]));
+    // an Init state's invariant violation is level 1's error even when level
+    // 1 is not expanded (max_levels = 1)
+    if (!fail[i]) status_err[i] = local_[i]->init_error();
   }
   if (!h_fail_) KC_HIP_TRY(hipHostMalloc(&h_fail_, 16 * 8));
   std::vector<uint64_t> widths;

@@ -432,8 +432,18 @@ struct kc_squeue {
   SegQueue q;
   hipStream_t st = nullptr;       // the queue's own stream (blocking: ordered with the null stream)
   int device = 0;
+  uint64_t max_states = 0;        // kc_squeue_create's capacity: a hard bound (0 = none)
   std::mutex mu;
   hipStream_t pick(void* s) const { return s ? (hipStream_t)s : st; }
+  // the round-1 constructor's contract: enqueue past capacity_states fails
+  int room(size_t n, const char* fn) const {
+    if (max_states && q.size() + n > max_states) {
+      set_error("%s: StateQueue full (%llu + %zu states > capacity %llu)", fn, (unsigned long long)q.size(), n,
+                (unsigned long long)max_states);
+      return -ENOMEM;
+    }
+    return 0;
+  }
 };
 
 extern "C" {
@@ -486,7 +496,9 @@ int kc_squeue_create(int state_words, uint64_t capacity_states, int device, kc_s
     set_error("kc_squeue_create: bad argument");
     return -EINVAL;
   }
-  return kc_squeue_create2(&c, out);
+  KC_TRY(kc_squeue_create2(&c, out));
+  (*out)->max_states = capacity_states;     // a bounded queue, as this constructor always was
+  return 0;
 }
 
 void kc_squeue_destroy(kc_squeue* q) {
@@ -503,6 +515,7 @@ void kc_squeue_destroy(kc_squeue* q) {
 int kc_squeue_enqueue(kc_squeue* q, const uint64_t* states, size_t n) {
   if (!q || (n && !states)) { set_error("kc_squeue_enqueue: bad argument"); return -EINVAL; }
   std::lock_guard<std::mutex> g(q->mu);
+  KC_TRY(q->room(n, "kc_squeue_enqueue"));
   KC_HIP_TRY(hipSetDevice(q->device));
   return q->q.enqueue_host(states, n, q->st);
 }
@@ -520,6 +533,7 @@ int kc_squeue_dequeue(kc_squeue* q, uint64_t* out, size_t max_n, size_t* n_out) 
 int kc_squeue_enqueue_dev(kc_squeue* q, const uint64_t* dev_states, size_t n, void* stream) {
   if (!q || (n && !dev_states)) { set_error("kc_squeue_enqueue_dev: bad argument"); return -EINVAL; }
   std::lock_guard<std::mutex> g(q->mu);
+  KC_TRY(q->room(n, "kc_squeue_enqueue_dev"));
   KC_HIP_TRY(hipSetDevice(q->device));
   return q->q.enqueue_dev(dev_states, n, q->pick(stream));
 }
@@ -537,6 +551,7 @@ int kc_squeue_dequeue_dev(kc_squeue* q, uint64_t* dev_out, size_t max_n, size_t*
 int kc_squeue_reserve_dev(kc_squeue* q, size_t n, uint64_t** dev_ptr, void* stream) {
   if (!q || !dev_ptr || n == 0) { set_error("kc_squeue_reserve_dev: bad argument"); return -EINVAL; }
   std::lock_guard<std::mutex> g(q->mu);
+  KC_TRY(q->room(n, "kc_squeue_reserve_dev"));
   return q->q.reserve(n, dev_ptr, q->pick(stream));
 }
 

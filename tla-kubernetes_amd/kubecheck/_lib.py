@@ -132,6 +132,7 @@ SIGNATURES = [
     ("kc_shard_create", C.c_int, [C.POINTER(KcModelConfig), C.c_int, C.c_int, C.POINTER(_P)]),
     ("kc_shard_destroy", None, [_P]),
     ("kc_shard_init", C.c_int, [_P, _U64P]),
+    ("kc_shard_init_error", C.c_int, [_P, _U64P]),
     ("kc_shard_set_stream", C.c_int, [_P, _P]),
     ("kc_shard_expand", C.c_int, [_P, _U64P, _U64P]),
     ("kc_shard_record_bytes", C.c_uint64, [_P]),

@@ -22,6 +22,7 @@ stages.
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 import time
 from typing import List, Optional, Sequence
@@ -78,6 +79,12 @@ class HipShard:
         n = C.c_uint64()
         check("kc_shard_init", self._lib.kc_shard_init(self._h, C.byref(n)))
         return n.value
+
+    def init_error(self) -> int:
+        """Key of this rank's first Init state violating an invariant (~0: none)."""
+        k = C.c_uint64()
+        check("kc_shard_init_error", self._lib.kc_shard_init_error(self._h, C.byref(k)))
+        return k.value
 
     def expand(self):
         counts = (C.c_uint64 * self.world)()
@@ -344,7 +351,10 @@ class ShardedModelChecker:
                 prof[name] = prof.get(name, 0.0) + tick() - t
             return tick()
 
-        status_new, status_err = be.init(), NONE_KEY
+        # an Init violation is level 1's error, reported at level 1's gather
+        # even when level 1 is not expanded (max_levels = 1)
+        status_new = be.init()
+        status_err = be.init_error()
         widths, level, err = [], 1, NONE_KEY
         self.records_sent = 0                             # to other ranks, this check
         rw = rb // 8                                      # record words
@@ -444,6 +454,26 @@ class ShardedModelChecker:
         return out
 
 
+def pmc_ratio(workload: str):
+    """PMC HBM bytes per algorithmic byte of the SHARDED k_claim, from the
+    newest committed profiles/*_<workload>_sharded_rocprof_summary.json
+    (tools/sharded_profile.py + tools/pmc_summary.py; bench.py cannot take
+    PMC counters itself).  Streaming parent reads are counted at half by the
+    counters (profiles/r02b_pmc_calibration.json) and restored here."""
+    import glob
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for f in reversed(sorted(glob.glob(os.path.join(root, "profiles", f"*_{workload}_sharded_rocprof_summary.json")))):
+        try:
+            d = json.load(open(f))
+            k, alg = d["kernels"]["k_claim"], d["algorithmic"]
+            hbm = k["fetch_bytes_per_launch_raw"] + alg["stream_read_bytes_per_launch"] / 2 + \
+                k["write_bytes_per_launch_raw"]
+            return hbm / alg["algorithmic_bytes_per_launch"], os.path.relpath(f, root)
+        except (OSError, ValueError, KeyError, ZeroDivisionError):
+            continue
+    return None, None
+
+
 def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict]:
     """bench.py --gpus N: every rank checks its shard; rank 0 reports.  The
     counts are checked against the golden fixture (bench.golden_check); the
@@ -516,11 +546,20 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
         }
         if tot_ns > 0:
             achieved = tot_bytes / (tot_ns * 1e-9) / 1e9
+            bpl = tot_bytes // max(tot_launch, 1)
             out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0,
                                "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
                                "kernel": "k_claim", "per": "GPU (all ranks' bytes / all ranks' k_claim time)",
                                "launches": tot_launch,
                                "avg_launch_us": round(tot_ns / 1e3 / max(tot_launch, 1), 2),
-                               "bytes_per_launch": tot_bytes // max(tot_launch, 1)}
+                               "bytes_per_launch": bpl}
+            ratio, src = pmc_ratio(args.workload)
+            if ratio:
+                out["roofline"]["traffic"] = int(ratio * bpl)
+                out["roofline"]["traffic_unit"] = "HBM bytes per launch (PMC)"
+                out["roofline"]["traffic_source"] = (
+                    f"{src}: PMC bytes / algorithmic bytes of the sharded k_claim = {ratio:.3f} "
+                    "(rocprofv3 FETCH_SIZE + WRITE_SIZE passes over emulated ranks on one GPU), "
+                    "times this run's algorithmic bytes per launch")
     dist.destroy_process_group()
     return out

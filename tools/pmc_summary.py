@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--out", required=True)
     ap.add_argument("--command", default="")
+    ap.add_argument("--algorithmic", help="JSON with the profiled run's algorithmic bytes (tools/sharded_profile.py)")
     a = ap.parse_args()
     trace = kernel_trace(a.trace)
     fetch, write = counters(a.fetch, "FETCH_SIZE"), counters(a.write, "WRITE_SIZE")
@@ -97,6 +98,8 @@ def main():
            "correction": "raw bytes = FETCH_SIZE*1024 + WRITE_SIZE*1024; hbm_read = raw fetch + "
                          "streaming_read/2 (profiles/r02b_pmc_calibration.json)",
            "kernels": kernels}
+    if a.algorithmic:
+        out["algorithmic"] = json.load(open(a.algorithmic))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
