@@ -12,3 +12,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_squ
 tail -3 $O/tests.log
 bash tools/gpu_r03_measure.sh $TAG || exit 1
 bash tools/gpu_r03_shprof.sh $TAG || exit 1
+echo "== random probe vs table size $(date +%T)"
+timeout -k 10 300 ./tools/microbench/random_probe > $O/random_probe.txt 2>&1 || { echo RP_FAIL; tail -5 $O/random_probe.txt; exit 1; }
+cat $O/random_probe.txt
+echo "== all done $(date +%T)"
