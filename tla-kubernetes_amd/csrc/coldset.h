@@ -69,6 +69,7 @@ struct ColdRun {
   uint32_t* d_bloom = nullptr;    // HBM: nblocks x 16 words (nullptr = no filter)
   uint64_t nblocks = 0;
   uint64_t meta_bytes = 0;        // HBM of dir + filter
+  uint64_t* d_keys = nullptr;     // HBM copy of the keys (the newest runs, as the budget allows)
   // disk runs: staging windows of wkeys keys; window w holds the keys in
   // [d_wkeys[w], d_wkeys[w + 1]) (d_wkeys[0] = 0, d_wkeys[nw] = ~0: HBM)
   uint64_t wkeys = 0, nw = 0;
@@ -80,6 +81,7 @@ struct ColdStats {
   uint64_t runs = 0, runs_disk = 0, keys = 0;
   uint64_t host_bytes = 0, disk_bytes = 0, meta_bytes = 0, peak_meta_bytes = 0;
   uint64_t merges = 0, merged_keys = 0, disk_written = 0, disk_read = 0, windows_skipped = 0;
+  uint64_t cached_runs = 0, cached_keys = 0, cache_bytes = 0, cache_uploaded = 0;
   uint64_t filter_tests = 0, filter_passed = 0;   // query x run pairs a filter saw / let through
   // host wall time: pinning buffers, CPU merges, directory/filter builds
   // (incl. the copy of a new run), writing runs to files
@@ -96,6 +98,7 @@ class ColdSet {
     uint64_t window_keys = 1ull << 23;   // disk runs: keys per staging window
     int merge_threads = 16;
     int bloom_bits = 10;           // target filter bits per key (0 = no filters)
+    bool cache_keys = true;        // copy the newest runs' keys into what HBM budget is left
   };
   ColdSet() = default;
   ~ColdSet();
@@ -126,6 +129,13 @@ class ColdSet {
   int read_window(const ColdRun& r, uint64_t w0, uint64_t w1, uint64_t* dst);
   void free_run(ColdRun& r);
   int staging(uint64_t keys);
+  // HBM copies of run keys: newest runs first, within what the directories
+  // and filters leave of the budget; dropped oldest-first when a new run's
+  // directory and filter need the room
+  int recache(hipStream_t st);
+  void uncache(ColdRun& r);
+  void make_room(uint64_t bytes);
+  uint64_t cache_used_ = 0, cache_uploaded_ = 0;
   // pinned host buffers are pooled: pinning GBs of pages costs more than the
   // merges that use them
   int pin_get(uint64_t keys, uint64_t** p, uint64_t* cap);

@@ -229,7 +229,54 @@ void ColdSet::free_meta(ColdRun& r) {
   r.nblocks = 0;
 }
 
+void ColdSet::uncache(ColdRun& r) {
+  if (!r.d_keys) return;
+  (void)hipFree(r.d_keys);
+  r.d_keys = nullptr;
+  cache_used_ -= r.bytes();
+}
+
+// free key copies, oldest run first, until `bytes` of the budget are free
+void ColdSet::make_room(uint64_t bytes) {
+  if (!cfg_.meta_hbm_bytes) return;
+  for (auto& r : runs_) {
+    if (meta_used_ + cache_used_ + bytes <= cfg_.meta_hbm_bytes) return;
+    uncache(r);
+  }
+}
+
+int ColdSet::recache(hipStream_t st) {
+  if (!cfg_.cache_keys) return 0;
+  for (size_t k = runs_.size(); k-- > 0;) {            // newest first
+    ColdRun& r = runs_[k];
+    if (r.d_keys || r.n == 0) continue;
+    if (cfg_.meta_hbm_bytes && meta_used_ + cache_used_ + r.bytes() > cfg_.meta_hbm_bytes) break;
+    if (hipMalloc(&r.d_keys, r.bytes()) != hipSuccess) {
+      r.d_keys = nullptr;
+      (void)hipGetLastError();
+      break;
+    }
+    cache_used_ += r.bytes();
+    cache_uploaded_ += r.bytes();
+    if (r.host) {
+      KC_HIP_TRY(hipMemcpyAsync(r.d_keys, r.host, r.bytes(), hipMemcpyHostToDevice, st));
+    } else {                                             // a file run: through the staging windows
+      KC_TRY(staging(r.wkeys));
+      for (uint64_t w0 = 0; w0 < r.n; w0 += r.wkeys) {
+        const uint64_t w1 = std::min(r.n, w0 + r.wkeys);
+        KC_HIP_TRY(hipStreamSynchronize(st));
+        KC_TRY(read_window(r, w0, w1, stage_[0]));
+        KC_HIP_TRY(hipMemcpyAsync(r.d_keys + w0, stage_[0], (w1 - w0) * 8, hipMemcpyHostToDevice, st));
+      }
+    }
+  }
+  peak_meta_ = std::max(peak_meta_, meta_used_ + cache_used_);
+  KC_HIP_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
 void ColdSet::free_run(ColdRun& r) {
+  uncache(r);
   free_meta(r);
   if (r.host) {
     pin_put(r.host, r.host_cap);
@@ -249,6 +296,7 @@ void ColdSet::clear() {
   runs_.clear();
   if (d_stat_) (void)hipMemset(d_stat_, 0, 16);
   merges_ = merged_keys_ = disk_written_ = disk_read_ = windows_skipped_ = 0;
+  cache_uploaded_ = 0;
   t_pin_ = t_merge_ = t_meta_ = t_evict_ = 0;
   peak_meta_ = meta_used_;
 }
@@ -259,6 +307,8 @@ int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
   int dbits = 1;
   while ((1ull << (dbits + 1)) * 16 <= r.n && dbits < 40) ++dbits;
   const uint64_t dir_bytes = ((1ull << dbits) + 1) * 8;
+  // directories and filters come before key copies
+  make_room(dir_bytes + (uint64_t)cfg_.bloom_bits * r.n / 8 + 64);
   if (cfg_.meta_hbm_bytes && meta_used_ + dir_bytes > cfg_.meta_hbm_bytes) {
     set_error("seen-set: HBM budget for cold-run directories exhausted (%llu + %llu > %llu B); raise seen_hbm_bytes",
               (unsigned long long)meta_used_, (unsigned long long)dir_bytes,
@@ -273,7 +323,7 @@ int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
   // filter bits per key: the target, or what the budget has left
   uint64_t bits = (uint64_t)cfg_.bloom_bits;
   if (cfg_.meta_hbm_bytes && r.n) {
-    const uint64_t left = cfg_.meta_hbm_bytes - meta_used_;
+    const uint64_t left = cfg_.meta_hbm_bytes - meta_used_ - cache_used_;
     bits = std::min<uint64_t>(bits, left * 8 / r.n);
   }
   if (bits >= 4 && r.n) {
@@ -286,7 +336,7 @@ int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
     hipLaunchKernelGGL(k_bloom_add, dim3(grid_of(r.n)), dim3(256), 0, st, keys, r.n, r.d_bloom, r.nblocks);
   }
   KC_HIP_TRY(hipGetLastError());
-  peak_meta_ = std::max(peak_meta_, meta_used_);
+  peak_meta_ = std::max(peak_meta_, meta_used_ + cache_used_);
   return 0;
 }
 
@@ -317,7 +367,7 @@ int ColdSet::add_run(const uint64_t* d_sorted, uint64_t n, hipStream_t st) {
     if (!any) break;
     KC_TRY(evict_oldest_host(st));
   }
-  return 0;
+  return recache(st);
 }
 
 int ColdSet::merge_last_two(hipStream_t st) {
@@ -477,9 +527,10 @@ int ColdSet::probe(const uint64_t* d_q, uint64_t m, uint8_t* d_found, unsigned l
   if (m == 0) return 0;
   for (size_t k = runs_.size(); k-- > 0;) {            // newest first
     const ColdRun& r = runs_[k];
-    if (r.host) {
-      hipLaunchKernelGGL(k_cold_probe, dim3(grid_of(m)), dim3(256), 0, st, d_q, m, d_found, r.host, 0ull, r.n,
-                         r.d_dir, r.dbits, r.d_bloom, r.nblocks, d_hits, d_stat_);
+    if (r.d_keys || r.host) {         // HBM copy, else the pinned host run read over the link
+      hipLaunchKernelGGL(k_cold_probe, dim3(grid_of(m)), dim3(256), 0, st, d_q, m, d_found,
+                         r.d_keys ? r.d_keys : r.host, 0ull, r.n, r.d_dir, r.dbits, r.d_bloom, r.nblocks, d_hits,
+                         d_stat_);
       continue;
     }
     // disk run: stream the windows holding at least one query's key range
@@ -533,6 +584,13 @@ void ColdSet::stats(ColdStats* s) const {
   s->disk_written = disk_written_;
   s->disk_read = disk_read_;
   s->windows_skipped = windows_skipped_;
+  for (const auto& r : runs_)
+    if (r.d_keys) {
+      s->cached_runs++;
+      s->cached_keys += r.n;
+    }
+  s->cache_bytes = cache_used_;
+  s->cache_uploaded = cache_uploaded_;
   s->pin_seconds = t_pin_;
   s->merge_seconds = t_merge_;
   s->meta_seconds = t_meta_;

@@ -758,10 +758,11 @@ class EngineT final : public EngineBase {
       res->seen_check_seconds = sp_check_seconds_;
       if (cfg_.verbose)
         fprintf(stderr, "kubecheck seen-set spill: %.3f s host (flushes %.3f: pin %.3f merge %.3f meta+copy %.3f files %.3f;"
-                        " checks %.3f), %llu flushes, %llu runs, %llu merges\n",
+                        " checks %.3f), %llu flushes, %llu runs (%llu with %llu keys in HBM), %llu merges, %.1f GB uploaded\n",
                 sp_seconds_, sp_flush_seconds_, cst.pin_seconds, cst.merge_seconds, cst.meta_seconds, cst.evict_seconds,
                 sp_check_seconds_, (unsigned long long)sp_flushes_, (unsigned long long)cst.runs,
-                (unsigned long long)cst.merges);
+                (unsigned long long)cst.cached_runs, (unsigned long long)cst.cached_keys,
+                (unsigned long long)cst.merges, cst.cache_uploaded / 1e9);
     }
     if (q_) {
       kc_squeue_stats qs;
@@ -927,8 +928,11 @@ class EngineT final : public EngineBase {
   int spill_setup() {
     if (!cs_.t) {
       const uint64_t B = cfg_.seen_hbm_bytes;
+      // the hot table's share of the budget: 1/2 (KC_SEEN_HOT_DIV=4: 1/4, A/B)
+      const char* hd = getenv("KC_SEEN_HOT_DIV");
+      const uint64_t div = hd && atoi(hd) >= 2 ? (uint64_t)atoi(hd) : 2;
       uint64_t ns = 1ull << 12;
-      while (ns * 2 * sizeof(ClaimEntry) <= B / 2) ns *= 2;
+      while (ns * 2 * sizeof(ClaimEntry) <= B / div) ns *= 2;
       KC_TRY(cs_.init(ns, st_));
       hot_limit_ = ns / 2;
       q_max_ = std::max<uint64_t>(CLAIM_TILE * 32, hot_limit_ / 3) / 256 * 256;
@@ -959,6 +963,8 @@ class EngineT final : public EngineBase {
       if (wk && atoll(wk) > 0) cc.window_keys = (uint64_t)atoll(wk);
       const char* bb = getenv("KC_COLD_BLOOM_BITS");  // filter bits per key (0 = no filters; A/B)
       if (bb) cc.bloom_bits = atoi(bb);
+      const char* ck = getenv("KC_COLD_CACHE");       // KC_COLD_CACHE=0: no HBM copies of run keys (A/B)
+      cc.cache_keys = !(ck && ck[0] == '0');
       KC_TRY(cold_.init(cc));
     } else {
       KC_TRY(cs_.clear(st_));
