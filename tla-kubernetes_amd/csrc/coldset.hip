@@ -30,25 +30,27 @@ __device__ __forceinline__ uint64_t bloom_hash(uint64_t k) {
 
 __host__ __device__ __forceinline__ uint64_t dir_bucket(uint64_t k, int dbits) { return k >> (64 - dbits); }
 
-// dir[b] = first index whose bucket is >= b (b in [0, 2^dbits]); thread i
+// dir[b] = first index whose bucket is >= b (b in [0, 2^dbits]): thread i
 // writes the buckets in (bucket(i-1), bucket(i)], thread n the tail.
-__global__ void k_run_dir(const uint64_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ dir, int dbits) {
+// Directory and filter in one pass over the keys (a merged run is read
+// over the host link once, not twice).
+__global__ void k_run_meta(const uint64_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ dir, int dbits,
+                           uint32_t* __restrict__ bloom, uint64_t nblocks) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n) return;
   const uint64_t nb = 1ull << dbits;
-  const uint64_t hi = i < n ? dir_bucket(keys[i], dbits) : nb;
-  const uint64_t lo = i > 0 ? dir_bucket(keys[i - 1], dbits) + 1 : 0;
+  const uint64_t k = i < n ? keys[i] : 0;
+  const uint64_t hi = i < n ? dir_bucket(k, dbits) : nb;
+  // the previous key's bucket: a neighbour lane's load (same line), or a load
+  const uint64_t prev = __shfl_up(k, 1, 64);
+  const uint64_t kp = i == 0 ? 0 : ((threadIdx.x & 63) ? prev : keys[i - 1]);
+  const uint64_t lo = i > 0 ? dir_bucket(kp, dbits) + 1 : 0;
   for (uint64_t b = lo; b <= hi; ++b) dir[b] = i;
-}
-
-__global__ void k_bloom_add(const uint64_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ bloom,
-                            uint64_t nblocks) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t k = keys[i];
-  uint32_t* blk = bloom + bloom_block(k, nblocks) * 16;
-  uint64_t h = bloom_hash(k);
-  for (int j = 0; j < kBloomK; ++j, h >>= 9) atomicOr(&blk[(h >> 5) & 15], 1u << (h & 31));
+  if (bloom && i < n) {
+    uint32_t* blk = bloom + bloom_block(k, nblocks) * 16;
+    uint64_t h = bloom_hash(k);
+    for (int j = 0; j < kBloomK; ++j, h >>= 9) atomicOr(&blk[(h >> 5) & 15], 1u << (h & 31));
+  }
 }
 
 // One query against one run, restricted to the run's indices [w0, w1) held
@@ -172,18 +174,21 @@ int ColdSet::pin_get(uint64_t keys, uint64_t** p, uint64_t* cap) {
     return 0;
   }
   const double t0 = now_s();
-  const uint64_t c = keys + keys / 4 + 1024;
+  // power-of-two size classes: runs of the binary-counter tiering recur in
+  // a few sizes, so freed buffers are reused instead of pinning new pages
+  uint64_t c = 1ull << 16;
+  while (c < keys) c *= 2;
   KC_HIP_TRY(hipHostMalloc(p, c * 8));
   *cap = c;
   t_pin_ += now_s() - t0;
   return 0;
 }
-// Back to the pool; the pool keeps its 4 largest buffers.
+// Back to the pool; the pool keeps its 6 largest buffers.
 void ColdSet::pin_put(uint64_t* p, uint64_t cap) {
   if (!p) return;
   pool_.push_back({p, cap});
   std::sort(pool_.begin(), pool_.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
-  while (pool_.size() > 4) {
+  while (pool_.size() > 6) {
     (void)hipHostFree(pool_.back().first);
     pool_.pop_back();
   }
@@ -319,7 +324,6 @@ int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
   r.dbits = dbits;
   r.meta_bytes = dir_bytes;
   meta_used_ += dir_bytes;
-  hipLaunchKernelGGL(k_run_dir, dim3(grid_of(r.n + 1)), dim3(256), 0, st, keys, r.n, r.d_dir, dbits);
   // filter bits per key: the target, or what the budget has left
   uint64_t bits = (uint64_t)cfg_.bloom_bits;
   if (cfg_.meta_hbm_bytes && r.n) {
@@ -333,8 +337,9 @@ int ColdSet::build_meta(ColdRun& r, const uint64_t* keys, hipStream_t st) {
     KC_HIP_TRY(hipMemsetAsync(r.d_bloom, 0, fb, st));
     r.meta_bytes += fb;
     meta_used_ += fb;
-    hipLaunchKernelGGL(k_bloom_add, dim3(grid_of(r.n)), dim3(256), 0, st, keys, r.n, r.d_bloom, r.nblocks);
   }
+  hipLaunchKernelGGL(k_run_meta, dim3(grid_of(r.n + 1)), dim3(256), 0, st, keys, r.n, r.d_dir, dbits, r.d_bloom,
+                     r.nblocks);
   KC_HIP_TRY(hipGetLastError());
   peak_meta_ = std::max(peak_meta_, meta_used_ + cache_used_);
   return 0;
