@@ -252,6 +252,48 @@ __global__ void k_contains(const uint64_t* __restrict__ fps, uint64_t n,
   if (i < n) seen[i] = (uint8_t)fpset_contains(slots, nbuckets, fps[i]);
 }
 
+// A combined round of <= SMALL_MAX single puts/contains (kc_fpset_put from
+// TLC's worker threads): ONE launch of one workgroup that reads the
+// fingerprints from pinned host memory and writes the answers and counts
+// straight back into it, so a round costs one launch and one sync instead of
+// copies, a batch table and two syncs.  Sequential semantics inside the
+// round: a fingerprint equal to an earlier one of the round is "already
+// present" for a put (the earlier one inserted it).
+constexpr int SMALL_MAX = 1024;
+__global__ void __launch_bounds__(SMALL_MAX) k_small_round(const uint64_t* __restrict__ in, uint32_t n, int op,
+                                                           unsigned long long* __restrict__ slots, uint64_t nbuckets,
+                                                           uint8_t* __restrict__ seen_out,
+                                                           unsigned long long* __restrict__ stats_out) {
+  __shared__ unsigned long long sh[SMALL_MAX];
+  __shared__ unsigned int sh_new, sh_full;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) sh_new = sh_full = 0;
+  const uint64_t fp = t < n ? normalize_fp(in[t]) : 0;
+  if (t < n) sh[t] = fp;
+  __syncthreads();
+  if (t < n) {
+    bool dup = false;
+    for (uint32_t j = 0; j < t && !dup; ++j) dup = sh[j] == fp;
+    uint8_t seen;
+    if (op == 1) {
+      seen = (uint8_t)fpset_contains(slots, nbuckets, fp);
+    } else if (dup) {
+      seen = 1;
+    } else {
+      const int r = fpset_insert(slots, nbuckets, fp);
+      if (r == 1) atomicAdd(&sh_new, 1u);
+      if (r < 0) atomicAdd(&sh_full, 1u);
+      seen = r == 0 ? 1 : 0;
+    }
+    seen_out[t] = seen;
+  }
+  __syncthreads();
+  if (t == 0) {
+    stats_out[0] = sh_new;
+    stats_out[1] = sh_full;
+  }
+}
+
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9e3779b97f4a7c15ull;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -430,9 +472,33 @@ struct kc_fpset {
   uint64_t part_cap = 0, part_off_cap = 0;
   uint8_t* scan_tmp = nullptr;
   uint64_t scan_cap = 0;
+  uint8_t* h_small = nullptr;   // pinned: SMALL_MAX fps, SMALL_MAX answers, 2 counts (k_small_round)
   std::mutex mu;
   Combiner comb;
 };
+
+// One combined round of n <= SMALL_MAX requests (op 0 put, 1 contains).
+static int small_round(kc_fpset* s, const uint64_t* fps, size_t n, int op, uint8_t* seen) {
+  std::lock_guard<std::mutex> g(s->mu);
+  KC_HIP_TRY(hipSetDevice(s->device));
+  if (!s->h_small) KC_HIP_TRY(hipHostMalloc(&s->h_small, SMALL_MAX * 9 + 64));
+  if (op == 0) KC_TRY(s->fs.reserve(n, s->stream));
+  uint64_t* hf = reinterpret_cast<uint64_t*>(s->h_small);
+  uint8_t* hs = s->h_small + SMALL_MAX * 8;
+  unsigned long long* hc = reinterpret_cast<unsigned long long*>(s->h_small + SMALL_MAX * 9 + 8 - (SMALL_MAX * 9) % 8);
+  memcpy(hf, fps, n * 8);
+  hipLaunchKernelGGL(k_small_round, dim3(1), dim3(SMALL_MAX), 0, s->stream, hf, (uint32_t)n, op, s->fs.slots,
+                     s->fs.nbuckets, hs, hc);
+  KC_HIP_TRY(hipGetLastError());
+  KC_HIP_TRY(hipStreamSynchronize(s->stream));
+  if (hc[1]) {
+    set_error("fpset full");
+    return -ENOMEM;
+  }
+  s->fs.count += hc[0];
+  memcpy(seen, hs, n);
+  return 0;
+}
 
 // Sum the striped stats rows (syncs the stream).
 static int read_stats(kc_fpset* s, hipStream_t st, unsigned long long out[4]) {
@@ -520,6 +586,7 @@ void kc_fpset_destroy(kc_fpset* s) {
   if (s->d_fps) (void)hipFree(s->d_fps);
   if (s->d_seen) (void)hipFree(s->d_seen);
   if (s->d_stats) (void)hipFree(s->d_stats);
+  if (s->h_small) (void)hipHostFree(s->h_small);
   for (void* p : {(void*)s->part_cnt, (void*)s->part_off, (void*)s->scan_tmp})
     if (p) (void)hipFree(p);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -816,8 +883,10 @@ static int combine_one(kc_fpset* s, uint64_t fp, int op, uint8_t* result) {
       size_t b = a;
       std::vector<uint64_t> fps;
       while (b < batch.size() && batch[b].op == batch[a].op) fps.push_back(batch[b++].fp);
-      const int rc = batch[a].op == 0 ? kc_fpset_put_batch(s, fps.data(), fps.size(), seen.data() + a)
-                                      : kc_fpset_contains_batch(s, fps.data(), fps.size(), seen.data() + a);
+      const int rc = fps.size() <= (size_t)SMALL_MAX
+                         ? small_round(s, fps.data(), fps.size(), batch[a].op, seen.data() + a)
+                         : batch[a].op == 0 ? kc_fpset_put_batch(s, fps.data(), fps.size(), seen.data() + a)
+                                            : kc_fpset_contains_batch(s, fps.data(), fps.size(), seen.data() + a);
       const std::string m = rc < 0 ? std::string(last_error()) : std::string();
       for (size_t k = a; k < b; ++k) {
         rcs[k] = rc;
