@@ -123,3 +123,17 @@ def test_seen_spill_np2_full(fixtures):
     assert r.complete and s["flushes"] > 5 and s["peak_hbm_bytes"] <= 4 << 30
     assert s["cold_fps"] + 0 <= r.distinct
     print(f"\nNP=2 seen-set 4 GiB: {r.seconds:.2f} s, {s}")
+
+
+@pytest.mark.parametrize("kw", [{}, dict(variant=3), dict(nc=2), dict(variant=1, invariants=7)])
+def test_seen_spill_with_frontier_spill(model1_ref, fixtures, tmp_path, kw):
+    # both spills at once (TLC's DiskStateQueue + OffHeapDiskFPSet, MC.out:5):
+    # frontiers in a StateQueue over HBM/host/disk and the seen-set under a
+    # 4 MiB budget; results equal the all-in-HBM engine's
+    ref = model1_ref[0] if not kw else _run(**kw)[0]
+    r, _ = _run(**kw, seen_hbm_bytes=4 * MiB, frontier_hbm_bytes=48 << 10, frontier_host_bytes=64 << 10,
+                frontier_segment_states=384, spill_dir=str(tmp_path))
+    _same(r, ref)
+    if not kw:
+        assert r.seen["flushes"] >= 2 and r.frontier_spilled_bytes > 0
+    assert os.listdir(tmp_path) == []

@@ -1162,7 +1162,7 @@ class EngineT final : public EngineBase {
       }
       const uint64_t next_gidx = level_gidx + n;
       if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + cand + 1, true));
-      KC_TRY(cs_.reserve(cand, st_));
+      if (!spill_) KC_TRY(cs_.reserve(cand, st_));
       const uint64_t cmax = std::min(n, chunk);
       {
         const uint64_t tiles = (cmax + CLAIM_TILE - 1) / CLAIM_TILE;
@@ -1214,6 +1214,8 @@ class EngineT final : public EngineBase {
           return -EIO;
         }
         const State* cur = reinterpret_cast<const State*>(p);
+        // seen-set spill: a chunk whose insertions fit the hot table (may flush it)
+        if (spill_) KC_TRY(spill_cut(cur, m, &m));
         ++res->levels_chunks;
         const unsigned tiles = (unsigned)((m + CLAIM_TILE - 1) / CLAIM_TILE);
         KC_HIP_TRY(hipMemsetAsync(claim_args_.ovf.count, 0, 8, st_));
@@ -1228,21 +1230,32 @@ class EngineT final : public EngineBase {
           hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
                              cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
+                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                             spill_ ? ttot_ : (uint32_t*)nullptr);
           hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
-                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
+                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, spill_ ? ttot_ : (uint32_t*)nullptr);
         });
-        size_t tmp_bytes = 0;
-        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)m, st_));
-        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-        hipError_t scan_err = hipSuccess;
-        timed(KK_SCAN, [&] {
-          scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)m, st_);
-        });
-        KC_HIP_TRY(scan_err);
-        KC_HIP_TRY(hipMemcpyAsync(h_last_, offsets_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
-        KC_HIP_TRY(hipMemcpyAsync(h_last_ + 1, newmask_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
+        if (spill_) {
+          // the tile-count path: the cold check clears winners and recounts tiles
+          timed(KK_SCAN, [&] {
+            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
+          });
+          KC_TRY(spill_check(cur, m, tiles));
+          KC_HIP_TRY(hipMemcpyAsync(h_last_, toff_ + tiles, 4, hipMemcpyDeviceToHost, st_));
+          h_last_[1] = 0;
+        } else {
+          size_t tmp_bytes = 0;
+          const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+          KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)m, st_));
+          KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+          hipError_t scan_err = hipSuccess;
+          timed(KK_SCAN, [&] {
+            scan_err = hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)m, st_);
+          });
+          KC_HIP_TRY(scan_err);
+          KC_HIP_TRY(hipMemcpyAsync(h_last_, offsets_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
+          KC_HIP_TRY(hipMemcpyAsync(h_last_ + 1, newmask_ + m - 1, 4, hipMemcpyDeviceToHost, st_));
+        }
         KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
         KC_HIP_TRY(hipStreamSynchronize(st_));
         collect_times();
@@ -1253,10 +1266,12 @@ class EngineT final : public EngineBase {
         timed(KK_EMIT, [&] {
           hipLaunchKernelGGL(k_emit<M>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st_, cur, m, start,
                              flags_, newmask_, offsets_, reinterpret_cast<State*>(dst), level_new, level_gidx,
-                             next_gidx, parent_, ord_, cfg_.keep_trace, d_ctr_);
+                             next_gidx, parent_, ord_, cfg_.keep_trace, d_ctr_,
+                             spill_ ? (const uint32_t*)toff_ : (const uint32_t*)nullptr);
         });
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_,
-                           (const uint32_t*)nullptr, (uint64_t)0, (unsigned long long*)nullptr);
+                           spill_ ? (const uint32_t*)toff_ : (const uint32_t*)nullptr, (uint64_t)(spill_ ? tiles : 0),
+                           (unsigned long long*)nullptr);
         KC_HIP_TRY(hipGetLastError());
         if (nn) KC_TRY(q_->commit(nn, st_));
         level_new += nn;
@@ -1276,7 +1291,7 @@ class EngineT final : public EngineBase {
       }
       const uint64_t cand_now = h_ctr_->cand_total;
       hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);   // next level's head
-      cs_.count += level_new;
+      cs_.count = spill_ ? hot_count_ : cs_.count + level_new;
       res->peak_frontier = std::max<uint64_t>(res->peak_frontier, n);
       if (seen_err != ~0ull) {
         KC_TRY(report_error(res, seen_err, level, level_gidx, n, have_parent ? &err_parent : nullptr));
