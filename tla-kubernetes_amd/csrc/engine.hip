@@ -50,8 +50,9 @@ const char* kActionNames[A_COUNT] = {
 __global__ void __launch_bounds__(64)
 k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask, uint64_t n,
           Counters* __restrict__ C, const uint32_t* __restrict__ tile_off, uint64_t tiles,
-          unsigned long long* __restrict__ host) {
+          unsigned long long* __restrict__ host, unsigned long long* __restrict__ ovf_count = nullptr) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
+  if (ovf_count && threadIdx.x == 0) *ovf_count = 0;   // the next chunk's candidate overflow list starts empty
   unsigned long long v = C->s[threadIdx.x].next_cand;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -335,7 +336,6 @@ class EngineT final : public EngineBase {
         ++res->levels_chunks;
         const unsigned grid = (unsigned)((cn + 255) / 256);
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
-        KC_HIP_TRY(hipMemsetAsync(claim_args_.ovf.count, 0, 8, st_));
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
@@ -360,10 +360,9 @@ class EngineT final : public EngineBase {
           });
         }
         timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
-          hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start,
-                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
+          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
+                             cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                             (uint32_t*)nullptr, tiles, claim_args_.ovf);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
                              tscan_ ? ttot_ : (uint32_t*)nullptr);
@@ -425,7 +424,8 @@ class EngineT final : public EngineBase {
         const bool last = start + cn >= n;
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_,
                            tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)tiles,
-                           last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr);
+                           last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr,
+                           claim_args_.ovf.count);
       }
       KC_HIP_TRY(hipGetLastError());
       if (headcopy_) {
@@ -904,6 +904,9 @@ class EngineT final : public EngineBase {
     KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
     KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
     if (!d_ovf_cnt_) KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
+    // empty at the level's start (a run that stopped mid-level may have left
+    // entries); k_advance empties it again after every chunk
+    KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
     claim_args_.ovf = CandOvf{d_ovf_cnt_, ovf_fp_, ovf_lk_, ovf_tile_,
                               std::min(ovf_fp_cap_, std::min(ovf_lk_cap_, ovf_tile_cap_))};
     const uint64_t b = rcount_cap_ * 4 + rec_fp_cap_ * 8 + rec_lk_cap_ * 4 + ovf_fp_cap_ * 8 + ovf_lk_cap_ * 4 +
@@ -1218,17 +1221,15 @@ class EngineT final : public EngineBase {
         if (spill_) KC_TRY(spill_cut(cur, m, &m));
         ++res->levels_chunks;
         const unsigned tiles = (unsigned)((m + CLAIM_TILE - 1) / CLAIM_TILE);
-        KC_HIP_TRY(hipMemsetAsync(claim_args_.ovf.count, 0, 8, st_));
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur, m, start, flags_,
                              cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level, abl_mask_, rcount_, rec_fp_,
                              rec_lk_, newmask_, d_ctr_, claim_args_);
         });
         timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u);
-          hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
-                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, (uint32_t*)nullptr);
+          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, m, start,
+                             cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                             (uint32_t*)nullptr, tiles, claim_args_.ovf);
           hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
                              cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
                              spill_ ? ttot_ : (uint32_t*)nullptr);
@@ -1271,7 +1272,7 @@ class EngineT final : public EngineBase {
         });
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_,
                            spill_ ? (const uint32_t*)toff_ : (const uint32_t*)nullptr, (uint64_t)(spill_ ? tiles : 0),
-                           (unsigned long long*)nullptr);
+                           (unsigned long long*)nullptr, claim_args_.ovf.count);
         KC_HIP_TRY(hipGetLastError());
         if (nn) KC_TRY(q_->commit(nn, st_));
         level_new += nn;

@@ -51,7 +51,8 @@ struct Counters {
   unsigned long long batch_used;  // >0: a batch-table probe run overflowed (retry)
   unsigned long long cand_total;  // sum of the next_cand stripes (k_advance)
   unsigned long long level_new;   // sharded insert: new states of the level (local + records)
-  unsigned long long head_pad[10];
+  unsigned long long emit_done;   // sharded insert: emit workgroups done (the last one reads the totals)
+  unsigned long long head_pad[9];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -556,15 +557,16 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
 // The same passes over the chunk's overflow list (after k_settle_rec<PASS>:
 // a PASS-1 winner then adds itself to its tile's count).
 template <int PASS>
-static __global__ void __launch_bounds__(256)
-k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
-             uint32_t* __restrict__ tile_total) {
+__device__ __forceinline__ void settle_ovf_blocks(uint32_t blk, uint32_t nblk, const CandOvf& ovf, uint64_t n,
+                                                  uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+                                                  uint32_t level, uint32_t* __restrict__ newmask,
+                                                  Counters* __restrict__ C, uint32_t rank,
+                                                  uint32_t* __restrict__ tile_total) {
   const unsigned long long c = *ovf.count;
   const uint64_t cnt = c < ovf.cap ? c : ovf.cap;
-  if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(&stripe(C).cand_ovf, (unsigned long long)cnt);
+  if (PASS == 0 && blk == 0 && threadIdx.x == 0 && cnt) atomicAdd(&stripe(C).cand_ovf, (unsigned long long)cnt);
   unsigned long long reads = 0;
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * blockDim.x) {
+  for (uint64_t k = (uint64_t)blk * blockDim.x + threadIdx.x; k < cnt; k += (uint64_t)nblk * blockDim.x) {
     const unsigned int tile = ovf.tile[k];
     const int v = settle_record<PASS>(tile, ovf.fp[k], &ovf.lk[k], n, base, cs, nbuckets, level, newmask, C, rank);
     reads += v ? 1 : 0;
@@ -574,7 +576,18 @@ k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs
   for (int off = 32; off > 0; off >>= 1) reads += __shfl_down(reads, off, 64);
   if ((threadIdx.x & 63) == 0 && reads) atomicAdd(&stripe(C).settles, reads);
 }
+template <int PASS>
+static __global__ void __launch_bounds__(256)
+k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ tile_total) {
+  settle_ovf_blocks<PASS>(blockIdx.x, gridDim.x, ovf, n, base, cs, nbuckets, level, newmask, C, rank, tile_total);
+}
 constexpr unsigned SETTLE_OVF_GRID = 1024;
+// blocks of settle pass A's launch that take the overflow list (pass A needs
+// no counts, so its overflow work shares the tiles' launch; pass B's adds to
+// the tile counts the tile blocks compute, so it runs in a launch of its own)
+constexpr unsigned SETTLE_OVF_BLOCKS = 256;
 
 template <int PASS>
 static __global__ void __launch_bounds__(CLAIM_TILE)
@@ -582,7 +595,14 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
              uint32_t level, const unsigned int* __restrict__ rcount,
              const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
              uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
-             uint32_t* __restrict__ tile_total = nullptr) {
+             uint32_t* __restrict__ tile_total = nullptr, uint32_t tiles = 0, CandOvf ovf = CandOvf{}) {
+  // PASS 0 launched with tiles + SETTLE_OVF_BLOCKS blocks: the blocks past
+  // the tiles settle the overflow list
+  if (PASS == 0 && blockIdx.x >= tiles && tiles) {
+    settle_ovf_blocks<0>(blockIdx.x - tiles, gridDim.x - tiles, ovf, n, base, cs, nbuckets, level, newmask, C, rank,
+                         nullptr);
+    return;
+  }
   settle_tile<PASS>(blockIdx.x, n, base, cs, nbuckets, level, rcount, rec_fp, rec_lk, newmask, C, rank, tile_total);
 }
 
