@@ -683,12 +683,17 @@ struct NewCount {
 // counters): 1 = no plan of the new state (the next level's candidate
 // count), 2 = also no invariant check, 3 = also no successor rebuild and no
 // state store (parent pointers only).
-template <class M, int ABL>
+// SH (the sharded insert's own winners, shard.hip k_shard_emit): `parent`
+// takes the parent keys rank << 60 | parent << 16 | position << 8 | action,
+// error keys carry the rank, the output starts at offset 0 (chunk_base is
+// the records' base there), and there is no outdegree (a rank sees only the
+// successors it owns).
+template <class M, int ABL, bool SH = false>
 __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
        const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
        typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
        unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
-       Counters* __restrict__ C, const uint32_t* __restrict__ tile_off) {
+       Counters* __restrict__ C, const uint32_t* __restrict__ tile_off, uint64_t rank = 0) {
   // offsets: per-parent exclusive offsets; or (tile_off != nullptr) per
   // 256-parent block, the wave bases then come from the block's own counts
   __shared__ unsigned int sh_act[A_COUNT];
@@ -712,7 +717,7 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
     if (mask) counts = M::plan(load_state<M>(cur, i), f).counts;
   }
   const int cnt = __builtin_popcount(mask);
-  if (i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
+  if (!SH && i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
   const int lane = (int)(threadIdx.x & 63);
   int incl = cnt;
 #pragma unroll
@@ -747,8 +752,8 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
     const int t = __ffs(m) - 1;
     const uint64_t pi = wave0 + (uint64_t)p;
     const uint64_t pidx = base + pi;
-    const uint64_t o = C->chunk_base + obase + (uint64_t)g;
-    if (keep_trace) {
+    const uint64_t o = (SH ? 0ull : C->chunk_base) + obase + (uint64_t)g;
+    if (!SH && keep_trace) {
       parent[next_gidx + o] = level_gidx + pidx;
       ord[next_gidx + o] = (uint8_t)t;
     }
@@ -760,9 +765,11 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
     typename M::State x;
     M::apply(s, slot, j, f, x);
     store_state<M>(next, o - next_base, x);   // next_base: the StateQueue run starts at o = next_base
-    if (ABL < 2 && M::check(x, f.inv_mask) >= 0)
-      atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)t << 8) | E_INVARIANT);
-    atomicAdd(&sh_act[M::slot_action(s, slot)], 1u);
+    const int act = M::slot_action(s, slot);
+    const uint64_t key = (SH ? rank << 60 : 0ull) | (pidx << 16) | ((uint64_t)t << 8);
+    if (SH) parent[next_gidx + o] = key | (uint64_t)act;
+    if (ABL < 2 && M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, key | E_INVARIANT);
+    atomicAdd(&sh_act[act], 1u);
     if (ABL == 0) {
       const typename M::Plan px = M::plan(x, f);
       cand += (unsigned long long)px.total;
@@ -775,7 +782,7 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
   __syncthreads();
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
-  if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
+  if (!SH && threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
     atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }

@@ -119,33 +119,40 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
 // Owner totals (world > 1; 0 at world 1) into tot and straight into pinned
 // host memory, with the level head (error key, overflow flags): what the
 // host reads after expand, with no copy launches.
-__device__ __forceinline__ void head_to_host(const Counters* __restrict__ C, unsigned long long* __restrict__ h) {
-  h[0] = C->err_key;
-  h[1] = C->chunk_base;
-  h[2] = C->overflow;
-  h[3] = C->batch_used;
-  h[4] = C->cand_total;
-  h[5] = C->level_new;
+// (device-scope loads: the last emit workgroup reads what the others' atomics wrote)
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Level head reset at the start of expand (one launch instead of two fills).
-__global__ void k_head_reset(Counters* __restrict__ C) {
+__device__ __forceinline__ void head_to_host(const Counters* __restrict__ C, unsigned long long* __restrict__ h) {
+  h[0] = ld_agent(&C->err_key);
+  h[1] = ld_agent(&C->chunk_base);
+  h[2] = ld_agent(&C->overflow);
+  h[3] = ld_agent(&C->batch_used);
+  h[4] = ld_agent(&C->cand_total);
+  h[5] = ld_agent(&C->level_new);
+}
+// Level head reset at the start of expand (one launch instead of fills),
+// with the candidate overflow list's count.
+__global__ void k_head_reset(Counters* __restrict__ C, unsigned long long* __restrict__ ovf_count) {
   if (threadIdx.x == 0) {
     C->err_key = ~0ull;
     C->chunk_base = 0;
     C->overflow = 0;
     C->batch_used = 0;
+    C->emit_done = 0;
+    *ovf_count = 0;
   }
 }
 // row != nullptr (ShardBase::expand_dev): the all-gather row too, in device
 // memory: totals, status_new, status_err (level 1: an Init-state invariant
 // key, 0x12, found by expand takes the status slot, as Group::run does), and
 // the failure word.
-__global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
-                               uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
-                               const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
-                               unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
-                               uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err,
-                               uint64_t rank) {
+__device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                                             uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
+                                             const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                                             unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
+                                             uint64_t status_new, uint64_t status_err, int level1,
+                                             uint64_t init_err) {
   const uint32_t o = threadIdx.x;
   if (o == 0) {
     head_to_host(C, host_head);
@@ -173,6 +180,13 @@ __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t*
   tot[o] = v;
   host_tot[o] = v;
   if (row && o < world) row[o] = v;
+}
+__global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                               uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
+                               const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                               unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
+                               uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err) {
+  owner_totals(off, cnt, n, world, tot, C, host_tot, host_head, row, status_new, status_err, level1, init_err);
 }
 
 // Record flags: 0 = out, 1 = candidate, 2 = inserted its fp, 3 = displacer.
@@ -227,21 +241,105 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
     isnew[i] = w;
   }
 }
-// One settle pass over this rank's own claim tiles (blocks [0, tiles)) and
-// the received records (the blocks after them), in one launch: the passes
-// of the two commute (atomicMax claims; a displaced candidate has no bit).
+// One settle pass over this rank's own claim tiles (blocks [0, tiles)), the
+// received records (the next rblocks) and the tiles' candidate overflow list
+// (the blocks after those), in one launch: the passes of the three commute
+// (atomicMax claims; a displaced candidate has no bit; with no per-tile
+// counts here, overflow winners set their bits like tile winners).  Pass A
+// also resets the level's error key for the emits.
 template <class M, int PASS>
 __global__ void __launch_bounds__(256)
-k_settle_both(uint32_t tiles, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
-              uint32_t rank, const unsigned int* __restrict__ rcount, const unsigned long long* __restrict__ rec_fp,
-              unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask, const Record<M>* __restrict__ in,
-              uint64_t n, const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
-              uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots,
+              uint32_t level, uint32_t rank, const unsigned int* __restrict__ rcount,
+              const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
+              uint32_t* __restrict__ newmask, const Record<M>* __restrict__ in, uint64_t n,
+              const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
+              uint32_t* __restrict__ isnew, Counters* __restrict__ C, CandOvf ovf) {
   static_assert(CLAIM_TILE == 256, "one block size for both halves");
+  if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0) C->err_key = ~0ull;   // (nothing before the emits sets it)
   if (blockIdx.x < tiles)
     settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank, nullptr);
-  else
+  else if (blockIdx.x < tiles + rblocks)
     rec_settle<M, PASS>(blockIdx.x - tiles, in, n, cs, nslots, level, rank, rfp, flag, newmask, n_local, isnew, C);
+  else
+    settle_ovf_blocks<PASS>(blockIdx.x - tiles - rblocks, gridDim.x - tiles - rblocks, ovf, n_local, 0, cs, nslots,
+                            level, newmask, C, rank, nullptr);
+}
+constexpr unsigned SHARD_OVF_BLOCKS = 256;
+
+// Narrow levels: both exclusive scans (own winners' popcounts, records'
+// isnew flags) and k_shard_base's totals in one workgroup, instead of two
+// device scans and a launch.
+constexpr uint64_t SHARD_SMALL_SCAN = 16384;
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) lds[wv] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t t = lds[k];
+    if (k < wv) before += t;
+    total += t;
+  }
+  __syncthreads();
+  return before + x - v;
+}
+// Narrow levels at world > 1: the owner-major exclusive scan of the count
+// matrix and k_owner_totals in one workgroup (instead of a device scan's two
+// launches and the totals launch).
+constexpr uint64_t OWNER_SMALL_SCAN = 16384;
+__global__ void __launch_bounds__(1024)
+k_owner_scan_small(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint64_t n, uint32_t world,
+                   uint64_t* __restrict__ tot, const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                   unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row, uint64_t status_new,
+                   uint64_t status_err, int level1, uint64_t init_err) {
+  __shared__ uint32_t lds[16];
+  const uint64_t cells = n * world;
+  uint32_t carry = 0, total = 0;
+  for (uint64_t b = 0; b < cells; b += blockDim.x) {
+    const uint64_t i = b + threadIdx.x;
+    const uint32_t v = i < cells ? cnt[i] : 0u;
+    const uint32_t e = block_exclusive_scan(v, lds, total);
+    if (i < cells) off[i] = carry + e;
+    carry += total;
+  }
+  __syncthreads();       // (the scan's global writes, for the totals' reads below)
+  if (threadIdx.x < 64)
+    owner_totals(off, cnt, n, world, tot, C, host_tot, host_head, row, status_new, status_err, level1, init_err);
+}
+__global__ void __launch_bounds__(1024)
+k_shard_scan_small(const uint32_t* __restrict__ newmask, uint64_t nlocal, uint32_t* __restrict__ offsets,
+                   const uint32_t* __restrict__ isnew, uint64_t nrec, uint32_t* __restrict__ ioff,
+                   Counters* __restrict__ C) {
+  __shared__ uint32_t lds[16];
+  uint32_t carry = 0, tot = 0;
+  for (uint64_t b = 0; b < nlocal; b += blockDim.x) {
+    const uint64_t i = b + threadIdx.x;
+    const uint32_t v = i < nlocal ? NewCount()(newmask[i]) : 0u;
+    const uint32_t e = block_exclusive_scan(v, lds, tot);
+    if (i < nlocal) offsets[i] = carry + e;
+    carry += tot;
+  }
+  const uint32_t lt = carry;
+  carry = 0;
+  for (uint64_t b = 0; b < nrec; b += blockDim.x) {
+    const uint64_t i = b + threadIdx.x;
+    const uint32_t v = i < nrec ? isnew[i] : 0u;
+    const uint32_t e = block_exclusive_scan(v, lds, tot);
+    if (i < nrec) ioff[i] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    C->chunk_base = lt;
+    C->level_new = (uint64_t)lt + carry;
+  }
 }
 
 // chunk_base = this rank's own new states (the records' emit base);
@@ -256,78 +354,20 @@ __global__ void k_shard_base(const uint32_t* __restrict__ offsets, const uint32_
   C->level_new = lt + rt;
 }
 
-// cand_total = sum of the next_cand stripes (one lane per stripe)
-// (then the level head straight into pinned host memory, host_head)
-__global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C,
-                                                   unsigned long long* __restrict__ host_head) {
-  static_assert(CTR_STRIPES == 64, "one lane per stripe");
-  unsigned long long v = C->s[threadIdx.x].next_cand;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  if (threadIdx.x == 0) {
-    C->cand_total = v;
-    head_to_host(C, host_head);
-  }
-}
-
-// The winners among this rank's own successors (newmask), in parent order.
+// The winners among the received records, after the local ones (one
+// workgroup's share).
 template <class M>
-__global__ void __launch_bounds__(256)
-k_shard_emit_local(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uint64_t rank,
-                   const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
-                   typename M::State* __restrict__ next, unsigned long long* __restrict__ pkeys,
-                   uint64_t next_gidx, Counters* __restrict__ C) {
+__device__ __forceinline__ void emit_rec_block(uint64_t blk, const Record<M>* __restrict__ in, uint64_t n,
+                                               const uint32_t* __restrict__ isnew, const uint32_t* __restrict__ ioff,
+                                               Flags f, typename M::State* __restrict__ next,
+                                               unsigned long long* __restrict__ pkeys, uint64_t next_gidx,
+                                               Counters* __restrict__ C) {
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned long long sh_cand;
   if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh_cand = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long cand = 0;
-  if (i < n) {
-    uint32_t mask = newmask[i];
-    if (mask) {
-      const typename M::State s = load_state<M>(cur, i);
-      const typename M::Plan pl = M::plan(s, f);
-      uint64_t o = offsets[i];
-      for (; mask; mask &= mask - 1) {
-        const int t = __ffs(mask) - 1;
-        int slot, j;
-        M::locate(pl, t, slot, j);
-        typename M::State x;
-        M::apply(s, slot, j, f, x);
-        store_state<M>(next, o, x);
-        const int act = M::slot_action(s, slot);
-        const uint64_t key = (rank << 60) | (i << 16) | ((uint64_t)t << 8);
-        pkeys[next_gidx + o] = key | (uint64_t)act;
-        if (M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, key | E_INVARIANT);
-        atomicAdd(&sh_act[act], 1u);
-        cand += (unsigned long long)M::plan(x, f).total;
-        ++o;
-      }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
-  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&sh_cand, cand);
-  __syncthreads();
-  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
-  if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
-}
-
-// The winners among the received records, after the local ones.
-template <class M>
-__global__ void __launch_bounds__(256)
-k_shard_emit_rec(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
-                 const uint32_t* __restrict__ ioff, Flags f, typename M::State* __restrict__ next,
-                 unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C) {
-  __shared__ unsigned int sh_act[A_COUNT];
-  __shared__ unsigned long long sh_cand;
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
-  if (threadIdx.x == 0) sh_cand = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = blk * blockDim.x + threadIdx.x;
   unsigned long long cand = 0;
   if (i < n && isnew[i]) {
     typename M::State x;
@@ -348,6 +388,55 @@ k_shard_emit_rec(const Record<M>* __restrict__ in, uint64_t n, const uint32_t* _
     atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
 }
+// cand_total = sum of the next_cand stripes (one lane per stripe), then the
+// level head straight into pinned host memory
+__device__ __forceinline__ void level_tail(Counters* __restrict__ C, unsigned long long* __restrict__ host_head) {
+  static_assert(CTR_STRIPES == 64, "one lane per stripe");
+  unsigned long long v = ld_agent(&C->s[threadIdx.x].next_cand);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if (threadIdx.x == 0) {
+    C->cand_total = v;
+    __threadfence();
+    head_to_host(C, host_head);
+  }
+}
+__global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C,
+                                                   unsigned long long* __restrict__ host_head) {
+  level_tail(C, host_head);
+}
+// Both emits in one launch: blocks [0, lblocks) this rank's own winners
+// (the engine's wave-balanced emit body, engine_kernels.h emit_body, with
+// parent keys), the rest the records'.  Narrow levels (tail != 0): the last
+// workgroup to finish runs k_shard_cand's tail; a wide level's grid would
+// queue that many device-scope atomics and fences on one counter
+// (measured: NP=2 sharded 172 -> 680 ms), so it takes the separate launch.
+template <class M>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_shard_emit(const typename M::State* __restrict__ cur, uint64_t n_local, uint32_t lblocks, Flags f, uint64_t rank,
+             const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
+             const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
+             const uint32_t* __restrict__ ioff, typename M::State* __restrict__ next,
+             unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C,
+             unsigned long long* __restrict__ host_head, int tail) {
+  __shared__ bool sh_last;
+  if (blockIdx.x < lblocks)
+    emit_body<M, 0, true>(cur, n_local, 0, f, newmask, offsets, next, 0, 0, next_gidx, pkeys, nullptr, 1, C, nullptr,
+                          rank);
+  else
+    emit_rec_block<M>(blockIdx.x - lblocks, in, n, isnew, ioff, f, next, pkeys, next_gidx, C);
+  if (!tail) return;
+  // every thread's atomics (error key, stripes) before this workgroup counts as done
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) sh_last = atomicAdd(&C->emit_done, 1ull) == gridDim.x - 1;
+  __syncthreads();
+  if (!sh_last || threadIdx.x >= 64) return;
+  __threadfence();
+  if (threadIdx.x == 0) C->emit_done = 0;
+  level_tail(C, host_head);
+}
+constexpr unsigned SHARD_TAIL_BLOCKS = 64;    // emit grids up to this size run the level tail themselves
 
 template <class M>
 class ShardT final : public ShardBase {
@@ -381,6 +470,7 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
+    KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));     // (zeroed by k_head_reset every level)
     KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipEventCreate(&ev_[0]));
     KC_HIP_TRY(hipEventCreate(&ev_[1]));
@@ -462,7 +552,7 @@ class ShardT final : public ShardBase {
   }
   int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
-    hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
+    hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_, d_ovf_cnt_);
     send_total_ = 0;
     dev_init_err_ = init_err_;
     init_err_ = ~0ull;
@@ -472,7 +562,7 @@ class ShardT final : public ShardBase {
       if (d_row)
         hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, (uint64_t)0, (uint32_t)world_,
                            d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
-                           d_row, status_new, status_err, (int)level1, dev_init_err_, (uint64_t)rank_);
+                           d_row, status_new, status_err, (int)level1, dev_init_err_);
       dev_empty_ = d_row == nullptr;
       dev_zero_ = true;
       return 0;
@@ -494,9 +584,7 @@ class ShardT final : public ShardBase {
       KC_TRY(grow_buffer_tight(ovf_fp_, ovf_fp_cap_, bound, st_));
       KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
       KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
-      if (!d_ovf_cnt_) KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
       ovf_ = CandOvf{d_ovf_cnt_, ovf_fp_, ovf_lk_, ovf_tile_, std::min(ovf_fp_cap_, std::min(ovf_lk_cap_, ovf_tile_cap_))};
-      KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
     }
     KC_TRY(grow_buffer(newmask_, mask_cap_, n_, false, st_));
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
@@ -532,15 +620,21 @@ class ShardT final : public ShardBase {
                 (unsigned long long)cells);
       return -ENOMEM;
     }
-    if (world_ > 1) {
-      size_t tmp_bytes = 0;
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
-      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
+    if (world_ > 1 && cells <= OWNER_SMALL_SCAN) {
+      hipLaunchKernelGGL(k_owner_scan_small, dim3(1), dim3(1024), 0, st_, cnt_, off_, n_, (uint32_t)world_,
+                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                         d_row, status_new, status_err, (int)level1, dev_init_err_);
+    } else {
+      if (world_ > 1) {
+        size_t tmp_bytes = 0;
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
+      }
+      hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
+                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                         d_row, status_new, status_err, (int)level1, dev_init_err_);
     }
-    hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
-                       d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
-                       d_row, status_new, status_err, (int)level1, dev_init_err_, (uint64_t)rank_);
     KC_HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -656,7 +750,6 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_insert: more than 2^31 records or parents in one level");
       return -ENOMEM;
     }
-    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->err_key, 0xff, 8, st_));
     KC_TRY(cs_.reserve(cand_ + n, st_));     // count excludes this level's local inserts (<= cand_)
     const uint32_t succ_level = (uint32_t)level_ + 1;
     const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
@@ -669,52 +762,49 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL(k_rec_claim<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
                          succ_level, rfp_, flag_, d_ctr_);
     }
-    // settle pass A (local tiles and records in one launch), then pass B
-    const unsigned lt = n_ ? tiles : 0u, sgrid = lt + (n ? rgrid : 0u);
-    if (sgrid) {
-      hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
-                         succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
-                         isnew_, d_ctr_);
-      if (lt)
-        hipLaunchKernelGGL(k_settle_ovf<0>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
-                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, (uint32_t*)nullptr);
-      hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, n_, cs_.t, cs_.nslots,
-                         succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_,
-                         isnew_, d_ctr_);
-      if (lt)
-        hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
-                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, (uint32_t*)nullptr);
-    }
+    // settle pass A (own tiles, records and the tiles' overflow list in one
+    // launch), then pass B; n_ = 0 with n > 0 still runs pass A's first
+    // workgroup, which resets the error key
+    const unsigned lt = n_ ? tiles : 0u, ob = n_ ? SHARD_OVF_BLOCKS : 0u;
+    const unsigned sgrid = std::max(lt + (n ? rgrid : 0u) + ob, 1u);
+    hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(sgrid), dim3(256), 0, st_, lt, n ? rgrid : 0u, n_, cs_.t,
+                       cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
+                       flag_, isnew_, d_ctr_, ovf_);
+    hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, n ? rgrid : 0u, n_, cs_.t,
+                       cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
+                       flag_, isnew_, d_ctr_, ovf_);
     // positions: this rank's own winners first, then the records'
-    size_t tmp_bytes = 0;
-    if (n_) {
-      KC_TRY(grow_buffer(offsets_, offsets_cap_, n_, false, st_));
-      const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)n_, st_));
-      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+    if (n_) KC_TRY(grow_buffer(offsets_, offsets_cap_, n_, false, st_));
+    if (n_ <= SHARD_SMALL_SCAN && n <= SHARD_SMALL_SCAN) {
+      hipLaunchKernelGGL(k_shard_scan_small, dim3(1), dim3(1024), 0, st_, newmask_, n_, offsets_, isnew_, n, ioff_,
+                         d_ctr_);
+    } else {
+      size_t tmp_bytes = 0;
+      if (n_) {
+        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+      }
+      if (n) {
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
+      }
+      hipLaunchKernelGGL(k_shard_base, dim3(1), dim3(64), 0, st_, offsets_, newmask_, n_, ioff_, isnew_, n, d_ctr_);
     }
-    if (n) {
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
-      KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-      KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
-    }
-    hipLaunchKernelGGL(k_shard_base, dim3(1), dim3(64), 0, st_, offsets_, newmask_, n_, ioff_, isnew_,
-                       n, d_ctr_);
     // capacity: at most one new state per own successor and per record
     const uint64_t bound = cand_ + n;
     KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const uint64_t next_gidx = level_base_.back() + n_;
     KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + bound + 1, true, st_));
-    if (n_)
-      hipLaunchKernelGGL(k_shard_emit_local<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
-                         cur_, n_, flags_, (uint64_t)rank_, newmask_, offsets_, next_, pkeys_, next_gidx,
-                         d_ctr_);
-    if (n)
-      hipLaunchKernelGGL(k_shard_emit_rec<M>, dim3(rgrid), dim3(256), 0, st_, in, n, isnew_, ioff_,
-                         flags_, next_, pkeys_, next_gidx, d_ctr_);
-    hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_,
-                       reinterpret_cast<unsigned long long*>(h_ctr_));
+    const unsigned lb = (unsigned)((n_ + 255) / 256), eg = std::max(lb + (n ? rgrid : 0u), 1u);
+    const int tail = eg <= SHARD_TAIL_BLOCKS;
+    hipLaunchKernelGGL(k_shard_emit<M>, dim3(eg), dim3(256), 0, st_, cur_, n_, lb, flags_, (uint64_t)rank_, newmask_,
+                       offsets_, in, n, isnew_, ioff_, next_, pkeys_, next_gidx, d_ctr_,
+                       reinterpret_cast<unsigned long long*>(h_ctr_), tail);
+    if (!tail)
+      hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_, reinterpret_cast<unsigned long long*>(h_ctr_));
     KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipStreamSynchronize(st_));
     if (h_ctr_->overflow || h_ctr_->batch_used) {
