@@ -374,6 +374,29 @@ typedef struct kc_group kc_group;
 int kc_rccl_unique_id(uint8_t *id_out /* KC_RCCL_ID_BYTES */);
 int kc_group_create_rccl(kc_shard *s, const uint8_t *id, kc_group **out);
 int kc_group_create_local(kc_shard **shards, int nshards, kc_group **out);
+/* One shard per process with the caller's own transport (MPI, gloo,
+ * sockets) instead of RCCL: the loop calls these on host buffers, from the
+ * thread that called kc_group_run; each returns 0 or < 0 (the run then fails
+ * with -EIO on every rank that sees it; like RCCL's, a transport failure on
+ * one rank only is the transport's to surface).  Every rank makes the same
+ * sequence of calls.
+ *   all_gather:     out[r * n + k] = rank r's in[k]  (n words)
+ *   exchange:       this rank's all-to-all as kc_exchange_plan lists it, in
+ *                   BYTES: xfers[4k..4k+3] = peer, 1 send / 0 receive, byte
+ *                   offset into sendbuf / recvbuf, bytes; post all of them,
+ *                   then wait (the k-th send from s to d pairs with the k-th
+ *                   receive at d from s)
+ *   broadcast:      *v from rank `root` to every rank
+ *   all_reduce_sum: v[0..n) summed over ranks, in place
+ * kubecheck.distributed.GlooHostComm implements it over torch.distributed. */
+typedef struct kc_host_comm {
+  void *ctx;
+  int (*all_gather)(void *ctx, const uint64_t *in, uint64_t n, uint64_t *out);
+  int (*exchange)(void *ctx, const uint64_t *xfers, int nxfers, const void *sendbuf, void *recvbuf);
+  int (*broadcast)(void *ctx, int root, uint64_t *v);
+  int (*all_reduce_sum)(void *ctx, uint64_t *v, uint64_t n);
+} kc_host_comm;
+int kc_group_create_host(kc_shard *s, const kc_host_comm *comm, kc_group **out);
 void kc_group_destroy(kc_group *g);
 int kc_group_run(kc_group *g, kc_result *res);
 /* Canonical tuple of trace state i of the last run's error; returns words. */

@@ -72,7 +72,8 @@ def test_struct_layouts_match_header(tmp_path):
     """The ctypes mirrors of the C structs have the header's sizes and field
     offsets (compiled with the host C compiler against include/kubecheck.h)."""
     structs = {"kc_model_config": _lib.KcModelConfig, "kc_result": _lib.KcResult,
-               "kc_squeue_config": _lib.KcSqueueConfig, "kc_squeue_stats": _lib.KcSqueueStats}
+               "kc_squeue_config": _lib.KcSqueueConfig, "kc_squeue_stats": _lib.KcSqueueStats,
+               "kc_host_comm": _lib.KcHostComm}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "kubecheck.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')

@@ -1,0 +1,115 @@
+"""The native sharded level loop with ONE SHARD PER PROCESS at world 2 and 3,
+on the one-GPU box: the layout `bench.py --gpus N` runs on N GPUs (RcclComm),
+which RCCL itself refuses on one device ("duplicate GPU", tools/gpu_r03_rccl2.sh).
+Here the collectives go over gloo through kc_group_create_host (HostComm,
+shard_driver.hip): the same Group::run with one local shard and R > 1, the
+device all-gather rows written by k_owner_totals, the exchange plan handed
+over whole, the cross-rank broadcast of the error walk and the failure word.
+Results must equal the fixtures exactly, as for the emulated ranks
+(tests/test_gpu_shard.py)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    {"name": "model1", "kw": {}},
+    {"name": "model1_hostrows", "kw": {}, "env": {"KC_DEVROW": "0"}},
+    {"name": "model1_pieces", "kw": {}, "env": {"KC_PIECE_BYTES": "4096"}},
+    {"name": "np2_40", "kw": {"np": 2, "max_levels": 40}},
+    {"name": "nc2", "kw": {"nc": 2}},
+    {"name": "variant2", "kw": {"variant": 2}},
+    {"name": "variant5", "kw": {"variant": 5}},
+    {"name": "ns0", "kw": {"ns": 0}},
+    {"name": "lost_update", "kw": {"variant": 1, "invariants": 7}},
+    {"name": "fault_pack", "kw": {}, "env": {"KC_FAULT": "1:7:1"}, "all_ranks": True},
+    {"name": "fault_expand_hostrows", "kw": {}, "env": {"KC_FAULT": "0:9:0", "KC_DEVROW": "0"}, "all_ranks": True},
+]
+
+
+def run_ranks(world, tmp_path):
+    spec = tmp_path / "cases.json"
+    spec.write_text(json.dumps(CASES))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.join(ROOT, "tests", "hostcomm_worker.py"), str(spec)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    out = {}
+    for line in p.stdout.splitlines():
+        if line.startswith("RESULT "):
+            r = json.loads(line[7:])
+            out.setdefault(r["case"], {})[r["rank"]] = r
+    return out
+
+
+@pytest.fixture(scope="module", params=[2, 3])
+def results(request, tmp_path_factory):
+    return request.param, run_ranks(request.param, tmp_path_factory.mktemp(f"hc{request.param}"))
+
+
+def test_model1_exact(results, fixtures):
+    world, res = results
+    fx = fixtures["model1"]
+    for name in ("model1", "model1_hostrows", "model1_pieces"):
+        r = res[name][0]
+        assert "exception" not in r, r.get("exception")
+        assert r["complete"] and r["error"] is None and r["world"] == world
+        assert r["level_width"] == fx["level_width"], name
+        assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+        assert r["act_gen"] == fx["act_gen"]
+        assert r["records_sent"] > 0          # records really crossed processes
+
+
+def test_np2_prefix_exact(results, fixtures):
+    _, res = results
+    fx = fixtures["np2_40levels"]
+    r = res["np2_40"][0]
+    assert r["level_width"] == fx["level_width"] and not r["complete"]
+    assert r["act_gen"] == fx["act_gen"]
+
+
+@pytest.mark.parametrize("key,name,kind", [("nc2", "nc2", "assertion"), ("variant2", "variant2", "invariant"),
+                                           ("variant5", "variant5", "invariant"), ("ns0", "ns0", "deadlock"),
+                                           ("variant1_lost_update", "lost_update", "invariant")])
+def test_errors_and_traces(results, fixtures, oracle, key, name, kind):
+    _, res = results
+    fx = fixtures[key]
+    r = res[name][0]
+    assert r["error"] == kind
+    assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
+    if kind == "assertion":
+        assert r["error_action"] == fx["err_action"]
+    if name == "lost_update":
+        assert r["error_invariant"] == "NoLostUpdate"
+    # the walk-back crossed ranks (broadcast); the trace is a real behaviour
+    kw = {"nc2": dict(nc=2), "ns0": dict(ns=0)}.get(name, {})
+    cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1),
+                        variant={"variant2": 2, "variant5": 5, "lost_update": 1}.get(name, 0),
+                        invariants=7 if name == "lost_update" else 3)
+    for a, b in zip(r["trace"], r["trace"][1:]):
+        succ, _ = oracle.successors(cfg, a)
+        assert any(list(map(int, x)) == b for _, x in succ)
+
+
+def test_fault_stops_every_rank(results):
+    world, res = results
+    for name in ("fault_pack", "fault_expand_hostrows"):
+        got = res[name]
+        assert sorted(got) == list(range(world)), name
+        for rk, r in got.items():
+            assert "exception" in r, (name, rk)
+            assert "injected fault" in r["exception"] or "failed" in r["exception"], r["exception"]

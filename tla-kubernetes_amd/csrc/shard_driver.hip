@@ -372,6 +372,106 @@ class RcclComm final : public Comm {
   size_t cap_ = 0;
 };
 
+// One shard per process; the collectives are the caller's (kc_host_comm:
+// MPI, gloo, sockets), on host buffers.  Structured like RcclComm: the
+// kernels write the all-gather row in device memory (k_owner_totals), and the
+// all-to-all is the same exchange plan, handed over whole (byte offsets into
+// pinned staging copies of the send and receive buffers).  Besides serving
+// hosts without RCCL, it runs the one-shard-per-process loop at world > 1 on
+// a single GPU, which RCCL refuses ("duplicate GPU"): tests/test_gpu_hostcomm.py.
+class HostComm final : public Comm {
+ public:
+  HostComm(ShardBase* s, const kc_host_comm& ops) : s_(s), ops_(ops) {}
+  ~HostComm() override {
+    if (drow_) (void)hipFree(drow_);
+    if (hrow_) (void)hipHostFree(hrow_);
+    if (hsend_) (void)hipHostFree(hsend_);
+    if (hrecv_) (void)hipHostFree(hrecv_);
+  }
+  int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
+    const size_t L = rows[0].size();
+    out.assign(L * (size_t)s_->world(), 0);
+    return call(ops_.all_gather(ops_.ctx, rows[0].data(), L, out.data()), "all_gather");
+  }
+  uint64_t* row_buffer(size_t i, size_t L) override {
+    if (i != 0) return nullptr;
+    if (L > row_cap_) {
+      if (drow_) (void)hipFree(drow_);
+      if (hrow_) (void)hipHostFree(hrow_);
+      drow_ = nullptr;
+      hrow_ = nullptr;
+      row_cap_ = 0;
+      if (hipMalloc(&drow_, L * 8) != hipSuccess || hipHostMalloc(&hrow_, L * 8) != hipSuccess) return nullptr;
+      row_cap_ = L;
+    }
+    return drow_;
+  }
+  int all_gather_dev(size_t L, std::vector<uint64_t>& out) override {
+    KC_HIP_TRY(hipMemcpyAsync(hrow_, drow_, L * 8, hipMemcpyDeviceToHost, s_->stream()));
+    KC_HIP_TRY(hipStreamSynchronize(s_->stream()));
+    out.assign(L * (size_t)s_->world(), 0);
+    return call(ops_.all_gather(ops_.ctx, hrow_, L, out.data()), "all_gather");
+  }
+  int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
+                 const std::vector<void*>& recv) override {
+    const int me = s_->rank(), R = s_->world();
+    uint64_t ns = 0, nr = 0;
+    for (int p = 0; p < R; ++p) {
+      ns += Mx[me][p];
+      nr += Mx[p][me];
+    }
+    KC_TRY(pinned(hsend_, hsend_cap_, ns * rb));
+    KC_TRY(pinned(hrecv_, hrecv_cap_, nr * rb));
+    hipStream_t st = s_->stream();
+    if (ns) KC_HIP_TRY(hipMemcpyAsync(hsend_, send[0], ns * rb, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));            // every record packed and staged
+    const std::vector<Xfer> plan = exchange_plan(Mx, me, std::max<uint64_t>(1, piece_bytes() / rb));
+    std::vector<uint64_t> xf(4 * plan.size());
+    for (size_t k = 0; k < plan.size(); ++k) {
+      xf[4 * k] = (uint64_t)plan[k].peer;
+      xf[4 * k + 1] = (uint64_t)plan[k].send;
+      xf[4 * k + 2] = plan[k].off * rb;
+      xf[4 * k + 3] = plan[k].n * rb;
+    }
+    KC_TRY(call(ops_.exchange(ops_.ctx, xf.data(), (int)plan.size(), hsend_, hrecv_), "exchange"));
+    if (nr) KC_HIP_TRY(hipMemcpyAsync(recv[0], hrecv_, nr * rb, hipMemcpyHostToDevice, st));
+    return 0;                                        // stream-ordered before insert
+  }
+  int broadcast(int root, uint64_t* v) override { return call(ops_.broadcast(ops_.ctx, root, v), "broadcast"); }
+  int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
+    out = v[0];
+    return call(ops_.all_reduce_sum(ops_.ctx, out.data(), out.size()), "all_reduce_sum");
+  }
+
+ private:
+  static int call(int rc, const char* what) {
+    if (rc < 0) {
+      set_error("kc_host_comm %s failed (%d)", what, rc);
+      return -EIO;
+    }
+    return 0;
+  }
+  // pinned staging, grown (the previous contents are not kept); the stream
+  // is idle here: every use follows a synchronisation of it
+  int pinned(uint8_t*& p, uint64_t& cap, uint64_t bytes) {
+    if (bytes <= cap) return 0;
+    KC_HIP_TRY(hipStreamSynchronize(s_->stream()));
+    if (p) KC_HIP_TRY(hipHostFree(p));
+    p = nullptr;
+    cap = std::max<uint64_t>(bytes, 2 * cap);
+    KC_HIP_TRY(hipHostMalloc(&p, cap));
+    return 0;
+  }
+  ShardBase* s_;
+  kc_host_comm ops_;
+  uint64_t* drow_ = nullptr;
+  uint64_t* hrow_ = nullptr;
+  size_t row_cap_ = 0;
+  uint8_t* hsend_ = nullptr;
+  uint8_t* hrecv_ = nullptr;
+  uint64_t hsend_cap_ = 0, hrecv_cap_ = 0;
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------- driver
@@ -741,6 +841,20 @@ int kc_group_create_rccl(kc_shard* s, const uint8_t* id, kc_group** out) {
   KC_NCCL_TRY(api->comm_init_rank(&comm, sh->world(), uid, sh->rank()));
   *out = new kc_group{std::unique_ptr<Group>(
       new Group({sh}, std::unique_ptr<Comm>(new RcclComm(sh, comm)), sh->config()))};
+  return 0;
+}
+
+int kc_group_create_host(kc_shard* s, const kc_host_comm* comm, kc_group** out) {
+  if (!s || !comm || !out) { set_error("kc_group_create_host: NULL"); return -EINVAL; }
+  *out = nullptr;
+  if (!comm->all_gather || !comm->exchange || !comm->broadcast || !comm->all_reduce_sum) {
+    set_error("kc_group_create_host: every kc_host_comm callback is required");
+    return -EINVAL;
+  }
+  ShardBase* sh = s->impl.get();
+  KC_HIP_TRY(hipSetDevice(sh->device()));
+  *out = new kc_group{std::unique_ptr<Group>(
+      new Group({sh}, std::unique_ptr<Comm>(new HostComm(sh, *comm)), sh->config()))};
   return 0;
 }
 

@@ -78,6 +78,18 @@ class KcSqueueStats(C.Structure):
 # (name, restype, argtypes) for every symbol of include/kubecheck.h
 _P = C.c_void_p
 _U64P = C.POINTER(C.c_uint64)
+
+# kc_host_comm: the caller's collectives for kc_group_create_host
+HC_ALL_GATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64))
+HC_EXCHANGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int, C.c_void_p, C.c_void_p)
+HC_BROADCAST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_uint64))
+HC_ALL_REDUCE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64)
+
+
+class KcHostComm(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("all_gather", HC_ALL_GATHER), ("exchange", HC_EXCHANGE),
+                ("broadcast", HC_BROADCAST), ("all_reduce_sum", HC_ALL_REDUCE)]
+
 _U8P = C.POINTER(C.c_uint8)
 _IP = C.POINTER(C.c_int)
 SIGNATURES = [
@@ -147,6 +159,7 @@ SIGNATURES = [
     ("kc_rccl_unique_id", C.c_int, [C.c_char_p]),
     ("kc_group_create_rccl", C.c_int, [_P, C.c_char_p, C.POINTER(_P)]),
     ("kc_group_create_local", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(_P)]),
+    ("kc_group_create_host", C.c_int, [_P, C.POINTER(KcHostComm), C.POINTER(_P)]),
     ("kc_group_destroy", None, [_P]),
     ("kc_group_run", C.c_int, [_P, C.POINTER(KcResult)]),
     ("kc_group_trace_tuple", C.c_int, [_P, C.c_int, _U64P]),

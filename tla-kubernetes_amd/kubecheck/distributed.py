@@ -30,7 +30,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import ACTIONS, INVARIANTS, ModelConfig, Spec
-from ._lib import KcResult, check, load
+from ._lib import (HC_ALL_GATHER, HC_ALL_REDUCE, HC_BROADCAST, HC_EXCHANGE, KcHostComm, KcResult, check,
+                   load)
 
 NONE_KEY = (1 << 64) - 1       # "no error" (the library's ~0)
 M44 = (1 << 44) - 1
@@ -130,6 +131,81 @@ class HipShard:
             self._h = C.c_void_p()
 
 
+class GlooHostComm:
+    """kc_host_comm over a torch.distributed process group on host tensors
+    (gloo): the native level loop with one shard per process and a transport
+    other than RCCL (kc_group_create_host).  Several ranks may then share one
+    GPU, which RCCL refuses ("duplicate GPU"); the tests use it to run the
+    one-shard-per-process loop at world > 1 on the one-GPU box.  Callbacks
+    run on the thread inside kc_group_run; an exception becomes rc -1 (the
+    loop then fails with -EIO) and is kept in `.errors`."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self._t, self._d, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.errors: List[str] = []
+        self.ops = KcHostComm(None, HC_ALL_GATHER(self._guard(self._all_gather)),
+                              HC_EXCHANGE(self._guard(self._exchange)),
+                              HC_BROADCAST(self._guard(self._broadcast)),
+                              HC_ALL_REDUCE(self._guard(self._all_reduce)))
+
+    def _guard(self, fn):
+        def call(*a):
+            try:
+                fn(*a)
+                return 0
+            except Exception as e:          # noqa: BLE001  (crosses the C-ABI as rc -1)
+                self.errors.append(f"{fn.__name__}: {e!r}")
+                return -1
+        return call
+
+    def _words(self, ptr, n):
+        return self._t.from_numpy(np.ctypeslib.as_array(ptr, (int(n),)).view(np.int64))
+
+    def _all_gather(self, _ctx, inp, n, out):
+        src = self._words(inp, n).clone()
+        parts = [self._t.empty(int(n), dtype=self._t.int64) for _ in range(self.world)]
+        self._d.all_gather(parts, src, group=self.group)
+        self._words(out, n * self.world).copy_(self._t.cat(parts))
+
+    def _exchange(self, _ctx, xf, nx, sendbuf, recvbuf):
+        x = np.ctypeslib.as_array(xf, (int(nx), 4)).astype(np.int64) if nx else np.zeros((0, 4), np.int64)
+        sends, recvs = x[x[:, 1] == 1], x[x[:, 1] == 0]
+        span = lambda v: int((v[:, 2] + v[:, 3]).max()) if len(v) else 0   # noqa: E731
+        sb = np.ctypeslib.as_array((C.c_uint8 * max(span(sends), 1)).from_address(sendbuf)) if len(sends) else None
+        rb = np.ctypeslib.as_array((C.c_uint8 * max(span(recvs), 1)).from_address(recvbuf)) if len(recvs) else None
+        reqs, piece = [], {}
+        own_s, own_r = [], []
+        for peer, snd, off, nb in x.tolist():
+            if peer == self.rank:                      # (never planned today: own claims stay in place)
+                (own_s if snd else own_r).append((off, nb))
+                continue
+            k = piece.get((peer, snd), 0)              # k-th piece of this (peer, direction): tag k
+            piece[(peer, snd)] = k + 1
+            if snd:
+                reqs.append(self._d.isend(self._t.from_numpy(sb[off: off + nb]), peer, group=self.group, tag=k))
+            else:
+                reqs.append(self._d.irecv(self._t.from_numpy(rb[off: off + nb]), peer, group=self.group, tag=k))
+        for (so, nb), (ro, _) in zip(own_s, own_r):
+            rb[ro: ro + nb] = sb[so: so + nb]
+        for r in reqs:
+            r.wait()
+
+    def _broadcast(self, _ctx, root, v):
+        t = self._words(v, 1).clone()
+        self._d.broadcast(t, src=int(root), group=self.group)
+        self._words(v, 1).copy_(t)
+
+    def _all_reduce(self, _ctx, v, n):
+        t = self._words(v, n).clone()
+        self._d.all_reduce(t, group=self.group)
+        self._words(v, n).copy_(t)
+
+
 class NativeShardedChecker:
     """The sharded BFS with the native level loop (libkubecheck kc_group_*):
     the same protocol and result dict as :class:`ShardedModelChecker`, with
@@ -140,9 +216,13 @@ class NativeShardedChecker:
       it, every rank joins one RCCL communicator.
     * ``NativeShardedChecker(cfg, emulate=R)``: ranks 0..R-1 in this process
       on one GPU, collectives by device copies (the multi-rank protocol on
-      one GPU)."""
+      one GPU).
+    * ``transport="host"``: one shard per process as with RCCL, the
+      collectives over the torch.distributed group on host buffers
+      (:class:`GlooHostComm`, kc_group_create_host)."""
 
-    def __init__(self, cfg: ModelConfig, rank: int = 0, world: int = 1, emulate: int = 0, group=None):
+    def __init__(self, cfg: ModelConfig, rank: int = 0, world: int = 1, emulate: int = 0, group=None,
+                 transport: str = "rccl"):
         self._lib = load()
         self.cfg = cfg
         self._c = cfg.to_c()
@@ -164,6 +244,14 @@ class NativeShardedChecker:
             h = C.c_void_p()
             check("kc_shard_create", self._lib.kc_shard_create(C.byref(self._c), rank, world, C.byref(h)))
             self._shards.append(h)
+            self.world = world
+            if transport == "host":
+                self.host_comm = GlooHostComm(group)
+                check("kc_group_create_host",
+                      self._lib.kc_group_create_host(h, C.byref(self.host_comm.ops), C.byref(self._g)))
+                self.records_sent = 0
+                self.record_bytes = int(self._lib.kc_shard_record_bytes(self._shards[0]))
+                return
             uid = C.create_string_buffer(128)
             if rank == 0:
                 check("kc_rccl_unique_id", self._lib.kc_rccl_unique_id(uid))
@@ -179,7 +267,11 @@ class NativeShardedChecker:
 
     def run(self) -> dict:
         r = KcResult()
-        check("kc_group_run", self._lib.kc_group_run(self._g, C.byref(r)))
+        rc = self._lib.kc_group_run(self._g, C.byref(r))
+        hc = getattr(self, "host_comm", None)
+        if rc < 0 and hc is not None and hc.errors:
+            raise RuntimeError(f"kc_group_run: host transport failed: {hc.errors[0]}")
+        check("kc_group_run", rc)
         self.records_sent = int(self._lib.kc_group_records_sent(self._g))
         na = len(ACTIONS)
         out = {
