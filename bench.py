@@ -98,7 +98,11 @@ def roofline_bfs(times, res, S):
                               op).  The kernel's LDS tile dedup lets about half
                               of the successors skip their probe, so the
                               achieved figure is an effective rate; `traffic`
-                              (PMC) is what the kernel actually moved.
+                              (PMC) is what the kernel actually moved.  A
+                              parent of a deferred frontier is
+                              rebuilt there: + S (its state written into the
+                              frontier) + 9 (its trace entry read); the read of
+                              its own parent is the S above.
       settle (k_settle_rec) : per candidate 12 (record read) + 64 (probe line);
                               per parent 8 (newmask + newcnt write)
       emit   (k_emit)       : per parent 8 (mask + offset); per new state S + 9
@@ -107,10 +111,12 @@ def roofline_bfs(times, res, S):
       scan                  : per parent 8
     """
     parents = res["parents"]
+    dfr = res.get("deferred", 0)
     per_kernel = {
-        "expand": parents * S + res["succ"] * 64,
+        "expand": parents * S + res["succ"] * 64 + dfr * (S + 9),
         "resolve": res["settles"] * (12 + 64) + parents * 8,
-        "emit": parents * 8 + res["new"] * (2 * S + 9),
+        # (deferred levels: k_emit_links writes only the 9-B trace entry)
+        "emit": parents * 8 + res["new"] * (2 * S + 9) if not dfr else parents * 8 + res["new"] * 9,
         "scan": parents * 8,
         # k_narrow runs whole levels (expand + probe + emit); its bytes are
         # only attributable when it ran every level of the check
@@ -240,7 +246,7 @@ def bench_single(args, kw, desc):
         mc.run()
     torch.cuda.synchronize()
     times = {"expand": [0.0, 0], "resolve": [0.0, 0], "scan": [0.0, 0], "emit": [0.0, 0]}
-    acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0, "settles": 0}
+    acc = {"parents": 0, "probes": 0, "succ": 0, "new": 0, "settles": 0, "deferred": 0}
     narrow = [0.0, 0, 0]          # narrow-level kernel: ms, launches, levels
     t0 = time.perf_counter()
     results = []
@@ -258,6 +264,7 @@ def bench_single(args, kw, desc):
         acc["settles"] += r.batch_inserts
         acc["succ"] += r.generated - r.init
         acc["new"] += r.distinct - r.init
+        acc["deferred"] += r.deferred_states
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     r = results[-1]
@@ -281,7 +288,8 @@ def bench_single(args, kw, desc):
                        f", frontiers in the StateQueue with a {args.frontier_hbm_mb} MiB HBM budget"
                        if args.frontier_hbm_mb else ""), "golden_check": golden,
                    "claimset_probes": r.fpset_probes, "settle_reads": r.batch_inserts,
-                   "chunks": r.levels_chunks},
+                   "chunks": r.levels_chunks, "deferred_frontier_states": r.deferred_states,
+                   "deferred_frontier_redone": r.defer_fallback},
     }
     if not args.no_timing:
         S = state_bytes(kw)

@@ -268,6 +268,12 @@ typedef struct {
   double seen_check_seconds;    /* ... in the per-chunk cold checks (queries, sort, probe) */
   uint64_t cand_overflow_records;  /* settle candidates beyond their tile's segment (overflow list) */
   uint64_t cand_buffer_peak_bytes; /* HBM of the candidate-record buffers (tile segments + overflow list) */
+  /* deferred frontier (the default wide path): states rebuilt from their
+   * links inside k_claim (which then also writes them), and whether this run
+   * was redone on the materialising path (an error or a capacity estimate
+   * exceeded; the reported result is the redone run's) */
+  uint64_t deferred_states;
+  uint64_t defer_fallback;
 } kc_result;
 
 typedef struct kc_engine kc_engine;

@@ -66,12 +66,14 @@ def test_multi_chunk_and_rehash_paths(model1):
     assert r.fpset_slots > 64
 
 
-@pytest.mark.parametrize("env", [{"KC_TSCAN_REG": "0"}, {"KC_TSCAN": "0"}, {"KC_HEADCOPY": "1"}])
+@pytest.mark.parametrize("env", [{"KC_TSCAN_REG": "0"}, {"KC_TSCAN": "0", "KC_DEFER": "0"}, {"KC_HEADCOPY": "1"},
+                                 {"KC_DEFER": "0"}])
 def test_wide_level_variants(model1, monkeypatch, env):
     # every level on the wide path (chunk_states turns the narrow kernel
     # off) with: the tile scan's loop path (levels wider than 65,536 tiles
-    # take it; forced here), the per-parent hipcub scan, and the copy +
-    # reset read-back of the level head
+    # take it; forced here), the per-parent hipcub scan (the materialising
+    # path only: the deferred emit takes tile offsets), the copy + reset
+    # read-back of the level head, and the materialising emit (KC_DEFER=0)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     r = run(chunk_states=1 << 20)
@@ -129,11 +131,16 @@ def test_enlarged_prefix(fixtures):
     assert not r.complete
 
 
-def test_enlarged_full(fixtures):
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_enlarged_full(fixtures, monkeypatch, defer):
+    # the whole NP=2 model on the deferred frontier (links in HBM: no trace
+    # store) and on the materialising path
     if "np2_full" not in fixtures:
         pytest.skip("np2_full fixture not generated")
+    monkeypatch.setenv("KC_DEFER", defer)
     fx = fixtures["np2_full"]
     r = run(np=2, keep_trace=False)
+    assert (r.deferred_states > 0) == (defer == "1") and not r.defer_fallback
     assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
     assert r.level_width == fx["level_width"]
     assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
@@ -247,3 +254,48 @@ def test_np3_prefix(fixtures):
     assert r.level_width == fx["level_width"]
     assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
     assert (r.distinct, r.generated) == (fx["distinct"], fx["generated"]) and not r.complete
+
+
+# --- deferred frontier (engine_kernels.h DeferArgs): the wide levels' new
+# states are built inside the next level's k_claim from their links
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_deferred_frontier_exact(fixtures, monkeypatch, defer):
+    monkeypatch.setenv("KC_DEFER", defer)
+    fx = fixtures["np2_40levels"]
+    r = run(np=2, max_levels=40)          # keep_trace: the links are the trace entries
+    assert r.level_width == fx["level_width"]
+    assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    assert r.outdeg_hist == fx["outdeg_hist"]
+    assert (r.deferred_states > 0) == (defer == "1") and not r.defer_fallback
+
+
+def test_deferred_capacity_estimate_redo(fixtures, monkeypatch):
+    # capacity estimates far too small (KC_DEFER_SLACK): the link buffer
+    # (sized by the estimate; no trace store) overflows its guard and the run
+    # is redone on the exact path
+    monkeypatch.setenv("KC_DEFER_SLACK", "0.001")
+    fx = fixtures["np2_40levels"]
+    r = run(np=2, max_levels=40, keep_trace=False)
+    assert r.defer_fallback and r.deferred_states == 0
+    assert r.level_width == fx["level_width"]
+    assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+
+
+@pytest.mark.parametrize("key,kw", [("variant3", dict(variant=3)), ("variant2", dict(variant=2))])
+def test_deferred_error_redone_exactly(fixtures, key, kw):
+    # an error on a deferred wide level (Model_1 on the wide path): the run
+    # is redone on the materialising path, trace state for state
+    fx = fixtures[key]
+    with ModelChecker(ModelConfig(chunk_states=1 << 20, **kw)) as mc:
+        r = mc.run()
+    assert r.defer_fallback
+    assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
+    assert [list(map(int, t)) for t in r.trace] == fx["trace"]
+
+
+def test_deferred_trace_in_host_memory(fixtures):
+    # trace_host: the trace lives in pinned host RAM, the links in HBM
+    fx = fixtures["np2_40levels"]
+    r = run(np=2, max_levels=40, trace_host=True)
+    assert r.deferred_states > 0 and not r.defer_fallback
+    assert r.level_width == fx["level_width"] and r.act_dist == fx["act_dist"]

@@ -69,10 +69,12 @@ k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ new
       host[3] = C->batch_used;
       host[4] = C->cand_total;
       host[5] = C->level_new;
+      host[7] = C->defer_flags;
       C->err_key = ~0ull;
       C->chunk_base = 0;
       C->overflow = 0;
       C->batch_used = 0;
+      C->defer_flags = 0;
     }
   }
 }
@@ -86,6 +88,7 @@ __global__ void k_level_reset(Counters* __restrict__ C) {
     C->chunk_base = 0;
     C->overflow = 0;
     C->batch_used = 0;
+    C->defer_flags = 0;
   }
 }
 
@@ -144,6 +147,15 @@ class EngineT final : public EngineBase {
     if (eo) emit_occ_ = atoi(eo);
     const char* hc = getenv("KC_HEADCOPY");
     headcopy_ = hc && hc[0] == '1';
+    // deferred frontier (engine_kernels.h DeferArgs): the default wide path
+    // (KC_DEFER=0: every level's k_emit builds and stores its new states)
+    const char* df = getenv("KC_DEFER");
+    defer_ = !(df && df[0] == '0') && !spill_ && !queued_ && !ablate_;
+    // KC_DEFER_SLACK: the capacity estimate's factor over the measured
+    // successors per state (tests shrink it to force the exact-path redo)
+    const char* ds = getenv("KC_DEFER_SLACK");
+    if (ds && atof(ds) > 0) defer_slack_ = atof(ds);
+    if (defer_) tscan_ = true;    // the link emit takes the tile offsets
   }
   ~EngineT() override { release(); }
 
@@ -172,7 +184,23 @@ class EngineT final : public EngineBase {
     return 0;
   }
 
+  // A deferred-frontier run that meets anything but a clean level (an error
+  // of any kind, a capacity estimate too small) is redone on the exact,
+  // materialising path from Init: error reports and every count then come
+  // from the path that checks each new state where it is emitted.
   int run(kc_result* res) override {
+    defer_now_ = defer_;
+    int rc = run_once(res);
+    if (rc == kDeferRetry) {
+      ++defer_fallbacks_;
+      defer_now_ = false;
+      rc = run_once(res);
+      res->defer_fallback = 1;
+    }
+    return rc;
+  }
+
+  int run_once(kc_result* res) {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     memset(res, 0, sizeof *res);
     res->err_action = res->err_self = res->err_invariant = -1;
@@ -239,6 +267,7 @@ class EngineT final : public EngineBase {
     cs_.count = ni;
     hot_count_ = ni;
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
+    if (d_ovf_cnt_) KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
     res->init = ni;
     res->generated = ni;
     res->distinct = ni;
@@ -273,12 +302,26 @@ class EngineT final : public EngineBase {
     // offsets are u32 (at most 32 new states per parent: < 2^32 per chunk)
     const uint64_t chunk =
         (std::min<uint64_t>(cfg_.chunk_states ? cfg_.chunk_states : kMaxChunk, kMaxChunk) + 255) / 256 * 256;
+    // Deferred frontier (defer_now_): `mat` = cur_ holds this level's states.
+    // Otherwise the level's k_claim rebuilds them from the previous frontier
+    // (next_, which starts at global index prev_gidx) and the links the
+    // previous level's emit wrote; `cand` is then unknown and the level's
+    // buffers are sized from `ratio`, the last measured successors per state.
+    bool mat = true;
+    uint64_t prev_gidx = 0;
+    double ratio = n ? (double)cand / (double)n : 1.0;
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
-      if (narrow_on_ && n <= (uint64_t)NARROW_MAX) {
+      if (narrow_on_ && n <= (uint64_t)NARROW_MAX &&
+          (mat || (double)n * ratio <= 1.25 * (double)NARROW_CAND_MAX)) {
         // ---- narrow levels: one single-workgroup launch runs as many
         // levels as fit (engine_narrow.h); the host takes over at the first
-        // level it cannot run
+        // level it cannot run.  It needs the states and their exact
+        // successor count: a deferred frontier is materialised first.
+        if (!mat) {
+          KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
+          mat = true;
+        }
         int stop = cfg_.max_levels;
         if (capture_level_ >= level + 1 && (stop == 0 || capture_level_ - 1 < stop)) stop = capture_level_ - 1;
         NarrowRun nr;
@@ -309,12 +352,28 @@ class EngineT final : public EngineBase {
         set_error("kubecheck: level wider than 2^32 states");
         return -ENOMEM;
       }
-      // capacity for this level's output (cand is exact: next_cand of the
-      // previous level)
-      KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
+      // capacity for this level's output: cand is exact (next_cand of the
+      // previous level) when the states are materialised; a deferred level's
+      // is estimated, and a level past the estimate (DF_CAPACITY, a full
+      // candidate list or table) is redone on the exact path
+      const bool dfr = defer_now_;
+      if (mat && n) ratio = std::max(1.0, (double)cand / (double)n);
+      const uint64_t bound = mat ? cand
+                                 : std::min<uint64_t>((uint64_t)((double)n * ratio * defer_slack_) + 4096,
+                                                      (uint64_t)M::MAXSUCC * n);
+      const bool use_link = !cfg_.keep_trace || cfg_.trace_host;   // links in HBM (the trace may be host memory)
+      if (dfr) {
+        if (!mat) KC_TRY(grow_buffer(cur_, cur_cap_, n, false, st_));   // (free: the previous frontier is in next_)
+        if (use_link) KC_TRY(grow_buffer(link_next_, link_next_cap_, std::max<uint64_t>(bound, 1), false, st_));
+      } else {
+        KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
+      }
       const uint64_t next_gidx = level_gidx + n;
-      if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + cand + 1, true));
-      if (!spill_) KC_TRY(cs_.reserve(cand, st_));
+      if (cfg_.keep_trace) KC_TRY(grow_trace(next_gidx + bound + 1, true));
+      // (a deferred level reserves for 16 new states per parent at least:
+      // (count + 16 n) * 2 <= capacity keeps even MAXSUCC = 32 per parent
+      // from filling the table, whatever the estimate)
+      if (!spill_) KC_TRY(cs_.reserve(mat ? bound : std::max<uint64_t>(bound, 16 * n), st_));
       {
         const uint64_t tiles = (std::min(n, chunk) + CLAIM_TILE - 1) / CLAIM_TILE;
         KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
@@ -324,9 +383,16 @@ class EngineT final : public EngineBase {
         }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
-        KC_TRY(cand_overflow(cand, level, n));
+        KC_TRY(cand_overflow(bound, level, n));
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
+      const DeferArgs df = mat ? DeferArgs{} : defer_args(level_gidx, prev_gidx);
+      if (!mat) res->deferred_states += n;
+      uint64_t link_cap = ~0ull;
+      if (dfr) {
+        if (use_link) link_cap = link_next_cap_;
+        if (cfg_.keep_trace) link_cap = std::min<uint64_t>(link_cap, std::min(par_cap_, ord_cap_) - next_gidx);
+      }
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
       const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
       for (uint64_t start = 0, cn = 0; start < n; start += cn) {
@@ -339,7 +405,7 @@ class EngineT final : public EngineBase {
         timed(KK_EXPAND, [&] {
           hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                              start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
+                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_, df);
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
@@ -408,7 +474,11 @@ class EngineT final : public EngineBase {
           });
         }
         timed(KK_EMIT, [&] {
-          if (emit_occ_ == 7)
+          if (dfr)
+            hipLaunchKernelGGL(k_emit_links, dim3(grid), dim3(256), 0, st_, cn, start, newmask_, toff_, level_gidx,
+                               next_gidx, cfg_.keep_trace ? parent_ : nullptr, cfg_.keep_trace ? ord_ : nullptr,
+                               use_link ? link_next_ : nullptr, link_cap, d_ctr_);
+          else if (emit_occ_ == 7)
             hipLaunchKernelGGL((k_emit_occ<M, 7>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
                                cfg_.keep_trace, d_ctr_, toff);
@@ -435,6 +505,8 @@ class EngineT final : public EngineBase {
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
+      // a deferred level with anything to report: redo the run exactly
+      if (dfr && (c.overflow || c.batch_used || c.err_key != ~0ull || c.defer_flags)) return kDeferRetry;
       if (c.overflow || c.batch_used) {
         set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
         return -ENOMEM;
@@ -453,17 +525,37 @@ class EngineT final : public EngineBase {
         fprintf(stderr, "kubecheck: level %d width %llu -> %llu new, %llu distinct\n",
                 level, (unsigned long long)n, (unsigned long long)n_new,
                 (unsigned long long)res->distinct);
-      if (capture_level_ == level + 1 && n_new) {
+      if (!dfr && capture_level_ == level + 1 && n_new) {
         captured_.resize(n_new);
         KC_HIP_TRY(hipMemcpy(captured_.data(), next_, n_new * sizeof(State), hipMemcpyDeviceToHost));
+      }
+      // successors counted this level: the new states' (materialising emit),
+      // or this level's own (a deferred k_claim)
+      const uint64_t dc = c.cand_total - cand_total;
+      cand_total = c.cand_total;
+      if (dfr) {
+        if (!mat && n) ratio = std::max(1.0, (double)dc / (double)n);
+        cand = 0;
+        prev_gidx = level_gidx;
+        mat = false;
+        if (use_link) {
+          std::swap(link_cur_, link_next_);
+          std::swap(link_cur_cap_, link_next_cap_);
+        }
+      } else {
+        cand = dc;
       }
       level_gidx = next_gidx;
       std::swap(cur_, next_);
       std::swap(cur_cap_, next_cap_);
       n = n_new;
-      cand = c.cand_total - cand_total;
-      cand_total += cand;
       ++level;
+      if (dfr && capture_level_ == level && n) {
+        KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
+        mat = true;
+        captured_.resize(n);
+        KC_HIP_TRY(hipMemcpy(captured_.data(), cur_, n * sizeof(State), hipMemcpyDeviceToHost));
+      }
       if (n) {
         if (level > KC_MAX_LEVELS) {
           set_error("kubecheck: more than %d levels", KC_MAX_LEVELS);
@@ -473,6 +565,8 @@ class EngineT final : public EngineBase {
         res->nlevels = level;
       }
     }
+    // the last, unexpanded level (max_levels): its states' invariants
+    if (!mat && n) KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
     last_level_ = res->nlevels;
     last_n_ = n;
     finish(res, t0, n);
@@ -784,7 +878,8 @@ class EngineT final : public EngineBase {
       parent_ = nullptr;
       ord_ = nullptr;
     }
-    for (void* p : {(void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_})
+    for (void* p : {(void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_, (void*)link_cur_,
+                    (void*)link_next_})
       if (p) (void)hipFree(p);
     if (sp_arena_) (void)hipFree(sp_arena_);
     if (sp_tsum_) (void)hipFree(sp_tsum_);
@@ -895,6 +990,40 @@ class EngineT final : public EngineBase {
     return 0;
   }
 
+  // Deferred frontier: the rebuild arguments of the level starting at global
+  // index level_gidx, whose parents (the previous frontier, from prev_gidx)
+  // are in next_; the states go to cur_.
+  DeferArgs defer_args(uint64_t level_gidx, uint64_t prev_gidx) const {
+    DeferArgs df;
+    df.prev = next_;
+    df.out = cur_;
+    if (!cfg_.keep_trace || cfg_.trace_host) {
+      df.link = link_cur_;
+    } else {
+      df.parent = parent_;
+      df.ord = ord_;
+      df.gidx0 = level_gidx;
+      df.prev_gidx0 = prev_gidx;
+    }
+    return df;
+  }
+  // Materialise a deferred frontier of n states into cur_ (k_materialize):
+  // invariants checked (a violation -> kDeferRetry), actions counted, and
+  // the exact successor count of the level into cand.
+  int materialize(uint64_t n, uint64_t level_gidx, uint64_t prev_gidx, uint64_t& cand, uint64_t& cand_total) {
+    KC_TRY(grow_buffer(cur_, cur_cap_, n, false, st_));
+    const DeferArgs df = defer_args(level_gidx, prev_gidx);
+    hipLaunchKernelGGL(k_materialize<M>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st_, df, n, flags_, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (h_ctr_->defer_flags) return kDeferRetry;
+    const uint64_t tot = h_ctr_->next_cand();
+    cand = tot - cand_total;
+    cand_total = tot;
+    return 0;
+  }
+
   // The chunk's candidate overflow list (engine_kernels.h CandOvf), sized by
   // the level's successor count `bound` (no chunk of the level has more), and
   // the peak of the candidate buffers (verbose: per level).
@@ -903,10 +1032,13 @@ class EngineT final : public EngineBase {
     KC_TRY(grow_buffer_tight(ovf_fp_, ovf_fp_cap_, bound, st_));
     KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
     KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
-    if (!d_ovf_cnt_) KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
-    // empty at the level's start (a run that stopped mid-level may have left
-    // entries); k_advance empties it again after every chunk
-    KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
+    // empty when allocated and at every run's start (run(); a run that
+    // stopped mid-level may have left entries); k_advance empties it again
+    // after every chunk, so a level needs no reset launch of its own
+    if (!d_ovf_cnt_) {
+      KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));
+      KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
+    }
     claim_args_.ovf = CandOvf{d_ovf_cnt_, ovf_fp_, ovf_lk_, ovf_tile_,
                               std::min(ovf_fp_cap_, std::min(ovf_lk_cap_, ovf_tile_cap_))};
     const uint64_t b = rcount_cap_ * 4 + rec_fp_cap_ * 8 + rec_lk_cap_ * 4 + ovf_fp_cap_ * 8 + ovf_lk_cap_ * 4 +
@@ -921,6 +1053,15 @@ class EngineT final : public EngineBase {
   unsigned int *ovf_lk_ = nullptr, *ovf_tile_ = nullptr;
   uint64_t ovf_fp_cap_ = 0, ovf_lk_cap_ = 0, ovf_tile_cap_ = 0, cand_buf_peak_ = 0;
   unsigned long long* d_ovf_cnt_ = nullptr;
+  // deferred frontier (DeferArgs): links of the level being expanded / being
+  // emitted, when they are not the (device) trace
+  unsigned long long* link_cur_ = nullptr;
+  unsigned long long* link_next_ = nullptr;
+  uint64_t link_cur_cap_ = 0, link_next_cap_ = 0;
+  static constexpr int kDeferRetry = -100000;
+  bool defer_ = false, defer_now_ = false;
+  double defer_slack_ = 1.25;
+  uint64_t defer_fallbacks_ = 0;
 
   // ---- seen-set spill (cfg.seen_hbm_bytes > 0; engine_spill.h, coldset.h).
   // HBM budget B: the hot ClaimSet takes the largest power-of-two table of

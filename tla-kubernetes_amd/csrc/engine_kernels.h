@@ -52,7 +52,8 @@ struct Counters {
   unsigned long long cand_total;  // sum of the next_cand stripes (k_advance)
   unsigned long long level_new;   // sharded insert: new states of the level (local + records)
   unsigned long long emit_done;   // sharded insert: emit workgroups done (the last one reads the totals)
-  unsigned long long head_pad[9];
+  unsigned long long defer_flags; // deferred frontier (DeferArgs): DF_* bits of the level
+  unsigned long long head_pad[8];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -90,8 +91,12 @@ struct Counters {
   }
 };
 // bytes of the per-level head (err_key, chunk_base, overflow, batch_used,
-// cand_total, level_new): what the host reads back after every level
-constexpr size_t kCtrHead = 6 * sizeof(unsigned long long);
+// cand_total, level_new, emit_done, defer_flags): what the host reads back
+// after every level
+constexpr size_t kCtrHead = 8 * sizeof(unsigned long long);
+// defer_flags: a rebuilt frontier state violates an invariant; a level's
+// links or trace entries did not fit the capacity the host estimated
+constexpr unsigned long long DF_INVARIANT = 1, DF_CAPACITY = 2;
 __device__ __forceinline__ CtrStripe& stripe(Counters* C) {
   return C->s[blockIdx.x & (CTR_STRIPES - 1)];
 }
@@ -245,6 +250,74 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
   return (uint32_t)__umul64hi(fp << 1, (uint64_t)world);
 }
 
+// Deferred frontier (the engine's default wide path): k_emit writes only
+// each new state's link (parent index in its level, successor position) —
+// the trace entries — and the next level's k_claim rebuilds its parent from
+// the previous frontier: load the grandparent, plan, apply the successor,
+// store the state into the frontier buffer, check the invariants and count
+// its action (act_dist).  That work then runs inside k_claim, whose time is
+// set by its random memory operations, instead of in a k_emit of its own.
+// Any invariant violation sets DF_INVARIANT: the host then re-runs the check
+// on the exact (materialising) path, so error reports are unchanged.
+struct DeferArgs {
+  const void* prev = nullptr;                 // the previous frontier (State*); nullptr: cur holds the states
+  const unsigned long long* parent = nullptr; // trace: global parent index per state (keep_trace) ...
+  const uint8_t* ord = nullptr;               // ... and successor position
+  const unsigned long long* link = nullptr;   // or, without a trace: parent index << 8 | position
+  uint64_t gidx0 = 0;                         // global index of this frontier's state 0 (trace path)
+  uint64_t prev_gidx0 = 0;                    // global index of the previous frontier's state 0
+  void* out = nullptr;                        // where the rebuilt states go (State*; the frontier buffer)
+};
+
+// Rebuild frontier state i (index within the level) from its link; stores it
+// into df.out, checks the invariants and counts its action into sh_actd.
+template <class M>
+__device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, uint64_t i, const Flags& f,
+                                                           unsigned int* sh_actd, Counters* __restrict__ C) {
+  uint64_t pp;
+  int t;
+  if (df.link) {
+    const unsigned long long lk = df.link[i];
+    pp = lk >> 8;
+    t = (int)(lk & 0xff);
+  } else {
+    pp = df.parent[df.gidx0 + i] - df.prev_gidx0;
+    t = (int)df.ord[df.gidx0 + i];
+  }
+  const typename M::State gp = load_state<M>(reinterpret_cast<const typename M::State*>(df.prev), pp);
+  const typename M::Plan pl{M::plan(gp, f).counts, 0, -1, -1};
+  int slot, j;
+  M::locate(pl, t, slot, j);
+  typename M::State s;
+  M::apply(gp, slot, j, f, s);
+  store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
+  if (M::check(s, f.inv_mask) >= 0) atomicOr(&C->defer_flags, DF_INVARIANT);
+  atomicAdd(&sh_actd[M::slot_action(gp, slot)], 1u);
+  return s;
+}
+
+// Deferred-frontier materialisation outside k_claim (the level before a
+// narrow run, a max_levels stop, a captured level): the same rebuild, plus
+// the level's successor count (next_cand).
+template <class M>
+__global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, Flags f, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_actd[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh_actd[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cand = 0;
+  if (i < n) {
+    const typename M::State s = defer_rebuild<M>(df, i, f, sh_actd, C);
+    cand = (unsigned long long)M::plan(s, f).total;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&stripe(C).next_cand, cand);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_actd[threadIdx.x])
+    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_actd[threadIdx.x]);
+}
+
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
 // KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only,
 // 3 = plan + fold only (no successor).
@@ -257,12 +330,14 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-        uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh) {
+        uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh, DeferArgs df = DeferArgs{}) {
   constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
   __shared__ unsigned long long sh_fp[NT];
   __shared__ unsigned int sh_key[NT];
   __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
   __shared__ unsigned int sh_act[A_COUNT];
+  __shared__ unsigned int sh_actd[A_COUNT];       // deferred frontier: actions that made the parents
+  __shared__ unsigned long long sh_dcand;         // deferred frontier: the parents' successor count
   __shared__ unsigned int sh_rc;
   __shared__ unsigned int sh_nrep;                // tile representatives
   // SH only (dynamic LDS): remote representatives per parent, then their
@@ -273,6 +348,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if (threadIdx.x == 0) {
     sh_rc = 0;
     sh_nrep = 0;
+    sh_dcand = 0;
   }
   for (int k = threadIdx.x; k < NT; k += CLAIM_TILE) {
     sh_fp[k] = 0ull;
@@ -284,7 +360,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   const uint64_t kbase = SH ? ((uint64_t)sh.rank << CLAIM_RANK_SHIFT) : 0ull;
   sh_cur[threadIdx.x] = 0;
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = 0;
+  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = sh_actd[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t tile = spread_tile(blockIdx.x, gridDim.x, sh.spread);
 #ifdef KC_DIAG
@@ -311,8 +387,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   const bool live = i < n;
   unsigned probes = 0;
   if (live) {
-    const typename M::State s = load_state<M>(cur, i);
+    const typename M::State s =
+        (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
+    // (an LDS total, not a register live through the kernel: k_claim sits at
+    // its 80-VGPR budget for 6 waves per SIMD)
+    if (!SH && df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
     const uint64_t fold = M::fp_fold(s);
     const uint64_t pidx = base + i;
     if (ABL == 0) {
@@ -437,6 +517,11 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
   if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
     atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (!SH && df.prev) {
+    if (threadIdx.x < A_COUNT && sh_actd[threadIdx.x])
+      atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_actd[threadIdx.x]);
+    if (threadIdx.x == 0 && sh_dcand) atomicAdd(&stripe(C).next_cand, sh_dcand);
+  }
 #ifdef KC_DIAG
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -785,6 +870,74 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
   if (!SH && threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
     atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
   if (threadIdx.x == 0 && sh_cand) atomicAdd(&stripe(C).next_cand, sh_cand);
+}
+
+// Deferred frontier's emit (DeferArgs): per new state only its link — the
+// trace entry (global parent index, position) with keep_trace, and/or a
+// level-local parent index << 8 | position (`link`, when the trace is off or
+// in host memory) — plus the outdegree histogram.
+// No state is loaded or built here; the next level's k_claim rebuilds them.
+// Entries at or past `cap` (the host's estimate of the level's new states)
+// are not written and set DF_CAPACITY: the host re-runs on the exact path.
+// Same wave-balanced dealing as emit_body: lane g of a round writes entry
+// obase + g, so a round's stores are contiguous.
+static __global__ void __launch_bounds__(256)
+k_emit_links(uint64_t n, uint64_t base, const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ tile_off,
+             uint64_t level_gidx, uint64_t next_gidx, unsigned long long* __restrict__ parent,
+             uint8_t* __restrict__ ord, unsigned long long* __restrict__ link, uint64_t cap,
+             Counters* __restrict__ C) {
+  __shared__ unsigned int sh_deg[OUTDEG_BINS];
+  __shared__ unsigned int sh_wtot[4];
+  if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t mask = i < n ? newmask[i] : 0u;
+  const int cnt = __builtin_popcount(mask);
+  if (i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
+  const int lane = (int)(threadIdx.x & 63);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  const int wtot = __shfl(incl, 63, 64);
+  const int excl = incl - cnt;
+  if (lane == 0) sh_wtot[threadIdx.x >> 6] = (unsigned int)wtot;
+  __syncthreads();
+  uint64_t obase = C->chunk_base + tile_off[blockIdx.x];
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) obase += sh_wtot[w];
+  const uint64_t wave0 = i - (uint64_t)lane;
+  bool over = false;
+  for (int r = 0; r < wtot; r += 64) {
+    const int g = r + lane;
+    int p = 0;                                       // last lane with excl <= g
+#pragma unroll
+    for (int b = 32; b > 0; b >>= 1) {
+      const int e = __shfl(excl, p + b, 64);
+      if (e <= g) p += b;
+    }
+    int k = g - __shfl(excl, p, 64);
+    uint32_t m = (uint32_t)__shfl((int)mask, p, 64);
+    if (g >= wtot) continue;
+    for (; k > 0; --k) m &= m - 1;
+    const int t = __ffs(m) - 1;
+    const uint64_t pidx = base + wave0 + (uint64_t)p;
+    const uint64_t o = obase + (uint64_t)g;
+    if (o >= cap) {
+      over = true;
+      continue;
+    }
+    if (link) link[o] = (pidx << 8) | (uint64_t)t;
+    if (parent) {
+      parent[next_gidx + o] = level_gidx + pidx;
+      ord[next_gidx + o] = (uint8_t)t;
+    }
+  }
+  if (over) atomicOr(&C->defer_flags, DF_CAPACITY);
+  __syncthreads();
+  if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
+    atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
 }
 
 // Pinned to 8 waves per SIMD (64 VGPRs; unpinned it took 68 = 7 waves):

@@ -113,6 +113,8 @@ class CheckResult:
     seen: Dict[str, float] = field(default_factory=dict)   # seen-set spill statistics (seen_* fields)
     cand_overflow_records: int = 0
     cand_buffer_peak_bytes: int = 0
+    deferred_states: int = 0       # frontier states rebuilt inside k_claim (deferred frontier)
+    defer_fallback: bool = False   # the run was redone on the materialising path
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -140,7 +142,8 @@ def _result(r: KcResult) -> CheckResult:
         frontier_spilled_bytes=r.frontier_spilled_bytes, frontier_reloaded_bytes=r.frontier_reloaded_bytes,
         frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes,
         seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")},
-        cand_overflow_records=r.cand_overflow_records, cand_buffer_peak_bytes=r.cand_buffer_peak_bytes)
+        cand_overflow_records=r.cand_overflow_records, cand_buffer_peak_bytes=r.cand_buffer_peak_bytes,
+        deferred_states=r.deferred_states, defer_fallback=bool(r.defer_fallback))
 
 
 class ModelChecker:
