@@ -101,8 +101,10 @@ def roofline_bfs(times, res, S):
                               (PMC) is what the kernel actually moved.  A
                               parent of a deferred frontier is
                               rebuilt there: + S (its state written into the
-                              frontier) + 9 (its trace entry read); the read of
-                              its own parent is the S above.
+                              frontier) + 9 (its trace entry read) + 8 (its
+                              parent's successor plan read); the read of its
+                              own parent is the S above; and every parent's
+                              plan is written for the next level (+ 8).
       settle (k_settle_rec) : per candidate 12 (record read) + 64 (probe line);
                               per parent 8 (newmask + newcnt write)
       emit   (k_emit)       : per parent 8 (mask + offset); per new state S + 9
@@ -113,7 +115,7 @@ def roofline_bfs(times, res, S):
     parents = res["parents"]
     dfr = res.get("deferred", 0)
     per_kernel = {
-        "expand": parents * S + res["succ"] * 64 + dfr * (S + 9),
+        "expand": parents * S + res["succ"] * 64 + (dfr * (S + 17) + parents * 8 if dfr else 0),
         "resolve": res["settles"] * (12 + 64) + parents * 8,
         # (deferred levels: k_emit_links writes only the 9-B trace entry)
         "emit": parents * 8 + res["new"] * (2 * S + 9) if not dfr else parents * 8 + res["new"] * 9,

@@ -153,6 +153,8 @@ class EngineT final : public EngineBase {
     defer_ = !(df && df[0] == '0') && !spill_ && !queued_ && !ablate_;
     // KC_DEFER_SLACK: the capacity estimate's factor over the measured
     // successors per state (tests shrink it to force the exact-path redo)
+    const char* dp = getenv("KC_DEFER_PC");
+    pc_pass_ = !(dp && dp[0] == '0');
     const char* ds = getenv("KC_DEFER_SLACK");
     if (ds && atof(ds) > 0) defer_slack_ = atof(ds);
     if (defer_) tscan_ = true;    // the link emit takes the tile offsets
@@ -310,6 +312,7 @@ class EngineT final : public EngineBase {
     bool mat = true;
     uint64_t prev_gidx = 0;
     double ratio = n ? (double)cand / (double)n : 1.0;
+    pc_valid_ = false;                 // pc_prev_ holds the previous frontier's plans
     while (n > 0) {
       if (cfg_.max_levels && level >= cfg_.max_levels) break;
       if (narrow_on_ && n <= (uint64_t)NARROW_MAX &&
@@ -322,6 +325,7 @@ class EngineT final : public EngineBase {
           KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
           mat = true;
         }
+        pc_valid_ = false;
         int stop = cfg_.max_levels;
         if (capture_level_ >= level + 1 && (stop == 0 || capture_level_ - 1 < stop)) stop = capture_level_ - 1;
         NarrowRun nr;
@@ -364,6 +368,7 @@ class EngineT final : public EngineBase {
       const bool use_link = !cfg_.keep_trace || cfg_.trace_host;   // links in HBM (the trace may be host memory)
       if (dfr) {
         if (!mat) KC_TRY(grow_buffer(cur_, cur_cap_, n, false, st_));   // (free: the previous frontier is in next_)
+        KC_TRY(grow_buffer(pc_cur_, pc_cur_cap_, n, false, st_));
         if (use_link) KC_TRY(grow_buffer(link_next_, link_next_cap_, std::max<uint64_t>(bound, 1), false, st_));
       } else {
         KC_TRY(grow_buffer(next_, next_cap_, cand ? cand : 1, false, st_));
@@ -386,7 +391,8 @@ class EngineT final : public EngineBase {
         KC_TRY(cand_overflow(bound, level, n));
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
-      const DeferArgs df = mat ? DeferArgs{} : defer_args(level_gidx, prev_gidx);
+      DeferArgs df = mat ? DeferArgs{} : defer_args(level_gidx, prev_gidx);
+      if (dfr && pc_pass_) df.counts_out = pc_cur_;   // this level's plans, for the next level's rebuild
       if (!mat) res->deferred_states += n;
       uint64_t link_cap = ~0ull;
       if (dfr) {
@@ -542,6 +548,9 @@ class EngineT final : public EngineBase {
           std::swap(link_cur_, link_next_);
           std::swap(link_cur_cap_, link_next_cap_);
         }
+        std::swap(pc_cur_, pc_prev_);
+        std::swap(pc_cur_cap_, pc_prev_cap_);
+        pc_valid_ = true;
       } else {
         cand = dc;
       }
@@ -879,7 +888,7 @@ class EngineT final : public EngineBase {
       ord_ = nullptr;
     }
     for (void* p : {(void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_, (void*)link_cur_,
-                    (void*)link_next_})
+                    (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_})
       if (p) (void)hipFree(p);
     if (sp_arena_) (void)hipFree(sp_arena_);
     if (sp_tsum_) (void)hipFree(sp_tsum_);
@@ -1005,6 +1014,7 @@ class EngineT final : public EngineBase {
       df.gidx0 = level_gidx;
       df.prev_gidx0 = prev_gidx;
     }
+    if (pc_valid_ && pc_pass_) df.prev_counts = pc_prev_;
     return df;
   }
   // Materialise a deferred frontier of n states into cur_ (k_materialize):
@@ -1058,6 +1068,12 @@ class EngineT final : public EngineBase {
   unsigned long long* link_cur_ = nullptr;
   unsigned long long* link_next_ = nullptr;
   uint64_t link_cur_cap_ = 0, link_next_cap_ = 0;
+  // plans (Plan::counts) of the frontier being expanded / of the previous one
+  unsigned long long* pc_cur_ = nullptr;
+  unsigned long long* pc_prev_ = nullptr;
+  uint64_t pc_cur_cap_ = 0, pc_prev_cap_ = 0;
+  bool pc_valid_ = false;
+  bool pc_pass_ = true;              // KC_DEFER_PC=0: rebuilds plan their grandparent (A/B)
   static constexpr int kDeferRetry = -100000;
   bool defer_ = false, defer_now_ = false;
   double defer_slack_ = 1.25;

@@ -267,6 +267,12 @@ struct DeferArgs {
   uint64_t gidx0 = 0;                         // global index of this frontier's state 0 (trace path)
   uint64_t prev_gidx0 = 0;                    // global index of the previous frontier's state 0
   void* out = nullptr;                        // where the rebuilt states go (State*; the frontier buffer)
+  // successor plans (Plan::counts) of the previous frontier's states, as its
+  // k_claim computed them (nullptr: plan the grandparent here)
+  const unsigned long long* prev_counts = nullptr;
+  // where k_claim writes its own parents' plans for the next level (any k_claim
+  // of the engine's wide path; nullptr: not kept)
+  unsigned long long* counts_out = nullptr;
 };
 
 // Rebuild frontier state i (index within the level) from its link; stores it
@@ -285,7 +291,7 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
     t = (int)df.ord[df.gidx0 + i];
   }
   const typename M::State gp = load_state<M>(reinterpret_cast<const typename M::State*>(df.prev), pp);
-  const typename M::Plan pl{M::plan(gp, f).counts, 0, -1, -1};
+  const typename M::Plan pl{df.prev_counts ? df.prev_counts[pp] : M::plan(gp, f).counts, 0, -1, -1};
   int slot, j;
   M::locate(pl, t, slot, j);
   typename M::State s;
@@ -390,6 +396,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const typename M::State s =
         (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
+    if (!SH && df.counts_out) df.counts_out[base + i] = pl.counts;
     // (an LDS total, not a register live through the kernel: k_claim sits at
     // its 80-VGPR budget for 6 waves per SIMD)
     if (!SH && df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
