@@ -149,6 +149,11 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 // key of the same tile, which can never be the level minimum; an LDS table
 // overflow just sends the copy to the ClaimSet directly.
 constexpr int CLAIM_TILE = 256;
+// tile representatives whose first probe loads a lane issues together (A/B:
+// build with -DKC_CLAIM_BATCH=1 for one at a time)
+#ifndef KC_CLAIM_BATCH
+#define KC_CLAIM_BATCH 2
+#endif
 constexpr int CLAIM_LDS_BITS = 11;
 constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
 // Candidate records (claimants whose claim may win): fp + tile-local key
@@ -485,30 +490,52 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     __syncthreads();
   }
-  // every tile representative claims its fp in the ClaimSet
+  // every tile representative claims its fp in the ClaimSet.  A lane takes
+  // representatives k = tid, tid + 256, ... in groups of KC_CLAIM_BATCH:
+  // the first probe loads of a group are issued back to back, then each
+  // claim runs from its loaded pair (a stale pair only shows a slot empty
+  // or a claim larger; the CAS and the settle passes decide).
   const int nrep = (int)sh_nrep;
-  for (int k = threadIdx.x; k < nrep; k += CLAIM_TILE) {
-    const unsigned long long fp = sh_fp[k];
-    const unsigned int lk = sh_key[k];
-    const unsigned int lp = lk >> 5, t = lk & 31;
-    const uint64_t pidx = base + tile0 + lp;
-    if (SH) {
-      const uint32_t o = owner_of(fp, sh.world);
-      if (o != sh.rank) {
-        atomicOr(&sh_rep[lp], 1u << t);
-        atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + lp], 1u << (8 * (o & 3)));
-        continue;
+  for (int k0 = threadIdx.x; k0 < nrep; k0 += CLAIM_TILE * KC_CLAIM_BATCH) {
+    unsigned long long fpq[KC_CLAIM_BATCH];
+    ulonglong2 eq[KC_CLAIM_BATCH];
+    uint64_t iq[KC_CLAIM_BATCH];
+#pragma unroll
+    for (int q = 0; q < KC_CLAIM_BATCH; ++q) {
+      const int k = k0 + q * CLAIM_TILE;
+      fpq[q] = k < nrep ? sh_fp[k] : 0ull;
+      if (fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank)) {
+        iq[q] = bucket_of(fpq[q], nbuckets);
+        eq[q] = claimset_first(cs, iq[q]);
       }
     }
-    ++probes;
-    const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level);
-    KC_DIAG_OUT(r);
-    if (r == CL_NEW)
-      atomicOr(&sh_cur[lp], 1u << t);
-    else if (r == CL_CUR)
-      push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk, sh.ovf, C);
-    else if (r == CL_FULL)
-      atomicAdd(&C->overflow, 1ull);
+#pragma unroll
+    for (int q = 0; q < KC_CLAIM_BATCH; ++q) {
+      const int k = k0 + q * CLAIM_TILE;
+      if (k >= nrep) break;
+      const unsigned long long fp = fpq[q];
+      const unsigned int lk = sh_key[k];
+      const unsigned int lp = lk >> 5, t = lk & 31;
+      const uint64_t pidx = base + tile0 + lp;
+      if (SH) {
+        const uint32_t o = owner_of(fp, sh.world);
+        if (o != sh.rank) {
+          atomicOr(&sh_rep[lp], 1u << t);
+          atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + lp], 1u << (8 * (o & 3)));
+          continue;
+        }
+      }
+      ++probes;
+      const int r = claimset_claim_store_from(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level,
+                                              iq[q], eq[q]);
+      KC_DIAG_OUT(r);
+      if (r == CL_NEW)
+        atomicOr(&sh_cur[lp], 1u << t);
+      else if (r == CL_CUR)
+        push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk, sh.ovf, C);
+      else if (r == CL_FULL)
+        atomicAdd(&C->overflow, 1ull);
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
