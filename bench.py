@@ -296,7 +296,7 @@ def bench_single(args, kw, desc):
     if not args.no_timing:
         S = state_bytes(kw)
         tt = {k: tuple(v) for k, v in times.items()}
-        if narrow[1] and narrow[2] // args.steps == r.depth - 1:     # every level ran narrow
+        if narrow[1] and narrow[2] // args.steps >= r.depth - 1:     # every level ran narrow
             tt["narrow"] = (narrow[0], narrow[1])
         name, roof = roofline_bfs(tt, acc, S)
         # k_claim streams its parents (S B each); everything else it reads is a random probe

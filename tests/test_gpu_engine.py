@@ -299,3 +299,18 @@ def test_deferred_trace_in_host_memory(fixtures):
     r = run(np=2, max_levels=40, trace_host=True)
     assert r.deferred_states > 0 and not r.defer_fallback
     assert r.level_width == fx["level_width"] and r.act_dist == fx["act_dist"]
+
+
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_wide_level_state_set_identical(oracle, monkeypatch, defer):
+    # a captured WIDE level of the NP=2 model (level 30: 35,224 states, past
+    # the narrow path): on the deferred frontier it is materialised for the
+    # capture; same states in the same FIFO order as the oracle
+    monkeypatch.setenv("KC_DEFER", defer)
+    with ModelChecker(ModelConfig(np=2, max_levels=32)) as mc:
+        mc.capture_level(30)
+        mc.run()
+        got = mc.level_tuples(30)
+    want = oracle.level_tuples(oracle.config(np_=2), 30)
+    assert got.shape == want.shape == (35224, got.shape[1])
+    assert np.array_equal(got, want)
