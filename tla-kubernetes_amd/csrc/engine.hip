@@ -590,6 +590,12 @@ class EngineT final : public EngineBase {
       fprintf(stderr, "kubecheck old-state level distance (KC_DIAG): 1:%llu 2:%llu 3:%llu 4:%llu 5-8:%llu 9-16:%llu 17+:%llu\n",
               h_ctr_->old_dist(0), h_ctr_->old_dist(1), h_ctr_->old_dist(2), h_ctr_->old_dist(3), h_ctr_->old_dist(4),
               h_ctr_->old_dist(5), h_ctr_->old_dist(6));
+      fprintf(stderr, "kubecheck k_claim successor loop (KC_DIAG): wave trips %llu x 64 lanes, lane trips %llu (%.3f busy);"
+              " dealt by successor count: wave trips %llu (%.3f busy)\n",
+              h_ctr_->loop_max(), h_ctr_->loop_sum(),
+              h_ctr_->loop_max() ? (double)h_ctr_->loop_sum() / (64.0 * h_ctr_->loop_max()) : 0.0,
+              h_ctr_->loop_sorted(),
+              h_ctr_->loop_sorted() ? (double)h_ctr_->loop_sum() / (64.0 * h_ctr_->loop_sorted()) : 0.0);
     }
     return 0;
   }

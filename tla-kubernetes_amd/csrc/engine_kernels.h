@@ -42,7 +42,12 @@ struct CtrStripe {                  // 1 KiB
   unsigned long long claim_out[4];
   unsigned long long old_dist[8];
   unsigned long long cand_ovf;      // candidate records that went to the overflow list
-  unsigned long long pad[128 - 2 * A_COUNT - 16 - OUTDEG_BINS];
+  // KC_DIAG builds only: k_claim successor-loop trips, per wave the max over
+  // its lanes (what the wave runs) and the sum (what its lanes need)
+  // (and loop_sorted: the wave trips if each tile's parents were dealt to
+  // its waves in order of successor count)
+  unsigned long long loop_max, loop_sum, loop_sorted;
+  unsigned long long pad[128 - 2 * A_COUNT - 19 - OUTDEG_BINS];
 };
 struct Counters {
   unsigned long long err_key;     // min error key of the level (~0 = none)
@@ -72,6 +77,9 @@ struct Counters {
     for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].claim_out[r];
     return t;
   }
+  unsigned long long loop_max() const { return sum1(&CtrStripe::loop_max); }
+  unsigned long long loop_sum() const { return sum1(&CtrStripe::loop_sum); }
+  unsigned long long loop_sorted() const { return sum1(&CtrStripe::loop_sorted); }
   unsigned long long old_dist(int b) const {
     unsigned long long t = 0;
     for (int k = 0; k < CTR_STRIPES; ++k) t += s[k].old_dist[b];
@@ -335,7 +343,9 @@ __global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, F
 // Occupancy: the LDS table (24 KB) allows 6 workgroups = 6 waves per SIMD;
 // the claims are latency-bound random probes, so the register budget is
 // pinned to match (one wave less measured +15 ms per NP=2 check).
-template <class M, int ABL = 0, bool SH = false>
+// OWN: the fingerprints' owner projection (kubeapi_spec.h; 1 on the sharded
+// path, also at world 1 where it runs the SH = false variant)
+template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0>
 __global__ void __launch_bounds__(CLAIM_TILE) __attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
@@ -349,6 +359,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   __shared__ unsigned int sh_act[A_COUNT];
   __shared__ unsigned int sh_actd[A_COUNT];       // deferred frontier: actions that made the parents
   __shared__ unsigned long long sh_dcand;         // deferred frontier: the parents' successor count
+  __shared__ uint32_t sh_proj[OWN ? CLAIM_TILE : 1];  // OWN = 1: each parent's owner projection (kubeapi_spec.h)
   __shared__ unsigned int sh_rc;
   __shared__ unsigned int sh_nrep;                // tile representatives
   // SH only (dynamic LDS): remote representatives per parent, then their
@@ -397,6 +408,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   const uint64_t i = tile0 + threadIdx.x;
   const bool live = i < n;
   unsigned probes = 0;
+#ifdef KC_DIAG
+  int diag_tot = 0;
+#endif
   if (live) {
     const typename M::State s =
         (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
@@ -406,6 +420,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     // its 80-VGPR budget for 6 waves per SIMD)
     if (!SH && df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
     const uint64_t fold = M::fp_fold(s);
+    if (OWN) sh_proj[threadIdx.x] = M::owner_proj(s);
     const uint64_t pidx = base + i;
     if (ABL == 0) {
       if (pl.fail_pos >= 0)
@@ -425,6 +440,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     uint64_t acc = fold ^ pl.counts;
     if (ABL == 3) tot = 0;
+#ifdef KC_DIAG
+    diag_tot = tot;
+#endif
     // (walking (slot, j) along with t instead of locate() measured slower:
     // its three live registers spill at k_claim's 80-VGPR budget; r03w)
     for (int t = 0; t < tot; ++t) {
@@ -433,7 +451,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       typename M::State x;
       int who;
       M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
+      const uint64_t fp = OWN ? M::template fingerprint_succ<1>(s, fold, x, who, sh_proj[threadIdx.x])
+                              : M::template fingerprint_succ<0>(s, fold, x, who);
       if (ABL == 2) {
         acc ^= fp;
         continue;
@@ -461,6 +480,34 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     if (ABL >= 2) sh_cur[threadIdx.x] = (unsigned)acc;
   }
+#ifdef KC_DIAG
+  {
+    int mx = diag_tot, sm = diag_tot;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      mx = max(mx, __shfl_xor(mx, off, 64));
+      sm += __shfl_xor(sm, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&stripe(C).loop_max, (unsigned long long)mx);
+      atomicAdd(&stripe(C).loop_sum, (unsigned long long)sm);
+    }
+    __shared__ unsigned int sh_hist[M::MAXSUCC + 1];
+    if (threadIdx.x <= M::MAXSUCC) sh_hist[threadIdx.x] = 0;
+    __syncthreads();
+    if (live) atomicAdd(&sh_hist[diag_tot], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long srt = 0;
+      unsigned int seen = 0, next = 0;
+      for (int v = M::MAXSUCC; v >= 0; --v) {
+        seen += sh_hist[v];
+        while (next < seen) { srt += v; next += 64; }
+      }
+      atomicAdd(&stripe(C).loop_sorted, srt);
+    }
+  }
+#endif
   __syncthreads();
   if (ABL != 0) {
     if (live) scratch[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];

@@ -699,15 +699,26 @@ struct Model {
   }
   // Owner bits.  Fingerprint-owner sharding (shard.hip) gives a state to
   // rank floor(fp * R / 2^63), i.e. to the fingerprint's top bits.  Those
-  // OWNER_BITS bits are a hash of a projection of the state — apiState and
-  // the first PVC controller's word — not of the whole state: 97% of all
-  // actions leave apiState alone and an action changes one process's word,
-  // so about 2/3 of successors keep their parent's owner (measured on the
-  // NP=2 model, levels 1-38) and siblings stay together for the LDS tile
-  // dedup, while the classes still spread evenly over 8 ranks (max/mean
-  // 1.10).  For R dividing 2^OWNER_BITS the owner depends on these bits
-  // only.  The other 59 bits are the Zobrist fold, so two states collide
-  // only if their projections hash alike and 59 fold bits agree.
+  // OWNER_BITS bits are a hash of a projection of the state, not of the
+  // whole state, so that most successors keep their parent's owner (no
+  // record to send) and siblings stay together for the LDS tile dedup.  For
+  // R dividing 2^OWNER_BITS the owner depends on these bits only.  The other
+  // 59 bits are the Zobrist fold, so two states collide only if their
+  // projections hash alike and 59 fold bits agree.  Two projections (the
+  // template parameter OWN of the fingerprint functions):
+  //  * OWN = 0 (the single-GPU engine, and every fingerprint the C-ABI
+  //    reports): apiState and the first PVC controller's word;
+  //  * OWN = 1 (the sharded path, shard.hip): apiState and the listRequests
+  //    objs words.  An action always rewrites its process's scalar word,
+  //    but only APIStart changes apiState and only list replies change objs,
+  //    so fewer successors change owner: records sent per NP=2 check at
+  //    R = 2 / 4 / 8 538M / 853M / 983M -> 338M / 510M / 603M
+  //    (tools/shard_records.py, profiles/r03ad_*), per-level balance on the
+  //    wide levels 1.02-1.11 at R = 8 (tools/owner_balance.py,
+  //    profiles/r03ab_owner.log).  The engine keeps OWN = 0: there the
+  //    owner bits buy nothing, and the objs words' extra live range spills
+  //    k_claim past its 80-VGPR budget (+6 ms per NP=2 check measured).
+  // A run uses one projection throughout; both give the same counts.
   static constexpr int OWNER_BITS = 4;
   static constexpr int OWNER_WORD = 1 + (NP > 0 ? NC : 0);   // first PVC controller (else client)
   KC_HD static uint64_t owner_hash(uint64_t w0, uint64_t wo) {
@@ -716,19 +727,46 @@ struct Model {
     z *= 0xbf58476d1ce4e5b9ull;
     return z >> (64 - OWNER_BITS);
   }
-  KC_HD static uint64_t fp_final(uint64_t h, const State& x) {
-    h = (h & ((1ull << (63 - OWNER_BITS)) - 1)) |
-        (owner_hash(x.w[0], x.w[OWNER_WORD]) << (63 - OWNER_BITS));
+  // OWN = 1: the objs words folded to 32 bits, XOR-linear in each word (a
+  // successor rewrites at most one, so its projection is its parent's XOR
+  // that word's change); owner_hash does the mixing
+  KC_HD static uint32_t owner_word(uint64_t w, int k) {
+    const uint32_t v = (uint32_t)(w ^ (w >> 32));
+    const int r = (8 * k) & 31;
+    return r ? (v << r) | (v >> (32 - r)) : v;
+  }
+  KC_HD static uint32_t owner_proj(const State& x) {
+    uint32_t wo = 0;
+#pragma unroll
+    for (int k = 0; k < OBJ_WORDS; ++k) wo ^= owner_word(x.w[1 + A + k], k);
+    return wo;
+  }
+  template <int OWN = 0>
+  KC_HD static uint64_t owner_bits(const State& x) {
+    if constexpr (OWN != 0)
+      return owner_hash(x.w[0], owner_proj(x));
+    else
+      return owner_hash(x.w[0], x.w[OWNER_WORD]);
+  }
+  KC_HD static uint64_t fp_final_ob(uint64_t h, uint64_t ob) {
+    h = (h & ((1ull << (63 - OWNER_BITS)) - 1)) | (ob << (63 - OWNER_BITS));
     return h ? h : 1;
   }
-  KC_HD static uint64_t fingerprint(const State& s) { return fp_final(fp_fold(s), s); }
+  template <int OWN = 0>
+  KC_HD static uint64_t fp_final(uint64_t h, const State& x) { return fp_final_ob(h, owner_bits<OWN>(x)); }
+  template <int OWN = 0>
+  KC_HD static uint64_t fingerprint(const State& s) { return fp_final<OWN>(fp_fold(s), s); }
 
   // Fingerprint of successor x of s, given s's fold and the process `who`
   // whose word the action rewrote (apply's out-parameter).  Equal to
-  // fingerprint(x).  (Caching the parent's per-word mixes instead of
+  // fingerprint<OWN>(x).  (Caching the parent's per-word mixes instead of
   // re-mixing the old words costs 15 VGPRs, one wave per SIMD of k_claim's
-  // occupancy, and measured slower.)
-  KC_HD static uint64_t fingerprint_succ(const State& s, uint64_t fold_s, const State& x, int who) {
+  // occupancy, and measured slower.)  OWN = 1 takes the parent's owner
+  // projection proj_s (the sharded k_claim keeps it in LDS).
+  template <int OWN = 0>
+  KC_HD static uint64_t fingerprint_succ(const State& s, uint64_t fold_s, const State& x, int who,
+                                         uint32_t proj_s = 0) {
+    uint32_t wo = proj_s;
     uint64_t h = fold_s;
     if (x.w[0] != s.w[0]) h ^= mix_salted(s.w[0] ^ salt_c(0)) ^ mix_salted(x.w[0] ^ salt_c(0));
     {
@@ -760,9 +798,13 @@ struct Model {
       if (o != nw) {
         const uint64_t sl = salt(wi);
         h ^= mix_salted(o ^ sl) ^ mix_salted(nw ^ sl);
+        if constexpr (OWN != 0) wo ^= owner_word(o ^ nw, wi - (1 + A));
       }
     }
-    return fp_final(h, x);
+    if constexpr (OWN != 0)
+      return fp_final_ob(h, owner_hash(x.w[0], wo));
+    else
+      return fp_final<0>(h, x);
   }
 
   // ------------------------------------------------ canonical tuple (ABI)

@@ -38,20 +38,15 @@
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
+#include "record.h"
 #include "shard.h"
 
 namespace kc {
 
 constexpr uint64_t KEY_INIT = 0xFull << 60;   // parent key of an Init state (| init index)
 
-// A record: the successor's W_RAW canonical words, then its key, padded to a
-// multiple of 16 B (48 B for NP = 2).  The receiver recomputes the
-// fingerprint instead of receiving it.
-template <class M>
-struct Record {
-  static constexpr int RW = (M::W_RAW + 2) & ~1;
-  uint64_t w[RW];
-};
+// A record (record.h): the successor's key, then its bit-packed canonical
+// state; 48 B for NP = 2.
 template <class M>
 __device__ __forceinline__ void load_record(const Record<M>* __restrict__ in, uint64_t i,
                                             typename M::State& x, uint64_t& key) {
@@ -63,13 +58,11 @@ __device__ __forceinline__ void load_record(const Record<M>* __restrict__ in, ui
     r[2 * k] = q.x;
     r[2 * k + 1] = q.y;
   }
-#pragma unroll
-  for (int k = 0; k < M::W; ++k) x.w[k] = k < M::W_RAW ? r[k] : 0ull;
-  key = r[M::W_RAW];
+  record_unpack<M>(r, x, key);
 }
 template <class M>
 __device__ __forceinline__ uint64_t record_key(const Record<M>* __restrict__ in, uint64_t i) {
-  return in[i].w[M::W_RAW];
+  return in[i].w[0];
 }
 
 // claim order key of a record key: (rank, parent index, successor position)
@@ -98,7 +91,7 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
     typename M::State x;
     int who;
     M::apply(s, slot, j, f, x, who);
-    const uint64_t fp = M::fingerprint_succ(s, fold, x, who);
+    const uint64_t fp = M::template fingerprint_succ<1>(s, fold, x, who, M::owner_proj(s));
     const uint32_t o = owner_of(fp, world);
     uint32_t r = 0;
 #pragma unroll
@@ -106,9 +99,7 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
       if (k == o) { r = c[k]; c[k] = r + 1; }
     const uint64_t pos = (uint64_t)off[(uint64_t)o * n + i] + r;   // owner-major scan
     uint64_t w[Record<M>::RW];
-#pragma unroll
-    for (int k = 0; k < Record<M>::RW; ++k) w[k] = k < M::W_RAW ? x.w[k] : 0ull;
-    w[M::W_RAW] = (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot);
+    record_pack<M>(x, (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot), w);
     ulonglong2* v = reinterpret_cast<ulonglong2*>(out + pos);
 #pragma unroll
     for (int k = 0; k < Record<M>::RW / 2; ++k) v[k] = make_ulonglong2(w[2 * k], w[2 * k + 1]);
@@ -203,7 +194,7 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
     typename M::State x;
     uint64_t key;
     load_record<M>(in, i, x, key);
-    const uint64_t fp = M::fingerprint(x);
+    const uint64_t fp = M::template fingerprint<1>(x);
     rfp[i] = fp;
     const int r = claimset_claim_store(cs, nslots, fp, make_claim(level, record_ckey(key)), level);
     if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
@@ -510,7 +501,7 @@ class ShardT final : public ShardBase {
     for (int k = 0; k < M::num_init(); ++k) {
       State s;
       M::init_state(k, s, cfg_.variant);
-      const uint64_t fp = M::fingerprint(s);
+      const uint64_t fp = M::template fingerprint<1>(s);
       const uint32_t o = (uint32_t)(((unsigned __int128)(fp << 1) * (uint64_t)world_) >> 64);
       if ((int)o != rank_) continue;
       mine.push_back(s);
@@ -601,7 +592,7 @@ class ShardT final : public ShardBase {
     if (world_ == 1) {
       // one rank owns everything: the single-GPU engine's claim kernel (no
       // owner counting; claim keys then carry rank 0, which they do anyway)
-      hipLaunchKernelGGL((k_claim<M, 0, false>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+      hipLaunchKernelGGL((k_claim<M, 0, false, 1>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                          d_ctr_, sh);

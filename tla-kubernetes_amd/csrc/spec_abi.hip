@@ -14,6 +14,7 @@
 #include "engine_util.h"
 #include "kc_common.h"
 #include "kubeapi_spec.h"
+#include "record.h"
 
 namespace kc {
 
@@ -256,6 +257,17 @@ int kc_spec_fp_selfcheck(const kc_model_config* cfg, const uint64_t* tuple) {
       typename M::State x;
       M::apply(s, slot, j, f, x, who);
       if (M::fingerprint_succ(s, fold, x, who) != M::fingerprint(x)) ++bad;
+      // the sharded path's owner projection (incremental from the parent's)
+      if (M::template fingerprint_succ<1>(s, fold, x, who, M::owner_proj(s)) != M::template fingerprint<1>(x)) ++bad;
+      // the sharded path's exchange record round-trips the successor exactly
+      uint64_t r[Record<M>::RW];
+      const uint64_t key = 0x9e3779b97f4a7c15ull * (uint64_t)(t + 1);
+      record_pack<M>(x, key, r);
+      typename M::State y;
+      uint64_t k2;
+      record_unpack<M>(r, y, k2);
+      for (int i = 0; i < M::W; ++i) bad += y.w[i] != x.w[i];
+      bad += k2 != key;
     }
     return bad;
   });
