@@ -159,6 +159,11 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
 constexpr int CLAIM_TILE = 256;
 // tile representatives whose first probe loads a lane issues together (A/B:
 // build with -DKC_CLAIM_BATCH=1 for one at a time)
+// k_claim deals each tile's parents to its waves by successor count (build
+// with -DKC_DEAL=0 for lane = parent)
+#ifndef KC_DEAL
+#define KC_DEAL 1
+#endif
 #ifndef KC_CLAIM_BATCH
 #define KC_CLAIM_BATCH 2
 #endif
@@ -372,9 +377,19 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     sh_nrep = 0;
     sh_dcand = 0;
   }
-  for (int k = threadIdx.x; k < NT; k += CLAIM_TILE) {
-    sh_fp[k] = 0ull;
-    sh_key[k] = ~0u;
+  // DEAL: each tile's parents are dealt to its waves in order of successor
+  // count (below), staged through the LDS table, which is cleared after that
+  constexpr bool DEAL = KC_DEAL && (M::W + 2) * CLAIM_TILE <= NT;
+  unsigned int* const deal_cnt = sh_key + CLAIM_TILE;   // parents per successor count
+  unsigned int* const deal_start = deal_cnt + 64;
+  static_assert(!DEAL || CLAIM_TILE + 64 + M::MAXSUCC + 1 <= NT, "deal counters");
+  if (DEAL) {
+    if (threadIdx.x <= M::MAXSUCC) deal_cnt[threadIdx.x] = 0;
+  } else {
+    for (int k = threadIdx.x; k < NT; k += CLAIM_TILE) {
+      sh_fp[k] = 0ull;
+      sh_key[k] = ~0u;
+    }
   }
   if (SH) {
     sh_rep[threadIdx.x] = 0;
@@ -408,21 +423,20 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   const uint64_t i = tile0 + threadIdx.x;
   const bool live = i < n;
   unsigned probes = 0;
-#ifdef KC_DIAG
-  int diag_tot = 0;
-#endif
+  typename M::State s;
+  uint64_t fold = 0, counts = 0;
+  int tot = 0;
   if (live) {
-    const typename M::State s =
-        (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
+    s = (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
     if (!SH && df.counts_out) df.counts_out[base + i] = pl.counts;
     // (an LDS total, not a register live through the kernel: k_claim sits at
     // its 80-VGPR budget for 6 waves per SIMD)
     if (!SH && df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
-    const uint64_t fold = M::fp_fold(s);
+    fold = M::fp_fold(s);
     if (OWN) sh_proj[threadIdx.x] = M::owner_proj(s);
-    const uint64_t pidx = base + i;
     if (ABL == 0) {
+      const uint64_t pidx = base + i;
       if (pl.fail_pos >= 0)
         atomicMin(&C->err_key, (pidx << 16) | ((uint64_t)pl.fail_pos << 8) | E_ASSERT);
       else if (pl.total == 0 && check_deadlock)
@@ -433,55 +447,17 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
       }
     }
-    int tot = pl.total;
+    tot = pl.total;
     if (tot > M::MAXSUCC) {
       if (ABL == 0) atomicAdd(&C->overflow, 1ull);
       tot = M::MAXSUCC;
     }
-    uint64_t acc = fold ^ pl.counts;
+    counts = pl.counts;
     if (ABL == 3) tot = 0;
-#ifdef KC_DIAG
-    diag_tot = tot;
-#endif
-    // (walking (slot, j) along with t instead of locate() measured slower:
-    // its three live registers spill at k_claim's 80-VGPR budget; r03w)
-    for (int t = 0; t < tot; ++t) {
-      int slot, j;
-      M::locate(pl, t, slot, j);
-      typename M::State x;
-      int who;
-      M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = OWN ? M::template fingerprint_succ<1>(s, fold, x, who, sh_proj[threadIdx.x])
-                              : M::template fingerprint_succ<0>(s, fold, x, who);
-      if (ABL == 2) {
-        acc ^= fp;
-        continue;
-      }
-      if (lds_claim<NT>(sh_fp, sh_key, fp, (threadIdx.x << 5) | (unsigned)t) < 0 && ABL == 0) {
-        // LDS table full: claim (or send) this copy directly
-        if (SH) {
-          const uint32_t o = owner_of(fp, sh.world);
-          if (o != sh.rank) {
-            atomicOr(&sh_rep[threadIdx.x], 1u << t);
-            atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + threadIdx.x], 1u << (8 * (o & 3)));
-            continue;
-          }
-        }
-        ++probes;
-        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | (uint64_t)t), level);
-        KC_DIAG_OUT(r);
-        if (r == CL_NEW)
-          atomicOr(&sh_cur[threadIdx.x], 1u << t);
-        else if (r == CL_CUR)
-          push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (threadIdx.x << 5) | (unsigned)t, sh.ovf, C);
-        else if (r == CL_FULL)
-          atomicAdd(&C->overflow, 1ull);
-      }
-    }
-    if (ABL >= 2) sh_cur[threadIdx.x] = (unsigned)acc;
   }
 #ifdef KC_DIAG
   {
+    const int diag_tot = live ? tot : 0;
     int mx = diag_tot, sm = diag_tot;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -508,6 +484,91 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
   }
 #endif
+  // Deal: a wave runs its successor loop as many times as its busiest lane
+  // needs.  Counting-sort the tile's parents by successor count (descending)
+  // and give lane k the k-th, so each wave's lanes need about the same number
+  // of trips.  The parent's state, fold and plan move through the (not yet
+  // used) LDS table; every key and mask below uses the parent's own index lp.
+  // (the parent's index travels in bits 56-63 of its plan, which locate()
+  // never reads: one register more across the loop spills k_claim)
+  static_assert(!DEAL || (M::NSLOT * 6 <= 56 && CLAIM_TILE <= 256), "deal: lp in the plan word");
+  if (DEAL) {
+    const unsigned int pos = live ? atomicAdd(&deal_cnt[tot], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int at = 0;
+      for (int v = M::MAXSUCC; v >= 0; --v) {
+        deal_start[v] = at;
+        at += deal_cnt[v];
+      }
+    }
+    __syncthreads();
+    if (live) {
+      const unsigned int d = deal_start[tot] + pos;
+#pragma unroll
+      for (int k = 0; k < M::W; ++k) sh_fp[k * CLAIM_TILE + d] = s.w[k];
+      sh_fp[M::W * CLAIM_TILE + d] = fold;
+      sh_fp[(M::W + 1) * CLAIM_TILE + d] = counts | ((uint64_t)threadIdx.x << 56);
+      sh_key[d] = (unsigned)tot;
+    }
+    __syncthreads();
+    if (live) {   // (the live lanes are a prefix of the tile: slot threadIdx.x was written)
+#pragma unroll
+      for (int k = 0; k < M::W; ++k) s.w[k] = sh_fp[k * CLAIM_TILE + threadIdx.x];
+      fold = sh_fp[M::W * CLAIM_TILE + threadIdx.x];
+      counts = sh_fp[(M::W + 1) * CLAIM_TILE + threadIdx.x];
+      tot = (int)sh_key[threadIdx.x];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < NT; k += CLAIM_TILE) {
+      sh_fp[k] = 0ull;
+      sh_key[k] = ~0u;
+    }
+    __syncthreads();
+  }
+  if (live) {
+#define KC_LP (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x)
+    const typename M::Plan pl{counts, tot, -1, -1};
+    uint64_t acc = fold ^ counts;
+    // (walking (slot, j) along with t instead of locate() measured slower:
+    // its three live registers spill at k_claim's 80-VGPR budget; r03w)
+    for (int t = 0; t < tot; ++t) {
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      int who;
+      M::apply(s, slot, j, f, x, who);
+      const uint64_t fp = OWN ? M::template fingerprint_succ<1>(s, fold, x, who, sh_proj[KC_LP])
+                              : M::template fingerprint_succ<0>(s, fold, x, who);
+      if (ABL == 2) {
+        acc ^= fp;
+        continue;
+      }
+      if (lds_claim<NT>(sh_fp, sh_key, fp, (KC_LP << 5) | (unsigned)t) < 0 && ABL == 0) {
+        // LDS table full: claim (or send) this copy directly
+        if (SH) {
+          const uint32_t o = owner_of(fp, sh.world);
+          if (o != sh.rank) {
+            atomicOr(&sh_rep[KC_LP], 1u << t);
+            atomicAdd(&sh_cnt[(o >> 2) * CLAIM_TILE + KC_LP], 1u << (8 * (o & 3)));
+            continue;
+          }
+        }
+        ++probes;
+        const uint64_t pidx = base + tile0 + KC_LP;
+        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | (uint64_t)t), level);
+        KC_DIAG_OUT(r);
+        if (r == CL_NEW)
+          atomicOr(&sh_cur[KC_LP], 1u << t);
+        else if (r == CL_CUR)
+          push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (KC_LP << 5) | (unsigned)t, sh.ovf, C);
+        else if (r == CL_FULL)
+          atomicAdd(&C->overflow, 1ull);
+      }
+    }
+    if (ABL >= 2) sh_cur[KC_LP] = (unsigned)acc;
+#undef KC_LP
+  }
   __syncthreads();
   if (ABL != 0) {
     if (live) scratch[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
