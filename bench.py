@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -151,7 +152,11 @@ def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     the profile's."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_rocprof_summary.json")))
+    def run_order(f):      # r03z < r03aa < r03an: round, then tag length, then tag
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(f))
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_rocprof_summary.json")), key=run_order)
     for f in reversed(files):
         try:
             with open(f) as fh:

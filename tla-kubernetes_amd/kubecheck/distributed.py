@@ -24,6 +24,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import re
 import time
 from typing import List, Optional, Sequence
 
@@ -554,7 +555,12 @@ def pmc_ratio(workload: str):
     counters (profiles/r02b_pmc_calibration.json) and restored here."""
     import glob
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    for f in reversed(sorted(glob.glob(os.path.join(root, "profiles", f"*_{workload}_sharded_rocprof_summary.json")))):
+    def run_order(f):      # r03z < r03aa < r03an: round, then tag length, then tag
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(f))
+
+    for f in reversed(sorted(glob.glob(os.path.join(root, "profiles", f"*_{workload}_sharded_rocprof_summary.json")),
+                             key=run_order)):
         try:
             d = json.load(open(f))
             k, alg = d["kernels"]["k_claim"], d["algorithmic"]
