@@ -379,7 +379,11 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   // DEAL: each tile's parents are dealt to its waves in order of successor
   // count (below), staged through the LDS table, which is cleared after that
-  constexpr bool DEAL = KC_DEAL && (M::W + 2) * CLAIM_TILE <= NT;
+  // (state words in sh_fp; fold and plan there too when they fit, else as
+  // 32-bit halves in sh_key past the counters: the sharded table is smaller)
+  constexpr bool DEAL_FP = (M::W + 2) * CLAIM_TILE <= NT;
+  constexpr int DEAL_KEY0 = CLAIM_TILE + 128;             // sh_key: fold lo/hi, plan lo/hi
+  constexpr bool DEAL = KC_DEAL && (DEAL_FP || (M::W * CLAIM_TILE <= NT && DEAL_KEY0 + 4 * CLAIM_TILE <= NT));
   unsigned int* const deal_cnt = sh_key + CLAIM_TILE;   // parents per successor count
   unsigned int* const deal_start = deal_cnt + 64;
   static_assert(!DEAL || CLAIM_TILE + 64 + M::MAXSUCC + 1 <= NT, "deal counters");
@@ -507,16 +511,30 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       const unsigned int d = deal_start[tot] + pos;
 #pragma unroll
       for (int k = 0; k < M::W; ++k) sh_fp[k * CLAIM_TILE + d] = s.w[k];
-      sh_fp[M::W * CLAIM_TILE + d] = fold;
-      sh_fp[(M::W + 1) * CLAIM_TILE + d] = counts | ((uint64_t)threadIdx.x << 56);
+      const uint64_t cl = counts | ((uint64_t)threadIdx.x << 56);
+      if (DEAL_FP) {
+        sh_fp[M::W * CLAIM_TILE + d] = fold;
+        sh_fp[(M::W + 1) * CLAIM_TILE + d] = cl;
+      } else {
+        sh_key[DEAL_KEY0 + d] = (unsigned)fold;
+        sh_key[DEAL_KEY0 + CLAIM_TILE + d] = (unsigned)(fold >> 32);
+        sh_key[DEAL_KEY0 + 2 * CLAIM_TILE + d] = (unsigned)cl;
+        sh_key[DEAL_KEY0 + 3 * CLAIM_TILE + d] = (unsigned)(cl >> 32);
+      }
       sh_key[d] = (unsigned)tot;
     }
     __syncthreads();
     if (live) {   // (the live lanes are a prefix of the tile: slot threadIdx.x was written)
 #pragma unroll
       for (int k = 0; k < M::W; ++k) s.w[k] = sh_fp[k * CLAIM_TILE + threadIdx.x];
-      fold = sh_fp[M::W * CLAIM_TILE + threadIdx.x];
-      counts = sh_fp[(M::W + 1) * CLAIM_TILE + threadIdx.x];
+      if (DEAL_FP) {
+        fold = sh_fp[M::W * CLAIM_TILE + threadIdx.x];
+        counts = sh_fp[(M::W + 1) * CLAIM_TILE + threadIdx.x];
+      } else {
+        fold = sh_key[DEAL_KEY0 + threadIdx.x] | ((uint64_t)sh_key[DEAL_KEY0 + CLAIM_TILE + threadIdx.x] << 32);
+        counts = sh_key[DEAL_KEY0 + 2 * CLAIM_TILE + threadIdx.x] |
+                 ((uint64_t)sh_key[DEAL_KEY0 + 3 * CLAIM_TILE + threadIdx.x] << 32);
+      }
       tot = (int)sh_key[threadIdx.x];
     }
     __syncthreads();
