@@ -277,6 +277,20 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t fp, uint32_t world) {
 // set by its random memory operations, instead of in a k_emit of its own.
 // Any invariant violation sets DF_INVARIANT: the host then re-runs the check
 // on the exact (materialising) path, so error reports are unchanged.
+// Per-action LDS counters of k_claim / k_materialize, ACT_STRIPES copies
+// indexed by lane: the lanes of a wave mostly count the same few actions,
+// and LDS atomics on one address serialise.
+#ifndef KC_ACT_STRIPES
+#define KC_ACT_STRIPES 4
+#endif
+constexpr int ACT_STRIPES = KC_ACT_STRIPES;
+template <int AS = ACT_STRIPES>
+__device__ __forceinline__ unsigned int act_sum(const unsigned int* sh, unsigned int a) {
+  unsigned int v = 0;
+#pragma unroll
+  for (int k = 0; k < AS; ++k) v += sh[a * AS + k];
+  return v;
+}
 struct DeferArgs {
   const void* prev = nullptr;                 // the previous frontier (State*); nullptr: cur holds the states
   const unsigned long long* parent = nullptr; // trace: global parent index per state (keep_trace) ...
@@ -295,7 +309,7 @@ struct DeferArgs {
 
 // Rebuild frontier state i (index within the level) from its link; stores it
 // into df.out, checks the invariants and counts its action into sh_actd.
-template <class M>
+template <class M, int AS = ACT_STRIPES>
 __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, uint64_t i, const Flags& f,
                                                            unsigned int* sh_actd, Counters* __restrict__ C) {
   uint64_t pp;
@@ -316,7 +330,7 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
   M::apply(gp, slot, j, f, s);
   store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
   if (M::check(s, f.inv_mask) >= 0) atomicOr(&C->defer_flags, DF_INVARIANT);
-  atomicAdd(&sh_actd[M::slot_action(gp, slot)], 1u);
+  atomicAdd(&sh_actd[M::slot_action(gp, slot) * AS + (threadIdx.x & (AS - 1))], 1u);
   return s;
 }
 
@@ -325,8 +339,8 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
 // the level's successor count (next_cand).
 template <class M>
 __global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, Flags f, Counters* __restrict__ C) {
-  __shared__ unsigned int sh_actd[A_COUNT];
-  if (threadIdx.x < A_COUNT) sh_actd[threadIdx.x] = 0;
+  __shared__ unsigned int sh_actd[A_COUNT * ACT_STRIPES];
+  if (threadIdx.x < A_COUNT * ACT_STRIPES) sh_actd[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long cand = 0;
@@ -338,8 +352,10 @@ __global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, F
   for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
   if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&stripe(C).next_cand, cand);
   __syncthreads();
-  if (threadIdx.x < A_COUNT && sh_actd[threadIdx.x])
-    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_actd[threadIdx.x]);
+  if (threadIdx.x < A_COUNT) {
+    const unsigned int v = act_sum(sh_actd, threadIdx.x);
+    if (v) atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)v);
+  }
 }
 
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
@@ -358,11 +374,14 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh, DeferArgs df = DeferArgs{}) {
   constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
+  // (one stripe of action counters on the sharded path: OWN's projections
+  // take that LDS, and 6 workgroups per CU need it)
+  constexpr int AS = OWN ? 1 : ACT_STRIPES;
   __shared__ unsigned long long sh_fp[NT];
   __shared__ unsigned int sh_key[NT];
   __shared__ unsigned int sh_cur[CLAIM_TILE];     // newmask of the tile's parents
-  __shared__ unsigned int sh_act[A_COUNT];
-  __shared__ unsigned int sh_actd[A_COUNT];       // deferred frontier: actions that made the parents
+  __shared__ unsigned int sh_act[A_COUNT * AS];
+  __shared__ unsigned int sh_actd[A_COUNT * AS];   // deferred frontier: actions that made the parents
   __shared__ unsigned long long sh_dcand;         // deferred frontier: the parents' successor count
   __shared__ uint32_t sh_proj[OWN ? CLAIM_TILE : 1];  // OWN = 1: each parent's owner projection (kubeapi_spec.h)
   __shared__ unsigned int sh_rc;
@@ -401,7 +420,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   const uint64_t kbase = SH ? ((uint64_t)sh.rank << CLAIM_RANK_SHIFT) : 0ull;
   sh_cur[threadIdx.x] = 0;
-  if (threadIdx.x < A_COUNT) sh_act[threadIdx.x] = sh_actd[threadIdx.x] = 0;
+  if (threadIdx.x < A_COUNT * AS) sh_act[threadIdx.x] = sh_actd[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t tile = spread_tile(blockIdx.x, gridDim.x, sh.spread);
 #ifdef KC_DIAG
@@ -431,7 +450,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   uint64_t fold = 0, counts = 0;
   int tot = 0;
   if (live) {
-    s = (!SH && df.prev) ? defer_rebuild<M>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
+    s = (!SH && df.prev) ? defer_rebuild<M, AS>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
     if (!SH && df.counts_out) df.counts_out[base + i] = pl.counts;
     // (an LDS total, not a register live through the kernel: k_claim sits at
@@ -448,7 +467,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 #pragma unroll
       for (int slot = 0; slot < M::NSLOT; ++slot) {      // per-action "generated" (msg 2772)
         const int c = (int)((pl.counts >> (6 * slot)) & 63);
-        if (c) atomicAdd(&sh_act[M::slot_action(s, slot)], (unsigned)c);
+        if (c) atomicAdd(&sh_act[M::slot_action(s, slot) * AS + (threadIdx.x & (AS - 1))], (unsigned)c);
       }
     }
     tot = pl.total;
@@ -677,11 +696,15 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) pw += __shfl_down(pw, off, 64);
   if ((threadIdx.x & 63) == 0 && pw) atomicAdd(&stripe(C).probes, pw);
-  if (threadIdx.x < A_COUNT && sh_act[threadIdx.x])
-    atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)sh_act[threadIdx.x]);
+  if (threadIdx.x < A_COUNT) {
+    const unsigned int v = act_sum<AS>(sh_act, threadIdx.x);
+    if (v) atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)v);
+  }
   if (!SH && df.prev) {
-    if (threadIdx.x < A_COUNT && sh_actd[threadIdx.x])
-      atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_actd[threadIdx.x]);
+    if (threadIdx.x < A_COUNT) {
+      const unsigned int v = act_sum<AS>(sh_actd, threadIdx.x);
+      if (v) atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)v);
+    }
     if (threadIdx.x == 0 && sh_dcand) atomicAdd(&stripe(C).next_cand, sh_dcand);
   }
 #ifdef KC_DIAG
@@ -1048,14 +1071,14 @@ k_emit_links(uint64_t n, uint64_t base, const uint32_t* __restrict__ newmask, co
              uint64_t level_gidx, uint64_t next_gidx, unsigned long long* __restrict__ parent,
              uint8_t* __restrict__ ord, unsigned long long* __restrict__ link, uint64_t cap,
              Counters* __restrict__ C) {
-  __shared__ unsigned int sh_deg[OUTDEG_BINS];
+  __shared__ unsigned int sh_deg[OUTDEG_BINS * ACT_STRIPES];   // (striped by lane, as k_claim's counters)
   __shared__ unsigned int sh_wtot[4];
-  if (threadIdx.x < OUTDEG_BINS) sh_deg[threadIdx.x] = 0;
+  if (threadIdx.x < OUTDEG_BINS * ACT_STRIPES) sh_deg[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t mask = i < n ? newmask[i] : 0u;
   const int cnt = __builtin_popcount(mask);
-  if (i < n) atomicAdd(&sh_deg[cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1], 1u);
+  if (i < n) atomicAdd(&sh_deg[(cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1) * ACT_STRIPES + (threadIdx.x & (ACT_STRIPES - 1))], 1u);
   const int lane = (int)(threadIdx.x & 63);
   int incl = cnt;
 #pragma unroll
@@ -1098,8 +1121,10 @@ k_emit_links(uint64_t n, uint64_t base, const uint32_t* __restrict__ newmask, co
   }
   if (over) atomicOr(&C->defer_flags, DF_CAPACITY);
   __syncthreads();
-  if (threadIdx.x < OUTDEG_BINS && sh_deg[threadIdx.x])
-    atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)sh_deg[threadIdx.x]);
+  if (threadIdx.x < OUTDEG_BINS) {
+    const unsigned int v = act_sum(sh_deg, threadIdx.x);
+    if (v) atomicAdd(&stripe(C).outdeg[threadIdx.x], (unsigned long long)v);
+  }
 }
 
 // Pinned to 8 waves per SIMD (64 VGPRs; unpinned it took 68 = 7 waves):
