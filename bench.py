@@ -160,17 +160,33 @@ def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     for f in reversed(files):
         try:
             with open(f) as fh:
-                k = json.load(fh)["kernels"].get(kernel, {})
-        except (OSError, ValueError):
+                d = json.load(fh)
+            k = d["kernels"].get(kernel, {})
+        except (OSError, ValueError, KeyError):
             continue
         if "fetch_bytes_per_launch_raw" in k and "write_bytes_per_launch_raw" in k:
             b = k["fetch_bytes_per_launch_raw"] + stream_read_bytes / 2 + k["write_bytes_per_launch_raw"]
-            return int(b), os.path.relpath(f, ROOT)
-        if "fetch_size_kib_per_launch_raw" in k and "write_size_kib_per_launch_raw" in k:   # r01 files
-            b = 1024 * (k["fetch_size_kib_per_launch_raw"] + k["write_size_kib_per_launch_raw"]) \
-                + stream_read_bytes / 2
-            return int(b), os.path.relpath(f, ROOT)
-    return None, None
+            return int(b), os.path.relpath(f, ROOT), d.get("build_id")
+    return None, None, None
+
+
+def set_traffic(roof: dict, traffic, src, bid) -> None:
+    """roofline.traffic is a PMC measurement only when the committed profile
+    was taken on the kernels of this build (same kubecheck.build_id); an
+    older profile's figure goes to traffic_estimate, traffic stays null."""
+    from kubecheck._lib import build_id
+
+    if traffic is None:
+        return
+    if bid == build_id():
+        roof["traffic"] = traffic
+        roof["traffic_unit"] = "HBM bytes per launch (PMC)"
+        roof["traffic_source"] = f"{src} (build {bid}, this build)"
+    else:
+        roof["traffic"] = None
+        roof["traffic_estimate"] = traffic
+        roof["traffic_source"] = (f"{src}: PMC of build {bid or 'unrecorded'}, not this build "
+                                  f"({build_id()}); an estimate, not a measurement of these kernels")
 
 
 def host_cpu_info() -> dict:
@@ -227,16 +243,24 @@ def cpu_baseline(kw, seconds):
     # (tools/gpu_prof_r02.sh ... cpu): too long for every bench run
     if (kw["nc"], kw["np"], kw["ns"]) == (1, 2, 1):
         import glob
-        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_cpu_np2_full.json")))[-1:]:
+        # the whole model at 16, 64, 128 and all 256 affinity CPUs of a GPU
+        # box's host (tools/gpu_r04_probe.sh): the box's CPU share makes more
+        # threads slower, so 16 is the comparator's best
+        sweep = []
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r04a_cpu_np2_full_t*.json"))):
             try:
                 with open(f) as fh:
                     full = json.load(fh)
-                out["full_model_run"] = {"seconds": full["seconds"], "threads": full["threads"],
-                                         "distinct": full["distinct"], "generated": full["generated"],
-                                         "distinct_per_s": full["distinct_per_s"],
-                                         "source": os.path.relpath(f, ROOT)}
+                sweep.append({"threads": full["threads"], "seconds": full["seconds"],
+                              "distinct_per_s": full["distinct_per_s"], "exact": full["distinct"] == 740607995,
+                              "source": os.path.relpath(f, ROOT)})
             except (OSError, ValueError, KeyError):
                 pass
+        if sweep:
+            sweep.sort(key=lambda e: e["threads"])
+            best = max(sweep, key=lambda e: e["distinct_per_s"])
+            out["full_model_run"] = dict(best)
+            out["full_model_thread_sweep"] = sweep
     return out
 
 
@@ -306,10 +330,7 @@ def bench_single(args, kw, desc):
         name, roof = roofline_bfs(tt, acc, S)
         # k_claim streams its parents (S B each); everything else it reads is a random probe
         stream = acc["parents"] * S / max(times["expand"][1], 1) if roof["kernel"] == "k_claim" else 0.0
-        roof["traffic"], src = pmc_traffic(args.workload, roof["kernel"], stream)
-        if src:
-            roof["traffic_unit"] = "HBM bytes per launch (PMC)"
-            roof["traffic_source"] = src
+        set_traffic(roof, *pmc_traffic(args.workload, roof["kernel"], stream))
         out["roofline"] = roof
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items() if v[0] > 0}
         if narrow[1]:
@@ -350,7 +371,6 @@ def bench_fpset(args):
         tlk += tl
     load, table_bytes = s.size() / s.capacity(), s.capacity() * 8
     s.close()
-    traffic, tsrc = pmc_traffic("fpset", "k_stress_insert")
     gbs = n * args.steps * 64 / tin / 1e9
     out = {
         "metric": "FPSet probe HBM GB/s (insert)", "value": round(gbs, 1), "unit": "GB/s",
@@ -364,11 +384,10 @@ def bench_fpset(args):
                    "lookups_per_s": round(n * args.steps / tlk, 1),
                    "lookups_found": int(found)},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_stress_insert", "bytes_per_launch": batch * 64,
-                     "traffic_unit": "HBM bytes per launch (PMC, one launch = one batch)",
-                     "traffic_source": tsrc},
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_stress_insert", "bytes_per_launch": batch * 64},
     }
+    set_traffic(out["roofline"], *pmc_traffic("fpset", "k_stress_insert"))
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fpset(args.fp_load)
     return out
@@ -480,8 +499,11 @@ def main():
                 return
         else:
             out = bench_single(args, kw, desc)
-        if args.gpus == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(kw, args.cpu_seconds)
+        if not args.no_cpu_baseline:
+            # rank 0 only (the other ranks returned above), after every rank's
+            # timed region; at N > 1 a shorter sample keeps the run within minutes
+            secs = args.cpu_seconds if args.gpus == 1 else min(args.cpu_seconds, 10.0)
+            out["cpu_baseline"] = cpu_baseline(kw, secs)
     print(json.dumps(out), file=jout, flush=True)
 
 

@@ -31,6 +31,9 @@ CASES = [
     {"name": "lost_update", "kw": {"variant": 1, "invariants": 7}},
     {"name": "fault_pack", "kw": {}, "env": {"KC_FAULT": "1:7:1"}, "all_ranks": True},
     {"name": "fault_expand_hostrows", "kw": {}, "env": {"KC_FAULT": "0:9:0", "KC_DEVROW": "0"}, "all_ranks": True},
+    # a failure after the all-gather, as if the exchange buffers could not be
+    # grown: the rank still takes part in the exchange through its sink
+    {"name": "fault_grow", "kw": {}, "env": {"KC_FAULT": "1:7:3"}, "all_ranks": True},
 ]
 
 
@@ -107,7 +110,7 @@ def test_errors_and_traces(results, fixtures, oracle, key, name, kind):
 
 def test_fault_stops_every_rank(results):
     world, res = results
-    for name in ("fault_pack", "fault_expand_hostrows"):
+    for name in ("fault_pack", "fault_expand_hostrows", "fault_grow"):
         got = res[name]
         assert sorted(got) == list(range(world)), name
         for rk, r in got.items():

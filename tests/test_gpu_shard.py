@@ -272,7 +272,7 @@ def test_native_multipiece_emulated(fixtures, monkeypatch):
     assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"]
 
 
-@pytest.mark.parametrize("stage", [0, 1, 2])
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
 @pytest.mark.parametrize("devrow", ["1", "0"])
 def test_native_fault_stops_every_rank(monkeypatch, stage, devrow):
     # a failure on one rank (KC_FAULT=rank:level:stage) travels in the

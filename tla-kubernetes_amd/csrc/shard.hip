@@ -368,7 +368,9 @@ __device__ __forceinline__ void emit_rec_block(uint64_t blk, const Record<M>* __
     store_state<M>(next, o, x);
     pkeys[next_gidx + o] = key;
     if (M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
-    atomicAdd(&sh_act[key & 0xff], 1u);
+    // (a record's action byte indexes LDS: a zeroed record of a failed rank
+    // reads 0; anything out of range would be a corrupt record, counted nowhere)
+    if ((key & 0xff) < (uint64_t)A_COUNT) atomicAdd(&sh_act[key & 0xff], 1u);
     cand = (unsigned long long)M::plan(x, f).total;
   }
 #pragma unroll

@@ -47,7 +47,10 @@ namespace {
 
 constexpr uint64_t NONE = ~0ull;
 constexpr uint64_t KEY44 = (1ull << 44) - 1;
-constexpr uint64_t PIECE_BYTES = 256ull << 20;   // largest single send/recv of the exchange
+// largest single send/recv of the exchange; also the size of each half of a
+// rank's failure sink (Group::run: a rank that cannot grow its exchange
+// buffers still takes part in the all-to-all, through the sink)
+constexpr uint64_t PIECE_BYTES = 64ull << 20;
 
 // Largest single transfer of the exchange in bytes: PIECE_BYTES, or
 // KC_PIECE_BYTES from the environment (tests shrink it so a small model runs
@@ -155,9 +158,12 @@ class Comm {
   // out = rank-major rows of every rank (world * L)
   virtual int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) = 0;
   // per local shard: send buffer grouped by destination; Mx[src][dst] record
-  // counts of every rank; recv buffers grouped by source
+  // counts of every rank; recv buffers grouped by source.  sunk[i]: local
+  // shard i failed without buffers for this exchange; it still takes part
+  // (its peers are waiting for it), sending zeroed records from the comm's
+  // sink and receiving into it, every piece at the sink's start.
   virtual int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx,
-                         uint64_t rec_bytes, const std::vector<void*>& recv) = 0;
+                         uint64_t rec_bytes, const std::vector<void*>& recv, const std::vector<char>& sunk) = 0;
   // *v: in on the local shard of rank `root` (if any), out everywhere
   virtual int broadcast(int root, uint64_t* v) = 0;
   // v[i] = the vector of local shard i; out = the element-wise sum over ranks
@@ -216,7 +222,7 @@ class LocalComm final : public Comm {
   // every rank's exchange plan, its pieces paired as RCCL pairs them: the
   // k-th send from src to dst with the k-th receive at dst from src
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx,
-                 uint64_t rb, const std::vector<void*>& recv) override {
+                 uint64_t rb, const std::vector<void*>& recv, const std::vector<char>& sunk) override {
     const int R = (int)s_.size();
     const uint64_t piece = std::max<uint64_t>(1, piece_bytes() / rb);
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every pack is done
@@ -240,8 +246,13 @@ class LocalComm final : public Comm {
                       (unsigned long long)sends[k]->n, (unsigned long long)recvs[k]->n);
             return -EIO;
           }
-          KC_HIP_TRY(hipMemcpyAsync((char*)recv[dst] + recvs[k]->off * rb, (const char*)send[src] + sends[k]->off * rb,
-                                    sends[k]->n * rb, hipMemcpyDeviceToDevice, s_[dst]->stream()));
+          if (sunk[dst]) continue;                  // (the failed rank's sink takes it)
+          char* to = (char*)recv[dst] + recvs[k]->off * rb;
+          if (sunk[src])                             // a failed sender's records are zeroes
+            KC_HIP_TRY(hipMemsetAsync(to, 0, sends[k]->n * rb, s_[dst]->stream()));
+          else
+            KC_HIP_TRY(hipMemcpyAsync(to, (const char*)send[src] + sends[k]->off * rb, sends[k]->n * rb,
+                                      hipMemcpyDeviceToDevice, s_[dst]->stream()));
         }
       }
     }
@@ -272,6 +283,7 @@ class RcclComm final : public Comm {
     trivial_ = s->world() == 1 && !(f && f[0] == '1');
   }
   ~RcclComm() override {
+    if (sink_) (void)hipFree(sink_);
     if (buf_) (void)hipFree(buf_);
     if (hbuf_) (void)hipHostFree(hbuf_);
     if (comm_ && rccl()) (void)rccl()->comm_destroy(comm_);
@@ -305,18 +317,33 @@ class RcclComm final : public Comm {
     out.assign(hbuf_ + L, hbuf_ + L + L * R);
     return 0;
   }
+  // The failure sink: allocated with the communicator (a rank that failed
+  // for want of memory could not allocate it then), two halves of one piece.
+  int make_sink() {
+    if (trivial_ || sink_) return 0;
+    KC_HIP_TRY(hipMalloc(&sink_, 2 * piece_bytes()));
+    return 0;
+  }
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
-                 const std::vector<void*>& recv) override {
+                 const std::vector<void*>& recv, const std::vector<char>& sunk) override {
     const uint64_t rw = rb / 8;                       // records are whole 8-byte words
     const uint64_t piece = std::max<uint64_t>(1, piece_bytes() / rb);   // records per piece
     hipStream_t st = s_->stream();
     const std::vector<Xfer> plan = exchange_plan(Mx, s_->rank(), piece);
+    const bool sk = sunk[0] != 0;
+    if (sk && !sink_) {
+      set_error("kc_group_run: rank %d failed without a failure sink", s_->rank());
+      return -EIO;
+    }
+    if (sk) KC_HIP_TRY(hipMemsetAsync(sink_, 0, piece * rb, st));
     KC_NCCL_TRY(rccl()->group_start());
     for (const auto& x : plan) {
       if (x.send)
-        KC_NCCL_TRY(rccl()->send((const uint64_t*)send[0] + x.off * rw, x.n * rw, ncclUint64, x.peer, comm_, st));
+        KC_NCCL_TRY(rccl()->send(sk ? (const uint64_t*)sink_ : (const uint64_t*)send[0] + x.off * rw, x.n * rw,
+                                 ncclUint64, x.peer, comm_, st));
       else
-        KC_NCCL_TRY(rccl()->recv((uint64_t*)recv[0] + x.off * rw, x.n * rw, ncclUint64, x.peer, comm_, st));
+        KC_NCCL_TRY(rccl()->recv(sk ? (uint64_t*)sink_ + piece * rw : (uint64_t*)recv[0] + x.off * rw, x.n * rw,
+                                 ncclUint64, x.peer, comm_, st));
     }
     KC_NCCL_TRY(rccl()->group_end());
     return 0;                                          // stream-ordered before insert
@@ -367,6 +394,7 @@ class RcclComm final : public Comm {
   ShardBase* s_;
   bool trivial_ = false;
   ncclComm_t comm_ = nullptr;
+  uint64_t* sink_ = nullptr;
   uint64_t* buf_ = nullptr;
   uint64_t* hbuf_ = nullptr;
   size_t cap_ = 0;
@@ -413,8 +441,9 @@ class HostComm final : public Comm {
     return call(ops_.all_gather(ops_.ctx, hrow_, L, out.data()), "all_gather");
   }
   int all_to_all(const std::vector<void*>& send, const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb,
-                 const std::vector<void*>& recv) override {
+                 const std::vector<void*>& recv, const std::vector<char>& sunk) override {
     const int me = s_->rank(), R = s_->world();
+    if (sunk[0]) return sunk_exchange(Mx, rb);
     uint64_t ns = 0, nr = 0;
     for (int p = 0; p < R; ++p) {
       ns += Mx[me][p];
@@ -444,6 +473,22 @@ class HostComm final : public Comm {
   }
 
  private:
+  // A failed rank's part of the exchange: zeroes out, every piece in and out
+  // at the start of a host sink (plain memory: its pinned staging is what it
+  // may have failed to grow).
+  int sunk_exchange(const std::vector<std::vector<uint64_t>>& Mx, uint64_t rb) {
+    const uint64_t piece = std::max<uint64_t>(1, piece_bytes() / rb);
+    const std::vector<Xfer> plan = exchange_plan(Mx, s_->rank(), piece);
+    std::vector<uint64_t> xf(4 * plan.size());
+    for (size_t k = 0; k < plan.size(); ++k) {
+      xf[4 * k] = (uint64_t)plan[k].peer;
+      xf[4 * k + 1] = (uint64_t)plan[k].send;
+      xf[4 * k + 2] = 0;
+      xf[4 * k + 3] = plan[k].n * rb;
+    }
+    std::vector<uint8_t> out(piece * rb, 0), in(piece * rb);
+    return call(ops_.exchange(ops_.ctx, xf.data(), (int)plan.size(), out.data(), in.data()), "exchange");
+  }
   static int call(int rc, const char* what) {
     if (rc < 0) {
       set_error("kc_host_comm %s failed (%d)", what, rc);
@@ -482,7 +527,8 @@ class Group {
     const char* dr = getenv("KC_DEVROW");     // KC_DEVROW=0: host rows + expand's own sync (A/B)
     dev_row_off_ = dr && dr[0] == '0';
     // fault injection for the failure-path tests: KC_FAULT=rank:level:stage
-    // (stage 0 expand, 1 pack, 2 insert) fails that rank's stage with -EIO
+    // (stage 0 expand, 1 pack, 2 insert, 3 after the all-gather as if the
+    // exchange buffers could not be grown) fails that rank's stage with -EIO
     const char* fl = getenv("KC_FAULT");
     if (fl && sscanf(fl, "%d:%d:%d", &fault_rank_, &fault_level_, &fault_stage_) != 3) fault_rank_ = -1;
     world_ = local_[0]->world();
@@ -564,9 +610,12 @@ class Group {
 // watchdog).  A rank that fails records the code and keeps taking part in
 // the collectives; the failure travels in the all-gather row (word R + 2;
 // claims that overflow set it on the device) and every rank stops at the
-// next gather with an error.  A failure after the gather (pack, insert)
-// sends zeroed records for the rest of the level; the error walk and the
-// final reduction carry a failure flag the same way.
+// next gather with an error.  A failure after the gather (the end of
+// expand, growing the exchange buffers, pack, insert) sends zeroed records
+// for the rest of the level — from the communicator's failure sink when the
+// buffers could not be grown — so no peer waits in the all-to-all and none
+// receives stale bytes; the error walk and the final reduction carry a
+// failure flag the same way.
 int Group::run(kc_result* res) {
   memset(res, 0, sizeof *res);
   res->err_action = res->err_self = res->err_invariant = -1;
@@ -621,7 +670,7 @@ int Group::run(kc_result* res) {
       for (size_t i = 0; i < nl; ++i) {
         std::fill(counts[i].begin(), counts[i].end(), 0);
         e1[i] = NONE;
-        KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+        if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
         inject(i, level, 0);
         if (!fail[i]) note(i, local_[i]->expand_dev(status_new[i], status_err[i], level == 1, d_rows[i]));
         if (fail[i]) {          // the row says so, whatever else it holds
@@ -644,8 +693,8 @@ int Group::run(kc_result* res) {
         std::fill(counts[i].begin(), counts[i].end(), 0);
         e1[i] = NONE;
         if (!last) inject(i, level, 0);
+        if (!last && !fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
         if (!last && !fail[i]) {
-          KC_HIP_TRY(hipSetDevice(local_[i]->device()));
           note(i, local_[i]->expand(counts[i].data(), &e1[i]));
           if (level == 1 && e1[i] != NONE && (e1[i] & 0xFF) == 0x12) {
             // an Init state violates an invariant: level 1's error, ahead of
@@ -679,6 +728,7 @@ int Group::run(kc_result* res) {
     }
     widths.push_back(total);
     if (last) break;
+    std::vector<char> sunk(nl, 0);
     for (size_t i = 0; i < nl; ++i) {
       const int me = local_[i]->rank();
       uint64_t ns = 0, nr = 0;
@@ -688,26 +738,33 @@ int Group::run(kc_result* res) {
       }
       sent_local_[i] += ns - Mx[me][me];
       const uint64_t rb = local_[i]->record_bytes();
-      // (without its buffers a rank cannot take part in the exchange at all)
-      KC_TRY(buffer(send_, send_cap_, i, std::max<uint64_t>(ns, 1) * rb));
-      KC_TRY(buffer(recv_, recv_cap_, i, std::max<uint64_t>(nr, 1) * rb));
-      KC_HIP_TRY(hipSetDevice(local_[i]->device()));
-      // (a rank cannot reach pack already failed: the gather above would
-      // have stopped every rank; a failed pack means a broken device, and
-      // its records are zeroed)
-      const bool pre = fail[i] != 0;
-      if (!pre) note(i, local_[i]->pack(send_[i]));
-      if (fail[i] && !pre && ns) KC_HIP_TRY(hipMemsetAsync(send_[i], 0, ns * rb, local_[i]->stream()));
+      // a rank that failed here (expand_done above, or growing its buffers)
+      // still takes part in the exchange: zeroed records, through the sink
+      // if it has no buffers of the size
+      if (!fail[i]) note(i, buffer(send_, send_cap_, i, std::max<uint64_t>(ns, 1) * rb));
+      if (!fail[i]) note(i, buffer(recv_, recv_cap_, i, std::max<uint64_t>(nr, 1) * rb));
+      const bool grow_fault = !fail[i] && local_[i]->rank() == fault_rank_ && level == fault_level_ && fault_stage_ == 3;
+      inject(i, level, 3);
+      if (fail[i] && (grow_fault || send_cap_[i] < std::max<uint64_t>(ns, 1) * rb ||
+                      recv_cap_[i] < std::max<uint64_t>(nr, 1) * rb))
+        sunk[i] = 1;
+      if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
+      bool packed = false;
+      if (!fail[i]) {
+        note(i, local_[i]->pack(send_[i]));
+        packed = !fail[i];
+      }
+      if (!packed && !sunk[i] && ns) note(i, hipMemsetAsync(send_[i], 0, ns * rb, local_[i]->stream()) == hipSuccess ? 0 : -EIO);
       inject(i, level, 1);      // (a failure found after a complete pack)
     }
     std::vector<void*> sv(send_.begin(), send_.end()), rv(recv_.begin(), recv_.end());
-    KC_TRY(comm_->all_to_all(sv, Mx, local_[0]->record_bytes(), rv));
+    KC_TRY(comm_->all_to_all(sv, Mx, local_[0]->record_bytes(), rv, sunk));
     for (size_t i = 0; i < nl; ++i) {
       const int me = local_[i]->rank();
       uint64_t nr = 0;
       for (int s = 0; s < R; ++s) nr += Mx[s][me];
       uint64_t n_new = 0, e2 = NONE;
-      KC_HIP_TRY(hipSetDevice(local_[i]->device()));
+      if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
       inject(i, level, 2);
       if (!fail[i]) note(i, local_[i]->insert(recv_[i], nr, &n_new, &e2));
       if (!fail[i]) note(i, local_[i]->advance());
@@ -839,8 +896,9 @@ int kc_group_create_rccl(kc_shard* s, const uint8_t* id, kc_group** out) {
   memcpy(&uid, id, sizeof uid);
   ncclComm_t comm = nullptr;
   KC_NCCL_TRY(api->comm_init_rank(&comm, sh->world(), uid, sh->rank()));
-  *out = new kc_group{std::unique_ptr<Group>(
-      new Group({sh}, std::unique_ptr<Comm>(new RcclComm(sh, comm)), sh->config()))};
+  std::unique_ptr<RcclComm> rc(new RcclComm(sh, comm));
+  KC_TRY(rc->make_sink());
+  *out = new kc_group{std::unique_ptr<Group>(new Group({sh}, std::move(rc), sh->config()))};
   return 0;
 }
 

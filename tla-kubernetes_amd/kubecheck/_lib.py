@@ -213,6 +213,25 @@ def load() -> C.CDLL:
     return lib
 
 
+def build_id() -> str:
+    """A digest of the HIP sources libkubecheck.so is built from (csrc/*.hip,
+    *.h and the C-ABI header).  Profiles record it (tools/pmc_summary.py), so
+    a bench line uses a committed PMC figure as a measurement only when it
+    was taken on the kernels of this build."""
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    hdr = os.path.join(os.path.dirname(os.path.dirname(csrc)), "include", "kubecheck.h")
+    h = hashlib.sha1()
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h"))) if os.path.isdir(csrc) else []
+    for f in [os.path.join(csrc, f) for f in files] + [hdr]:
+        try:
+            with open(f, "rb") as fh:
+                h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+        except OSError:
+            pass
+    return h.hexdigest()[:16]
+
+
 def check(func: str, rc: int) -> int:
     if rc < 0:
         msg = load().kc_last_error()

@@ -566,10 +566,10 @@ def pmc_ratio(workload: str):
             k, alg = d["kernels"]["k_claim"], d["algorithmic"]
             hbm = k["fetch_bytes_per_launch_raw"] + alg["stream_read_bytes_per_launch"] / 2 + \
                 k["write_bytes_per_launch_raw"]
-            return hbm / alg["algorithmic_bytes_per_launch"], os.path.relpath(f, root)
+            return hbm / alg["algorithmic_bytes_per_launch"], os.path.relpath(f, root), d.get("build_id")
         except (OSError, ValueError, KeyError, ZeroDivisionError):
             continue
-    return None, None
+    return None, None, None
 
 
 def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict]:
@@ -621,6 +621,25 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     dist.all_reduce(agg, op=dist.ReduceOp.SUM)
     tot_bytes, tot_ns, tot_launch, xgmi = [int(x) for x in agg.tolist()]
     mc.close() if native else be.close()
+    # the loop's per-level fixed cost, measured: Model_1 (124 levels, at most
+    # 3,939 states wide) through the same loop and ranks is nearly all fixed
+    # cost (launches, host syncs, collectives)
+    fixed = None
+    if native:
+        m1 = NativeShardedChecker(ModelConfig(device=local, keep_trace=False), rank, world)
+        try:
+            m1.run()
+            dist.barrier()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                r1 = m1.run()
+            d1 = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
+            dist.all_reduce(d1, op=dist.ReduceOp.MAX)
+            fixed = {"model1_ms_per_check": round(float(d1.item()) / 3 * 1e3, 3), "levels": r1["depth"],
+                     "us_per_level": round(float(d1.item()) / 3 / r1["depth"] * 1e6, 2),
+                     "narrow_levels": r1.get("narrow_levels")}
+        finally:
+            m1.close()
     out = None
     if rank == 0:
         golden = golden_check(args.workload, res) if golden_check else None
@@ -640,7 +659,8 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
                                       "RCCL all-to-all per BFS level",
                        "xgmi_bytes_per_step": xgmi // max(args.steps, 1),
                        "xgmi_GBps_per_gpu": round(xgmi / max(args.steps, 1) / world
-                                                  / (dt / args.steps) / 1e9, 2)},
+                                                  / (dt / args.steps) / 1e9, 2),
+                       "per_level_fixed_cost": fixed},
         }
         if tot_ns > 0:
             achieved = tot_bytes / (tot_ns * 1e-9) / 1e9
@@ -651,13 +671,20 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
                                "launches": tot_launch,
                                "avg_launch_us": round(tot_ns / 1e3 / max(tot_launch, 1), 2),
                                "bytes_per_launch": bpl}
-            ratio, src = pmc_ratio(args.workload)
+            ratio, src, bid = pmc_ratio(args.workload)
             if ratio:
-                out["roofline"]["traffic"] = int(ratio * bpl)
-                out["roofline"]["traffic_unit"] = "HBM bytes per launch (PMC)"
-                out["roofline"]["traffic_source"] = (
-                    f"{src}: PMC bytes / algorithmic bytes of the sharded k_claim = {ratio:.3f} "
-                    "(rocprofv3 FETCH_SIZE + WRITE_SIZE passes over emulated ranks on one GPU), "
-                    "times this run's algorithmic bytes per launch")
+                from ._lib import build_id
+                roof = out["roofline"]
+                how = (f"{src}: PMC bytes / algorithmic bytes of the sharded k_claim = {ratio:.3f} "
+                       "(rocprofv3 FETCH_SIZE + WRITE_SIZE passes over emulated ranks on one GPU), "
+                       "times this run's algorithmic bytes per launch")
+                if bid == build_id():
+                    roof["traffic"] = int(ratio * bpl)
+                    roof["traffic_unit"] = "HBM bytes per launch (PMC ratio of this build's kernel)"
+                    roof["traffic_source"] = f"{how}; profile build {bid} = this build"
+                else:                      # a profile of other kernels: not a measurement of these
+                    roof["traffic_estimate"] = int(ratio * bpl)
+                    roof["traffic_source"] = (f"{how}; profile build {bid or 'unrecorded'} is not this build "
+                                              f"({build_id()}): an estimate only")
     dist.destroy_process_group()
     return out

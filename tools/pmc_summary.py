@@ -94,7 +94,10 @@ def main():
             e["hbm_bytes_per_launch_raw"] = e["fetch_bytes_per_launch_raw"] + e["write_bytes_per_launch_raw"]
             e["hbm_GBps_raw"] = round(e["hbm_bytes_per_launch_raw"] / (e["avg_us"] * 1e3), 2)
         kernels[k] = e
-    out = {"command": a.command,
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tla-kubernetes_amd"))
+    from kubecheck._lib import build_id
+    out = {"command": a.command, "build_id": build_id(),
            "correction": "raw bytes = FETCH_SIZE*1024 + WRITE_SIZE*1024; hbm_read = raw fetch + "
                          "streaming_read/2 (profiles/r02b_pmc_calibration.json)",
            "kernels": kernels}
