@@ -274,6 +274,12 @@ typedef struct {
    * exceeded; the reported result is the redone run's) */
   uint64_t deferred_states;
   uint64_t defer_fallback;
+  /* the level an exact redo of a deferred-frontier anomaly started from (the
+   * anomaly's level; 1 = from Init), 0 if there was none */
+  uint64_t defer_redo_level;
+  /* levels run by a device-driven narrow path (single-GPU engine: k_nfinish;
+   * sharded loop: the fixed-slot exchange levels, shard_narrow.h) */
+  uint64_t narrow_levels;
 } kc_result;
 
 typedef struct kc_engine kc_engine;

@@ -1076,6 +1076,7 @@ typedef struct {
   pvec cur;
   _Atomic uint64_t next;            /* next frontier index to take */
   _Atomic uint64_t *slots;          /* fingerprint set (0 = empty) */
+  unsigned __int128 *slots2;        /* or (fp_bits 128) two-hash keys (0 = empty) */
   uint64_t mask;
   struct timespec t0;
   double budget;
@@ -1106,6 +1107,26 @@ static uint64_t packed_fp(const uint64_t *w, int n) {
   uint64_t a = 0x243f6a8885a308d3ull;
   for (int i = 0; i < n; i++) a = mix64(a ^ w[i]) + 0x9e3779b97f4a7c15ull;
   return a ? a : 1;
+}
+
+/* a second, independent 64-bit hash of the same words (128-bit keys) */
+static uint64_t packed_fp2(const uint64_t *w, int n) {
+  uint64_t a = 0x13198a2e03707344ull;
+  for (int i = 0; i < n; i++) a = mix64((a + 0xa4093822299f31d0ull) ^ (w[i] * 0xff51afd7ed558ccdull));
+  return a ? a : 1;
+}
+/* 128-bit keys: every probe is one locked 16-byte compare-exchange (the
+ * returned value is the slot's, read atomically), so no torn read of a
+ * slot being filled can look like another key */
+static int par_insert2(par_level *L, uint64_t h1, uint64_t h2) {   /* 1 if new */
+  const unsigned __int128 key = ((unsigned __int128)h2 << 64) | h1;
+  uint64_t i = (h1 * 0x9e3779b97f4a7c15ull >> 17) & L->mask;
+  for (;;) {
+    const unsigned __int128 e = __sync_val_compare_and_swap(&L->slots2[i], (unsigned __int128)0, key);
+    if (e == 0) return 1;
+    if (e == key) return 0;
+    i = (i + 1) & L->mask;
+  }
 }
 
 static int par_insert(par_level *L, uint64_t fp) {   /* 1 if new */
@@ -1146,7 +1167,9 @@ static void *par_work(void *arg) {
           /* the packed words are canonical: hash those (cheaper than the
            * whole kstate) and store them as they are */
           kpacked pk; kpack(m, &succ[k], &pk);
-          if (par_insert(L, packed_fp(pk.w, pw))) pv_append(&w->out, pk.w);
+          const int fresh = L->slots2 ? par_insert2(L, packed_fp(pk.w, pw), packed_fp2(pk.w, pw))
+                                      : par_insert(L, packed_fp(pk.w, pw));
+          if (fresh) pv_append(&w->out, pk.w);
         }
       }
       if (elapsed_since(&L->t0) > L->budget) atomic_store(&L->stop, 1);
@@ -1162,23 +1185,30 @@ double ko_bench_parallel(const ko_config *cfg, int threads, double budget, ko_pa
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   const int log2 = cfg->fpset_log2 > 0 ? cfg->fpset_log2 : 28;
+  const int wide = cfg->fp_bits == 128;       /* (explicit: the timed comparator keeps 64-bit keys) */
   static par_level L;
   memset(&L, 0, sizeof L);
   L.m = &m; L.mask = (1ull << log2) - 1; L.budget = budget;
-  const size_t bytes = (1ull << log2) * sizeof(uint64_t);
+  const size_t bytes = (1ull << log2) * (wide ? 16 : sizeof(uint64_t));
   clock_gettime(CLOCK_MONOTONIC, &L.t0);
-  L.slots = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-  if (L.slots == MAP_FAILED) { fprintf(stderr, "kubeapi_oracle: out of memory\n"); abort(); }
-  madvise((void *)L.slots, bytes, MADV_HUGEPAGE);
+  void *mem = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (mem == MAP_FAILED) { fprintf(stderr, "kubeapi_oracle: out of memory\n"); abort(); }
+  madvise(mem, bytes, MADV_HUGEPAGE);
+  if (wide) L.slots2 = mem; else L.slots = mem;
+  out->fp_bits = wide ? 128 : 64;
   const int pw = 1 + 2 * (cfg->nc + cfg->np + cfg->ns);
   L.cur = (pvec){0, 0, 0, pw};
   kstate inits[16]; int ni = init_states(&m, inits);
   for (int i = 0; i < ni; i++) {
     kpacked pk; kpack(&m, &inits[i], &pk);
     out->generated++;
-    if (par_insert(&L, packed_fp(pk.w, pw))) pv_append(&L.cur, pk.w);
+    const int fresh = wide ? par_insert2(&L, packed_fp(pk.w, pw), packed_fp2(pk.w, pw))
+                           : par_insert(&L, packed_fp(pk.w, pw));
+    if (fresh) pv_append(&L.cur, pk.w);
   }
   out->distinct = L.cur.n;
+  out->depth = 1;
+  out->level_width[0] = L.cur.n;
   par_worker *W = calloc(threads, sizeof *W);
   pthread_t *T = calloc(threads, sizeof *T);
   pthread_barrier_init(&L.start, NULL, threads + 1);
@@ -1188,6 +1218,7 @@ double ko_bench_parallel(const ko_config *cfg, int threads, double budget, ko_pa
     pthread_create(&T[t], NULL, par_work, &W[t]);
   }
   while (L.cur.n && !atomic_load(&L.stop)) {
+    if (cfg->max_levels && out->depth >= cfg->max_levels) break;   /* (as the engine: depth max_levels) */
     out->levels++;
     atomic_store(&L.next, 0);
     for (int t = 0; t < threads; t++) W[t].out.n = 0;
@@ -1208,6 +1239,7 @@ double ko_bench_parallel(const ko_config *cfg, int threads, double budget, ko_pa
       nxt.n += W[t].out.n;
     }
     out->distinct += total;
+    if (total && out->depth < KO_MAXLEVELS) out->level_width[out->depth++] = total;
     free(L.cur.v);
     L.cur = nxt;
     if ((out->distinct + L.cur.n) * 10 > (L.mask + 1) * 6) {   /* keep the set below 60% */
@@ -1225,6 +1257,6 @@ double ko_bench_parallel(const ko_config *cfg, int threads, double budget, ko_pa
   pthread_barrier_destroy(&L.end);
   for (int t = 0; t < threads; t++) free(W[t].out.v);
   free(W); free(T); free(L.cur.v);
-  munmap((void *)L.slots, bytes);
+  munmap(mem, bytes);
   return out->seconds > 0 ? out->distinct / out->seconds : 0;
 }

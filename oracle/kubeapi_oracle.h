@@ -143,6 +143,11 @@ typedef struct {
   uint64_t distinct, generated;
   int levels, complete, set_full, threads;
   double seconds;
+  /* (golden fixtures of level-bounded models: cfg.max_levels is honoured,
+   * and cfg.fp_bits == 128 keys the set by two independent 64-bit hashes) */
+  int fp_bits;
+  int depth;                              /* levels of states found (level 1 = Init) */
+  uint64_t level_width[KO_MAXLEVELS];
 } ko_par_result;
 double ko_bench_parallel(const ko_config *cfg, int threads, double seconds_budget, ko_par_result *out);
 

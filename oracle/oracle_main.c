@@ -30,6 +30,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "-lostupdate")) cfg.lost_update = 1;
     else if (!strcmp(argv[i], "-trace")) print_trace = 1;
     else if (!strcmp(argv[i], "-fp64")) cfg.fp_bits = 64;
+    else if (!strcmp(argv[i], "-fp128")) cfg.fp_bits = 128;   /* (-threads: 128-bit keys) */
     else if (!strcmp(argv[i], "-fpsetlog2") && i + 1 < argc) cfg.fpset_log2 = atoi(argv[++i]);
     else if (!strcmp(argv[i], "-progress")) cfg.progress = 1;
     else if (!strcmp(argv[i], "-threads") && i + 1 < argc) threads = atoi(argv[++i]);
@@ -41,9 +42,13 @@ int main(int argc, char **argv) {
     double rate = ko_bench_parallel(&cfg, threads, budget, &p);
     printf("{\"nc\": %d, \"np\": %d, \"ns\": %d, \"threads\": %d, \"distinct\": %llu, "
            "\"generated\": %llu, \"levels\": %d, \"complete\": %d, \"set_full\": %d, "
-           "\"seconds\": %.3f, \"distinct_per_s\": %.1f}\n",
+           "\"seconds\": %.3f, \"distinct_per_s\": %.1f, \"fp_bits\": %d, \"depth\": %d, "
+           "\"max_levels\": %d, \"level_width\": [",
            cfg.nc, cfg.np, cfg.ns, p.threads, (unsigned long long)p.distinct,
-           (unsigned long long)p.generated, p.levels, p.complete, p.set_full, p.seconds, rate);
+           (unsigned long long)p.generated, p.levels, p.complete, p.set_full, p.seconds, rate, p.fp_bits,
+           p.depth, cfg.max_levels);
+    for (int l = 0; l < p.depth; l++) printf("%s%llu", l ? ", " : "", (unsigned long long)p.level_width[l]);
+    printf("]}\n");
     return 0;
   }
   static ko_result r;

@@ -151,7 +151,8 @@ def successors(cfg: KoConfig, tup):
 class KoParResult(C.Structure):
     _fields_ = [("distinct", C.c_uint64), ("generated", C.c_uint64), ("levels", C.c_int),
                 ("complete", C.c_int), ("set_full", C.c_int), ("threads", C.c_int),
-                ("seconds", C.c_double)]
+                ("seconds", C.c_double), ("fp_bits", C.c_int), ("depth", C.c_int),
+                ("level_width", C.c_uint64 * 4096)]
 
 
 def bench_parallel(cfg: KoConfig, threads: int, seconds: float) -> dict:

@@ -43,7 +43,8 @@ def main():
                 else:
                     os.environ[k] = v
         if rank == 0 or case.get("all_ranks"):
-            print("RESULT " + json.dumps(out), flush=True)
+            # one write of the whole line (the ranks share the launcher's stdout)
+            os.write(1, ("RESULT " + json.dumps(out) + "\n").encode())
         dist.barrier()
     dist.destroy_process_group()
 

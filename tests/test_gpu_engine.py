@@ -256,6 +256,22 @@ def test_np3_prefix(fixtures):
     assert (r.distinct, r.generated) == (fx["distinct"], fx["generated"]) and not r.complete
 
 
+def test_np3_52_levels():
+    # the scaling-sized workload (bench.py --workload np3_52): NP=3's first 52
+    # levels, 1.1e9 states, against the oracle's multi-threaded BFS with
+    # 128-bit keys (tools/np3_golden.sh; its first 40 levels equal the
+    # sequential oracle's np3_40levels)
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "np3_52levels.json")))
+    assert fx["fp_bits"] == 128 and fx["max_levels"] == 52 and not fx["set_full"]
+    r = run(np=3, max_levels=52, keep_trace=False)
+    assert r.level_width == fx["level_width"]
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"]) == (
+        r.distinct, r.generated, 52)
+    assert not r.complete and r.error is None
+
+
 # --- deferred frontier (engine_kernels.h DeferArgs): the wide levels' new
 # states are built inside the next level's k_claim from their links
 @pytest.mark.parametrize("defer", ["1", "0"])
@@ -276,21 +292,39 @@ def test_deferred_capacity_estimate_redo(fixtures, monkeypatch):
     monkeypatch.setenv("KC_DEFER_SLACK", "0.001")
     fx = fixtures["np2_40levels"]
     r = run(np=2, max_levels=40, keep_trace=False)
-    assert r.defer_fallback and r.deferred_states == 0
+    # each level past its estimate is redone from that level (not from Init)
+    assert r.defer_fallback and r.defer_redo_level > 1
     assert r.level_width == fx["level_width"]
     assert r.act_gen == fx["act_gen"] and r.act_dist == fx["act_dist"]
+    assert r.outdeg_hist == fx["outdeg_hist"]
+    # the same from Init (KC_DEFER_REDO=0)
+    monkeypatch.setenv("KC_DEFER_REDO", "0")
+    r0 = run(np=2, max_levels=40, keep_trace=False)
+    assert r0.defer_fallback and r0.defer_redo_level == 1
+    assert (r0.level_width, r0.act_gen, r0.act_dist) == (r.level_width, r.act_gen, r.act_dist)
 
 
 @pytest.mark.parametrize("key,kw", [("variant3", dict(variant=3)), ("variant2", dict(variant=2))])
-def test_deferred_error_redone_exactly(fixtures, key, kw):
+def test_deferred_error_redone_exactly(fixtures, monkeypatch, key, kw):
     # an error on a deferred wide level (Model_1 on the wide path): the run
-    # is redone on the materialising path, trace state for state
+    # is redone on the materialising path from the level the error belongs
+    # to — an Assert is found among the level's own parents (that level),
+    # an invariant among the states the level rebuilt (the previous level's
+    # emit would have found it) — trace state for state
     fx = fixtures[key]
     with ModelChecker(ModelConfig(chunk_states=1 << 20, **kw)) as mc:
         r = mc.run()
     assert r.defer_fallback
+    assert r.defer_redo_level == fx["err_level"] - (1 if r.error == "invariant" else 0)
     assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
     assert [list(map(int, t)) for t in r.trace] == fx["trace"]
+    # every partial count as the exact (materialising) path reports it
+    monkeypatch.setenv("KC_DEFER", "0")
+    with ModelChecker(ModelConfig(chunk_states=1 << 20, **kw)) as mc:
+        e = mc.run()
+    assert not e.defer_fallback and e.deferred_states == 0
+    for k in ("distinct", "generated", "level_width", "act_gen", "act_dist", "outdeg_hist", "error_level"):
+        assert getattr(r, k) == getattr(e, k), k
 
 
 def test_deferred_trace_in_host_memory(fixtures):

@@ -52,9 +52,11 @@ def run_ranks(world, tmp_path):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     out = {}
+    dec = json.JSONDecoder()
     for line in p.stdout.splitlines():
-        if line.startswith("RESULT "):
-            r = json.loads(line[7:])
+        # (a line may hold more than one rank's record if their writes interleave)
+        for chunk in line.split("RESULT ")[1:]:
+            r, _ = dec.raw_decode(chunk)
             out.setdefault(r["case"], {})[r["rank"]] = r
     return out
 

@@ -50,9 +50,18 @@ const char* kActionNames[A_COUNT] = {
 __global__ void __launch_bounds__(64)
 k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask, uint64_t n,
           Counters* __restrict__ C, const uint32_t* __restrict__ tile_off, uint64_t tiles,
-          unsigned long long* __restrict__ host, unsigned long long* __restrict__ ovf_count = nullptr) {
+          unsigned long long* __restrict__ host, unsigned long long* __restrict__ ovf_count = nullptr,
+          CtrStripe* __restrict__ snap = nullptr) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
   if (ovf_count && threadIdx.x == 0) *ovf_count = 0;   // the next chunk's candidate overflow list starts empty
+  // the level's last chunk: the counters as the level leaves them, kept for
+  // a deferred-frontier redo from the next level (lane k copies stripe k)
+  if (snap) {
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&C->s[threadIdx.x]);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(&snap[threadIdx.x]);
+#pragma unroll 8
+    for (int k = 0; k < (int)(sizeof(CtrStripe) / 16); ++k) dst[k] = src[k];
+  }
   unsigned long long v = C->s[threadIdx.x].next_cand;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -93,6 +102,31 @@ __global__ void k_level_reset(Counters* __restrict__ C) {
 }
 
 const char* action_name(int a) { return (a >= 0 && a < A_COUNT) ? kActionNames[a] : "?"; }
+
+// Deferred-frontier redo from level X: every fingerprint claimed at a
+// successor level above X (inserted by level X or later) leaves the
+// ClaimSet.  Linear probing never moves an entry, so with no rehash since
+// level X began the table is then exactly what level X found.
+__global__ void k_claimset_drop(ClaimEntry* __restrict__ t, uint64_t nslots, uint32_t level) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) {
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+    if (e.x && ((~e.y) >> CLAIM_KEY_BITS) >= level)
+      *reinterpret_cast<ulonglong2*>(t + i) = make_ulonglong2(0ull, 0ull);
+  }
+}
+
+// The counters as a redo from level X needs them: every stripe as level
+// X - 1 left it (prev), except the per-action distinct counts, taken from
+// level X's snapshot (cur): on the deferred frontier a level's own states
+// are counted when its k_claim rebuilds them, which the exact path (it
+// counts them in the previous level's emit) will not do again.
+__global__ void __launch_bounds__(64)
+k_counters_restore(Counters* __restrict__ C, const CtrStripe* __restrict__ prev, const CtrStripe* __restrict__ cur) {
+  CtrStripe& d = C->s[threadIdx.x];
+  d = prev[threadIdx.x];
+#pragma unroll
+  for (int a = 0; a < A_COUNT; ++a) d.act_dist[a] = cur[threadIdx.x].act_dist[a];
+}
 
 // fingerprints of a ClaimSet into a dense array (order irrelevant: sorted next)
 __global__ void k_claimset_fps(const ClaimEntry* __restrict__ t, uint64_t nslots,
@@ -155,6 +189,8 @@ class EngineT final : public EngineBase {
     // successors per state (tests shrink it to force the exact-path redo)
     const char* dp = getenv("KC_DEFER_PC");
     pc_pass_ = !(dp && dp[0] == '0');
+    const char* dr = getenv("KC_DEFER_REDO");      // KC_DEFER_REDO=0: an anomaly redoes the run from Init
+    redo_on_ = !(dr && dr[0] == '0');
     const char* ds = getenv("KC_DEFER_SLACK");
     if (ds && atof(ds) > 0) defer_slack_ = atof(ds);
     if (defer_) tscan_ = true;    // the link emit takes the tile offsets
@@ -186,10 +222,14 @@ class EngineT final : public EngineBase {
     return 0;
   }
 
-  // A deferred-frontier run that meets anything but a clean level (an error
-  // of any kind, a capacity estimate too small) is redone on the exact,
-  // materialising path from Init: error reports and every count then come
-  // from the path that checks each new state where it is emitted.
+  // A deferred level that meets anything but a clean level (an error of any
+  // kind, a capacity estimate too small) is redone on the exact,
+  // materialising path from the level the anomaly belongs to (redo_from:
+  // the ClaimSet, the counters and the host state are put back as that
+  // level found them), so error reports and every count come from the path
+  // that checks each new state where it is emitted.  When that cannot be
+  // done exactly (a rehash since, KC_DEFER_REDO=0) the whole run is redone
+  // from Init on the exact path.
   int run(kc_result* res) override {
     defer_now_ = defer_;
     int rc = run_once(res);
@@ -198,6 +238,7 @@ class EngineT final : public EngineBase {
       defer_now_ = false;
       rc = run_once(res);
       res->defer_fallback = 1;
+      res->defer_redo_level = 1;
     }
     return rc;
   }
@@ -213,6 +254,10 @@ class EngineT final : public EngineBase {
     ev_used_ = 0;
     for (auto& c : klaunch_) c = 0;
     narrow_levels_ = 0;
+    exact_until_ = 0;
+    for (auto& v : snap_lv_) v = -1;
+    for (auto& h : hs_) h.level = -1;
+    for (auto& v : succ_lv_) v = -1;
     const auto t0 = std::chrono::steady_clock::now();
 
     // ---- Init (KubeAPI.tla:455-469), on the host: 2^NC states
@@ -270,6 +315,7 @@ class EngineT final : public EngineBase {
     hot_count_ = ni;
     KC_HIP_TRY(hipMemsetAsync(d_ctr_, 0, sizeof(Counters), st_));
     if (d_ovf_cnt_) KC_HIP_TRY(hipMemsetAsync(d_ovf_cnt_, 0, 8, st_));
+    if (defer_now_) KC_TRY(counter_snap(0));
     res->init = ni;
     res->generated = ni;
     res->distinct = ni;
@@ -324,6 +370,7 @@ class EngineT final : public EngineBase {
         if (!mat) {
           KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
           mat = true;
+          KC_TRY(counter_snap(level - 1));     // (k_materialize counted the states' actions)
         }
         pc_valid_ = false;
         int stop = cfg_.max_levels;
@@ -344,6 +391,7 @@ class EngineT final : public EngineBase {
         n = nr.n;
         cand = nr.cand;
         if (nr.levels) res->nlevels = n ? level : level - 1;
+        if (defer_now_ && nr.levels && nr.reason != NX_ERROR) KC_TRY(counter_snap(level - 1));
         if (nr.reason == NX_ERROR) {
           KC_TRY(report_error(res, h_ns_->err_key, level, level_gidx, n));
           finish(res, t0, 0);
@@ -360,7 +408,7 @@ class EngineT final : public EngineBase {
       // previous level) when the states are materialised; a deferred level's
       // is estimated, and a level past the estimate (DF_CAPACITY, a full
       // candidate list or table) is redone on the exact path
-      const bool dfr = defer_now_;
+      const bool dfr = defer_now_ && level > exact_until_;
       if (mat && n) ratio = std::max(1.0, (double)cand / (double)n);
       const uint64_t bound = mat ? cand
                                  : std::min<uint64_t>((uint64_t)((double)n * ratio * defer_slack_) + 4096,
@@ -400,6 +448,9 @@ class EngineT final : public EngineBase {
         if (cfg_.keep_trace) link_cap = std::min<uint64_t>(link_cap, std::min(par_cap_, ord_cap_) - next_gidx);
       }
       KC_TRY(grow_buffer(offsets_, off_cap_, std::min(n, chunk), false, st_));
+      if (defer_now_)      // (after this level's ClaimSet growth: a rehash later rules out a redo from here)
+        hs_[level % 3] = HostSnap{level, n, level_gidx, cand, prev_gidx, cs_.count, res->distinct,
+                                  res->peak_frontier, cand_total, cs_.nslots, res->nlevels, mat, ratio};
       const uint32_t succ_level = (uint32_t)level + 1;   // BFS level of the successors
       for (uint64_t start = 0, cn = 0; start < n; start += cn) {
         cn = std::min(chunk, n - start);
@@ -501,7 +552,8 @@ class EngineT final : public EngineBase {
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_,
                            tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)tiles,
                            last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr,
-                           claim_args_.ovf.count);
+                           claim_args_.ovf.count,
+                           last && defer_now_ && !headcopy_ ? d_snap_[level % 3].s : (CtrStripe*)nullptr);
       }
       KC_HIP_TRY(hipGetLastError());
       if (headcopy_) {
@@ -511,8 +563,21 @@ class EngineT final : public EngineBase {
       KC_HIP_TRY(hipStreamSynchronize(st_));
       collect_times();
       const Counters& c = *h_ctr_;
-      // a deferred level with anything to report: redo the run exactly
-      if (dfr && (c.overflow || c.batch_used || c.err_key != ~0ull || c.defer_flags)) return kDeferRetry;
+      // a deferred level with anything to report: redo exactly, from the level
+      // the anomaly belongs to
+      if (dfr && (c.overflow || c.batch_used || c.err_key != ~0ull || c.defer_flags)) {
+        // an invariant violation among the states this level rebuilt is
+        // the previous level's error (its emit would have found it); the
+        // rest (Assert / deadlock keys of this level's parents, a capacity
+        // estimate too small) are this level's
+        const int X = (c.defer_flags & DF_INVARIANT) ? level - 1 : level;
+        const uint64_t dc_here = c.cand_total - cand_total;
+        if (!redo_from(X, level, mat, dc_here, res, n, level_gidx, cand, prev_gidx, cand_total, ratio)) return kDeferRetry;
+        level = X;
+        mat = true;
+        pc_valid_ = false;
+        continue;
+      }
       if (c.overflow || c.batch_used) {
         set_error("kubecheck: state with more than %d successors or full table", M::MAXSUCC);
         return -ENOMEM;
@@ -539,6 +604,11 @@ class EngineT final : public EngineBase {
       // or this level's own (a deferred k_claim)
       const uint64_t dc = c.cand_total - cand_total;
       cand_total = c.cand_total;
+      if (defer_now_) {              // this level's counters (k_advance) and successor count, for a redo
+        if (!headcopy_) snap_lv_[level % 3] = level;
+        succ_[level % 3] = mat ? cand : dc;
+        succ_lv_[level % 3] = level;
+      }
       if (dfr) {
         if (!mat && n) ratio = std::max(1.0, (double)dc / (double)n);
         cand = 0;
@@ -562,6 +632,7 @@ class EngineT final : public EngineBase {
       if (dfr && capture_level_ == level && n) {
         KC_TRY(materialize(n, level_gidx, prev_gidx, cand, cand_total));
         mat = true;
+        KC_TRY(counter_snap(level - 1));
         captured_.resize(n);
         KC_HIP_TRY(hipMemcpy(captured_.data(), cur_, n * sizeof(State), hipMemcpyDeviceToHost));
       }
@@ -846,6 +917,7 @@ class EngineT final : public EngineBase {
     res->batch_inserts = h_ctr_->settles();
     res->cand_overflow_records = h_ctr_->cand_ovf();
     res->cand_buffer_peak_bytes = cand_buf_peak_;
+    res->narrow_levels = narrow_levels_;
     if (spill_) {
       ColdStats cst;
       cold_.stats(&cst);
@@ -907,6 +979,7 @@ class EngineT final : public EngineBase {
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_last_) (void)hipHostFree(h_last_);
     if (d_ns_) (void)hipFree(d_ns_);
+    if (d_snap_) (void)hipFree(d_snap_);
     if (d_nsc_) (void)hipFree(d_nsc_);
     if (d_ntrace_) (void)hipFree(d_ntrace_);
     if (h_ns_) (void)hipHostFree(h_ns_);
@@ -1084,6 +1157,79 @@ class EngineT final : public EngineBase {
   bool defer_ = false, defer_now_ = false;
   double defer_slack_ = 1.25;
   uint64_t defer_fallbacks_ = 0;
+  // deferred-frontier redo from a level (redo_from): per level mod 3, the
+  // counters as the level left them (k_advance), the host state as it began
+  // and its states' successor count
+  struct HostSnap {
+    int level = -1;
+    uint64_t n = 0, level_gidx = 0, cand = 0, prev_gidx = 0, cs_count = 0, distinct = 0, peak = 0, cand_total = 0,
+             nslots = 0;
+    int nlevels = 0;
+    bool mat = true;
+    double ratio = 1.0;
+  };
+  Counters* d_snap_ = nullptr;        // [3]
+  int snap_lv_[3] = {-1, -1, -1};
+  HostSnap hs_[3];
+  uint64_t succ_[3] = {0, 0, 0};
+  int succ_lv_[3] = {-1, -1, -1};
+  int exact_until_ = 0;               // levels <= this run on the exact path (after a redo)
+  bool redo_on_ = true;               // KC_DEFER_REDO=0: an anomaly redoes the run from Init
+
+  // The counters after level `lv` (end of a narrow run, or the start) into
+  // snapshot lv mod 3.
+  int counter_snap(int lv) {
+    if (!d_snap_) KC_HIP_TRY(hipMalloc(&d_snap_, 3 * sizeof(Counters)));
+    KC_HIP_TRY(hipMemcpyAsync(d_snap_[lv % 3].s, d_ctr_->s, sizeof(d_ctr_->s), hipMemcpyDeviceToDevice, st_));
+    snap_lv_[lv % 3] = lv;
+    return 0;
+  }
+  // Put the run back as level X found it (L = the level that met the
+  // anomaly, X = L or L - 1): ClaimSet entries of levels > X dropped,
+  // counters of level X - 1 restored (k_counters_restore), the host state of X's start; X's
+  // states are cur_ (X = L: k_claim rebuilt or had them) or next_ (X = L -
+  // 1: the previous frontier).  Levels <= L then run exactly.  False: not
+  // possible exactly (the caller redoes the run from Init).
+  bool redo_from(int X, int L, bool mat, uint64_t dc_here, kc_result* res, uint64_t& n, uint64_t& level_gidx,
+                 uint64_t& cand, uint64_t& prev_gidx, uint64_t& cand_total, double& ratio) {
+    if (!redo_on_ || X < 1 || !d_snap_ || snap_lv_[(X - 1) % 3] != X - 1 || hs_[X % 3].level != X) return false;
+    // level X's own snapshot: X = L - 1 completed; X = L's k_advance wrote it (the anomaly is seen after)
+    if (X != L && snap_lv_[X % 3] != X) return false;
+    if (X == L && headcopy_) return false;
+    const HostSnap& h = hs_[X % 3];
+    if (h.nslots != cs_.nslots) return false;      // rehashed since: dropping entries would break probe chains
+    uint64_t c;
+    if (X == L) {
+      c = mat ? cand : dc_here;                    // k_claim rebuilt the states into cur_ and counted them
+    } else {
+      if (mat || succ_lv_[X % 3] != X) return false;   // (X's states are the previous frontier, next_)
+      c = succ_[X % 3];
+    }
+    const unsigned grid = (unsigned)std::min<uint64_t>(8192, (cs_.nslots + 255) / 256);
+    hipLaunchKernelGGL(k_claimset_drop, dim3(grid), dim3(256), 0, st_, cs_.t, cs_.nslots, (uint32_t)X + 1);
+    hipLaunchKernelGGL(k_counters_restore, dim3(1), dim3(64), 0, st_, d_ctr_, d_snap_[(X - 1) % 3].s, d_snap_[X % 3].s);
+    hipLaunchKernelGGL(k_level_reset, dim3(1), dim3(64), 0, st_, d_ctr_);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st_) != hipSuccess) return false;
+    if (X != L) {
+      std::swap(cur_, next_);
+      std::swap(cur_cap_, next_cap_);
+    }
+    n = h.n;
+    level_gidx = h.level_gidx;
+    cand = c;
+    prev_gidx = h.prev_gidx;
+    cand_total = h.cand_total;
+    ratio = h.ratio;
+    cs_.count = h.cs_count;
+    res->distinct = h.distinct;
+    res->peak_frontier = h.peak;
+    res->nlevels = h.nlevels;
+    exact_until_ = L;
+    res->defer_fallback = 1;
+    res->defer_redo_level = (uint64_t)X;
+    ++defer_fallbacks_;
+    return true;
+  }
 
   // ---- seen-set spill (cfg.seen_hbm_bytes > 0; engine_spill.h, coldset.h).
   // HBM budget B: the hot ClaimSet takes the largest power-of-two table of

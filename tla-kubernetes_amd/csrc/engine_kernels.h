@@ -565,13 +565,20 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   if (live) {
 #define KC_LP (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x)
+    // KC_LOCATE_SWAR: the slot lookup from cumulative counts (its top byte
+    // keeps the dealt parent's index)
+    constexpr bool SWAR = KC_LOCATE_SWAR && M::CUM_OK;
+    if (SWAR) counts = M::plan_cum(counts);
     const typename M::Plan pl{counts, tot, -1, -1};
     uint64_t acc = fold ^ counts;
     // (walking (slot, j) along with t instead of locate() measured slower:
     // its three live registers spill at k_claim's 80-VGPR budget; r03w)
     for (int t = 0; t < tot; ++t) {
       int slot, j;
-      M::locate(pl, t, slot, j);
+      if (SWAR)
+        M::locate_cum(counts, t, slot, j);
+      else
+        M::locate(pl, t, slot, j);
       typename M::State x;
       int who;
       M::apply(s, slot, j, f, x, who);

@@ -37,6 +37,16 @@
 #define KC_HD inline
 #endif
 
+// A/B build switches of the successor loop (k_claim): the single-GPU
+// fingerprint's top bits from the fold (no owner projection), and slot
+// lookup by byte-parallel compares of cumulative counts (locate_cum)
+#ifndef KC_OWN0_FOLD
+#define KC_OWN0_FOLD 0
+#endif
+#ifndef KC_LOCATE_SWAR
+#define KC_LOCATE_SWAR 0
+#endif
+
 namespace kc {
 
 // ---------------------------------------------------------------- labels
@@ -419,6 +429,29 @@ struct Model {
     });
     return pl;
   }
+  // The same lookup without a loop: cum holds the cumulative slot ends
+  // E_i = c_0 + ... + c_i one per byte (plan_cum; NSLOT <= 7, the top byte
+  // is the caller's), and slot = #{i : E_i <= t}, counted with byte-wise
+  // subtractions (t | 0x80) - E_i (no borrow: E_i <= 32) and a popcount.
+  static constexpr bool CUM_OK = NSLOT <= 7;
+  KC_HD static uint64_t plan_cum(uint64_t counts) {
+    uint64_t cum = counts & 0xff00000000000000ull;
+    uint32_t e = 0;
+    static_for<(NSLOT < 7 ? NSLOT : 7)>([&](auto SI) {
+      e += (uint32_t)((counts >> (6 * (int)SI)) & 63);
+      cum |= (uint64_t)e << (8 * (int)SI);
+    });
+    return cum;
+  }
+  KC_HD static void locate_cum(uint64_t cum, int t, int& slot, int& j) {
+    constexpr uint64_t G = (NSLOT >= 7 ? 0x0080808080808080ull : ((1ull << (8 * NSLOT)) - 1) & 0x8080808080808080ull);
+    const uint32_t tb = (uint32_t)t * 0x01010101u;
+    const uint64_t T = ((uint64_t)tb << 32) | tb;
+    const uint64_t D = ((T | G) - (cum & (G >> 1 | G >> 2 | G >> 3 | G >> 4 | G >> 5 | G >> 6 | G >> 7))) & G;
+    slot = popc(D);
+    j = t - (int)(((cum << 8) >> (8 * slot)) & 0xff);
+  }
+
   // successor t of a plan -> (slot, index within slot)
   KC_HD static void locate(const Plan& pl, int t, int& slot, int& j) {
     int s = 0;
@@ -752,8 +785,19 @@ struct Model {
     h = (h & ((1ull << (63 - OWNER_BITS)) - 1)) | (ob << (63 - OWNER_BITS));
     return h ? h : 1;
   }
+  // KC_OWN0_FOLD (A/B build switch): OWN = 0 takes its top bits from the
+  // fold itself, i.e. no owner projection at all (one GPU has no owners)
   template <int OWN = 0>
-  KC_HD static uint64_t fp_final(uint64_t h, const State& x) { return fp_final_ob(h, owner_bits<OWN>(x)); }
+  KC_HD static uint64_t fp_final(uint64_t h, const State& x) {
+#if KC_OWN0_FOLD
+    if constexpr (OWN == 0) {
+      (void)x;
+      h &= 0x7fffffffffffffffull;
+      return h ? h : 1;
+    }
+#endif
+    return fp_final_ob(h, owner_bits<OWN>(x));
+  }
   template <int OWN = 0>
   KC_HD static uint64_t fingerprint(const State& s) { return fp_final<OWN>(fp_fold(s), s); }
 

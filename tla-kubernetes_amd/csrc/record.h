@@ -33,6 +33,9 @@ namespace rec {
 template <int RW, int POS, int N>
 KC_HD void put(uint64_t (&r)[RW], uint64_t v) {
   constexpr int wd = POS / 64, off = POS % 64;
+  // (a field never carries bits past its width in a canonical state; masked
+  // anyway, so a stray bit cannot overwrite the next field of the record)
+  if constexpr (N < 64) v &= (1ull << N) - 1;
   r[wd] |= v << off;
   if constexpr (off + N > 64) r[wd + 1] |= v >> (64 - off);
 }

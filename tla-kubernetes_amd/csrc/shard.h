@@ -50,6 +50,29 @@ class ShardBase {
   virtual int replay(int init_idx, const std::vector<int>& ords, int kind, int pos,
                      std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
                      int* err_inv) = 0;
+
+  // ---- device-driven narrow levels (shard_narrow.h), driven by the native
+  // loop: sn_setup once (the control block, scratch and the fixed exchange
+  // slots: world x (slot_cap + 1) records each way), then per batch
+  // sn_begin, per level sn_pre (expand, send, pack), the caller's fixed
+  // exchange of the slots, sn_post (receive, claim, scan, emit), and
+  // sn_end (one host sync; the levels the batch ran).
+  struct SNOut {
+    int levels = 0;                 // levels run (the same on every rank)
+    int reason = 0;                 // SNReason (0: every level of the batch ran)
+    std::vector<uint64_t> widths;   // global width of each level run
+    uint64_t status_new = 0;        // this rank's width of the next level
+    uint64_t status_err = ~0ull;    // the previous level's errors (the counted loop's status_err)
+    uint64_t sent = 0;              // records this rank sent to other ranks in the levels run
+  };
+  virtual int sn_setup(uint32_t slot_cap) = 0;
+  virtual uint64_t sn_slot_bytes() const = 0;
+  virtual void* sn_send() = 0;
+  virtual void* sn_recv() = 0;
+  virtual int sn_begin(uint64_t status_new, uint64_t status_err, int batch) = 0;
+  virtual int sn_pre(uint32_t lev, bool fail) = 0;
+  virtual int sn_post(uint32_t lev) = 0;
+  virtual int sn_end(SNOut* out) = 0;
 };
 
 // One transfer of a rank's all-to-all (shard_driver.hip exchange_plan).

@@ -40,6 +40,7 @@
 #include "kc_common.h"
 #include "record.h"
 #include "shard.h"
+#include "shard_narrow.h"
 
 namespace kc {
 
@@ -813,6 +814,123 @@ class ShardT final : public ShardBase {
     return 0;
   }
 
+  // ---- device-driven narrow levels (shard_narrow.h)
+  int sn_setup(uint32_t cap) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    sn_cap_ = std::max<uint32_t>(1, std::min<uint32_t>(cap, SN_SLOT_MAX));
+    KC_HIP_TRY(hipMalloc(&d_snc_, sizeof(SNCtl)));
+    KC_HIP_TRY(hipHostMalloc(&h_snc_, sizeof(SNCtl)));
+    KC_HIP_TRY(hipMalloc(&d_sns_, sizeof(SNScratch)));
+    KC_HIP_TRY(hipMalloc(&sn_send_, (uint64_t)world_ * sn_slot_bytes()));
+    KC_HIP_TRY(hipMalloc(&sn_recv_, (uint64_t)world_ * sn_slot_bytes()));
+    KC_HIP_TRY(hipMemset(d_snc_, 0, sizeof(SNCtl)));
+    KC_HIP_TRY(hipMemset(sn_send_, 0, (uint64_t)world_ * sn_slot_bytes()));
+    KC_HIP_TRY(hipMemset(sn_recv_, 0, (uint64_t)world_ * sn_slot_bytes()));
+    return 0;
+  }
+  uint64_t sn_slot_bytes() const override { return (uint64_t)(sn_cap_ + 1) * sizeof(Rec); }
+  void* sn_send() override { return sn_send_; }
+  void* sn_recv() override { return sn_recv_; }
+
+  // A batch's control block.  It is written whatever happens: when a buffer
+  // cannot be grown the block says "failed", so this rank's next level stops
+  // every rank (through its headers) instead of running on short buffers.
+  int sn_begin(uint64_t status_new, uint64_t status_err, int batch) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    int rc = 0;
+    if (status_new != n_) {
+      set_error("kc_shard narrow: status %llu is not the frontier's width %llu", (unsigned long long)status_new,
+                (unsigned long long)n_);
+      rc = -EIO;
+    }
+    const uint64_t in = (uint64_t)(world_ - 1) * sn_cap_;
+    const uint64_t per = SN_CAND_MAX + in + 1;           // new states one level may add, at most
+    const uint64_t bufs = std::max<uint64_t>(SN_MAX, per);
+    const uint64_t base = level_base_.back();
+    if (!rc) rc = grow_buffer(cur_, cur_cap_, bufs, true, st_);
+    if (!rc) rc = grow_buffer(next_, next_cap_, bufs, false, st_);
+    if (!rc) rc = grow_buffer(pkeys_, pk_cap_, base + n_ + (uint64_t)batch * per + 1, true, st_);
+    if (!rc) rc = cs_.reserve((uint64_t)batch * per, st_);
+    SNCtl& h = *h_snc_;
+    memset(&h, 0, offsetof(SNCtl, lwidths));
+    h.active = 1;
+    h.level = (uint32_t)level_;
+    h.world = (uint32_t)world_;
+    h.rank = (uint32_t)rank_;
+    h.slot_cap = sn_cap_;
+    h.stop_level = (uint32_t)cfg_.max_levels;
+    h.n = n_;
+    h.level_gidx = base;
+    h.cand = cand_;
+    h.err[(level_ - 1) & 1] = status_err;
+    h.err[level_ & 1] = ~0ull;
+    if (rc) {
+      h.fail = 1;           // (buf_cap = room = par_cap = 0: nothing runs)
+    } else {
+      h.room = cs_.capacity() / 2 > cs_.count ? cs_.capacity() / 2 - cs_.count : 0;
+      h.buf_cap = std::min(cur_cap_, next_cap_);
+      h.par_cap = pk_cap_;
+    }
+    sn_n0_ = n_;
+    KC_HIP_TRY(hipMemcpyAsync(d_snc_, h_snc_, offsetof(SNCtl, lwidths), hipMemcpyHostToDevice, st_));
+    KC_HIP_TRY(hipMemsetAsync(d_sns_->lt, 0, sizeof(d_sns_->lt), st_));
+    return rc;
+  }
+  int sn_pre(uint32_t lev, bool fail) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    if (fail) hipLaunchKernelGGL(k_sn_fail, dim3(1), dim3(64), 0, st_, d_snc_);
+    hipLaunchKernelGGL(k_sn_expand<M>, dim3(SN_XWG), dim3(SN_THREADS), 0, st_, cur_, next_, flags_,
+                       cfg_.check_deadlock, lev, d_snc_, d_sns_);
+    if (world_ > 1)
+      hipLaunchKernelGGL(k_sn_pack<M>, dim3(SN_PWG), dim3(SN_THREADS), 0, st_, cur_, next_, flags_, lev, d_snc_,
+                         d_sns_, sn_send_);
+    KC_HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  int sn_post(uint32_t lev) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    const unsigned rgrid = world_ > 1 ? (unsigned)(((uint64_t)world_ * sn_cap_ + SN_THREADS - 1) / SN_THREADS) : 0u;
+    if (world_ > 1)
+      hipLaunchKernelGGL(k_sn_recv<M>, dim3(rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_, d_ctr_);
+    hipLaunchKernelGGL(k_sn_claim<M>, dim3(SN_CWG + rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_,
+                       cs_.t, cs_.nslots, d_ctr_);
+    hipLaunchKernelGGL(k_sn_emit<M>, dim3(SN_PWG + rgrid), dim3(SN_THREADS), 0, st_, cur_, next_, flags_, lev, d_snc_,
+                       d_sns_, sn_recv_, pkeys_, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  int sn_end(SNOut* out) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    KC_HIP_TRY(hipMemcpyAsync(h_snc_, d_snc_, sizeof(SNCtl), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const SNCtl& h = *h_snc_;
+    if (h_ctr_->overflow) {
+      set_error("kc_shard narrow: a full level table or ClaimSet, or a header of another level");
+      return -ENOMEM;
+    }
+    out->levels = (int)h.levels;
+    out->reason = h.active ? SN_RUN : h.reason;
+    out->widths.assign(h.gwidths, h.gwidths + std::min<uint32_t>(h.levels, KC_MAX_LEVELS));
+    uint64_t w = sn_n0_;
+    for (uint32_t k = 0; k < h.levels; ++k) {
+      level_base_.push_back(level_base_.back() + w);
+      w = k < (uint32_t)KC_MAX_LEVELS ? h.lwidths[k] : 0;
+    }
+    cs_.count += h.new_total;
+    level_ = (int)h.level;
+    n_ = h.n;
+    cand_ = h.cand;
+    if (h.levels & 1) {
+      std::swap(cur_, next_);
+      std::swap(cur_cap_, next_cap_);
+    }
+    out->status_new = n_;
+    out->status_err = h.err[(h.level - 1) & 1];
+    out->sent = h.sent_total;
+    return 0;
+  }
+
   int advance() override {
     level_base_.push_back(level_base_.back() + n_);
     std::swap(cur_, next_);
@@ -873,6 +991,9 @@ class ShardT final : public ShardBase {
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_owner_base_) (void)hipHostFree(h_owner_base_);
+    for (void* p : {(void*)d_snc_, (void*)d_sns_, (void*)sn_send_, (void*)sn_recv_})
+      if (p) (void)hipFree(p);
+    if (h_snc_) (void)hipHostFree(h_snc_);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
     if (st_ && own_st_) (void)hipStreamDestroy(st_);
@@ -921,6 +1042,12 @@ class ShardT final : public ShardBase {
   std::vector<uint64_t> level_base_;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   bool async_pack_ = false;
+  // device-driven narrow levels
+  SNCtl *d_snc_ = nullptr, *h_snc_ = nullptr;
+  SNScratch* d_sns_ = nullptr;
+  uint64_t *sn_send_ = nullptr, *sn_recv_ = nullptr;
+  uint32_t sn_cap_ = SN_SLOT_DEFAULT;
+  uint64_t sn_n0_ = 0;
   double claim_ms_ = 0;
   uint64_t claim_launches_ = 0, claim_parents_ = 0;
 };

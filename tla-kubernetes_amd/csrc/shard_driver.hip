@@ -40,6 +40,7 @@
 #include "engine_util.h"
 #include "kc_common.h"
 #include "shard.h"
+#include "shard_narrow.h"
 
 namespace kc {
 
@@ -183,6 +184,11 @@ class Comm {
     set_error("all_gather_dev: not supported by this communicator");
     return -EINVAL;
   }
+  // The narrow levels' fixed exchange (shard_narrow.h): slot p of local
+  // shard i's send buffer goes to rank p's receive buffer, at slot (rank
+  // of i); every slot is slot_bytes.  The same transfers every level,
+  // whatever the ranks' device state, so they always match.
+  virtual int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot_bytes) = 0;
 };
 
 class LocalComm final : public Comm {
@@ -257,6 +263,18 @@ class LocalComm final : public Comm {
       }
     }
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
+    return 0;
+  }
+  int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot) override {
+    const int R = (int)s_.size();
+    if (R == 1) return 0;
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every rank's slots are written
+    for (int d = 0; d < R; ++d)
+      for (int src = 0; src < R; ++src)
+        if (src != d)
+          KC_HIP_TRY(hipMemcpyAsync((char*)recv[d] + src * slot, (const char*)send[src] + d * slot, slot,
+                                    hipMemcpyDeviceToDevice, s_[d]->stream()));
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // (before any rank's next pack)
     return 0;
   }
   int broadcast(int, uint64_t*) override { return 0; }   // the driver read it from the local root
@@ -347,6 +365,22 @@ class RcclComm final : public Comm {
     }
     KC_NCCL_TRY(rccl()->group_end());
     return 0;                                          // stream-ordered before insert
+  }
+  // enqueued on the shard's stream between its pack and its receive kernels:
+  // no host synchronisation
+  int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot) override {
+    const int R = s_->world(), me = s_->rank();
+    if (R == 1) return 0;
+    const uint64_t w = slot / 8;
+    hipStream_t st = s_->stream();
+    KC_NCCL_TRY(rccl()->group_start());
+    for (int p = 0; p < R; ++p) {
+      if (p == me) continue;
+      KC_NCCL_TRY(rccl()->send((const uint64_t*)send[0] + p * w, w, ncclUint64, p, comm_, st));
+      KC_NCCL_TRY(rccl()->recv((uint64_t*)recv[0] + p * w, w, ncclUint64, p, comm_, st));
+    }
+    KC_NCCL_TRY(rccl()->group_end());
+    return 0;
   }
   int broadcast(int root, uint64_t* v) override {
     if (trivial_) return 0;
@@ -466,6 +500,29 @@ class HostComm final : public Comm {
     if (nr) KC_HIP_TRY(hipMemcpyAsync(recv[0], hrecv_, nr * rb, hipMemcpyHostToDevice, st));
     return 0;                                        // stream-ordered before insert
   }
+  // synchronous: the caller's transport works on host buffers
+  int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot) override {
+    const int R = s_->world(), me = s_->rank();
+    if (R == 1) return 0;
+    KC_TRY(pinned(hsend_, hsend_cap_, R * slot));
+    KC_TRY(pinned(hrecv_, hrecv_cap_, R * slot));
+    hipStream_t st = s_->stream();
+    KC_HIP_TRY(hipMemcpyAsync(hsend_, send[0], R * slot, hipMemcpyDeviceToHost, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint64_t> xf;
+    for (int p = 0; p < R; ++p) {
+      if (p == me) continue;
+      for (uint64_t dir : {1ull, 0ull}) {
+        xf.push_back((uint64_t)p);
+        xf.push_back(dir);
+        xf.push_back(p * slot);
+        xf.push_back(slot);
+      }
+    }
+    KC_TRY(call(ops_.exchange(ops_.ctx, xf.data(), (int)(xf.size() / 4), hsend_, hrecv_), "exchange"));
+    KC_HIP_TRY(hipMemcpyAsync(recv[0], hrecv_, R * slot, hipMemcpyHostToDevice, st));
+    return 0;
+  }
   int broadcast(int root, uint64_t* v) override { return call(ops_.broadcast(ops_.ctx, root, v), "broadcast"); }
   int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
     out = v[0];
@@ -538,6 +595,19 @@ class Group {
     recv_.assign(local_.size(), nullptr);
     send_cap_.assign(local_.size(), 0);
     recv_cap_.assign(local_.size(), 0);
+    // device-driven narrow levels (shard_narrow.h); KC_SNARROW=0: every level
+    // on the counted path; KC_SN_SLOT: records per peer slot
+    const char* sn = getenv("KC_SNARROW");
+    sn_on_ = !(sn && sn[0] == '0');
+    const char* sc = getenv("KC_SN_SLOT");
+    sn_cap_ = sc && atoi(sc) > 0 ? (uint32_t)atoi(sc) : SN_SLOT_DEFAULT;
+  }
+  // The narrow levels' buffers, allocated with the group (a failure here is
+  // the caller's before any collective of a run).
+  int setup() {
+    if (!sn_on_) return 0;
+    for (auto* s : local_) KC_TRY(s->sn_setup(sn_cap_));
+    return 0;
   }
   ~Group() {
     if (h_fail_) (void)hipHostFree(h_fail_);
@@ -600,9 +670,12 @@ class Group {
   std::vector<std::vector<uint64_t>> trace_;
   std::vector<uint64_t> sent_local_;   // records each local shard sent to other ranks
   uint64_t sent_ = 0;                  // all ranks (after run)
+  uint64_t sn_levels_ = 0;             // levels run narrow (this run)
   bool dev_row_off_ = false;
   uint64_t* h_fail_ = nullptr;         // pinned: failure words copied into device rows
   int fault_rank_ = -1, fault_level_ = 0, fault_stage_ = 0;
+  bool sn_on_ = true;
+  uint32_t sn_cap_ = SN_SLOT_DEFAULT;
 };
 
 // Failure handling: no rank may leave the loop alone, or its peers would
@@ -621,6 +694,7 @@ int Group::run(kc_result* res) {
   res->err_action = res->err_self = res->err_invariant = -1;
   trace_.clear();
   sent_ = 0;
+  sn_levels_ = 0;
   sent_local_.assign(local_.size(), 0);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t nl = local_.size();
@@ -656,8 +730,82 @@ int Group::run(kc_result* res) {
   std::vector<std::vector<uint64_t>> counts(nl, std::vector<uint64_t>(R, 0)), rows(nl);
   std::vector<uint64_t> all;
   std::vector<std::vector<uint64_t>> Mx(R, std::vector<uint64_t>(R, 0));
+  // narrow batches: run while they complete; after one stopped at a level
+  // too wide (SN_STOP) the counted path takes over until the frontier
+  // shrinks again.  Batches grow 8 -> 32 levels while they complete (a
+  // batch's levels past the one that stopped it still exchange their slots).
+  bool sn_blocked = false;
+  int sn_batch = 8;
+  uint64_t prev_total = ~0ull;
+  std::vector<ShardBase::SNOut> so(nl);
   for (;;) {
     const bool last = cfg_.max_levels && level >= cfg_.max_levels;
+    if (sn_on_ && !last && !sn_blocked) {
+      const uint64_t slot = local_[0]->sn_slot_bytes();
+      for (size_t i = 0; i < nl; ++i) {
+        so[i] = ShardBase::SNOut{};
+        if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
+        // (a failed begin still leaves a control block that stops the batch)
+        note(i, local_[i]->sn_begin(status_new[i], status_err[i], sn_batch));
+      }
+      std::vector<void*> ss(nl), rr(nl);
+      for (size_t i = 0; i < nl; ++i) {
+        ss[i] = local_[i]->sn_send();
+        rr[i] = local_[i]->sn_recv();
+      }
+      for (int k = 0; k < sn_batch; ++k) {
+        for (size_t i = 0; i < nl; ++i) {
+          // a failed rank marks its control block: the level stops every rank
+          bool f = k == 0 && fail[i];
+          if (!fail[i] && local_[i]->rank() == fault_rank_ && level + k == fault_level_) {
+            set_error("kc_group_run: injected fault (KC_FAULT) on rank %d at level %d, narrow", fault_rank_,
+                      level + k);
+            note(i, -EIO);
+            f = true;
+          }
+          note(i, local_[i]->sn_pre((uint32_t)k, f));
+        }
+        KC_TRY(comm_->sn_exchange(ss, rr, slot));
+        for (size_t i = 0; i < nl; ++i) note(i, local_[i]->sn_post((uint32_t)k));
+      }
+      const ShardBase::SNOut* g = nullptr;
+      for (size_t i = 0; i < nl; ++i) {
+        const bool pre = fail[i] != 0;
+        note(i, local_[i]->sn_end(&so[i]));
+        if (!pre && !fail[i]) {
+          if (g && (g->levels != so[i].levels || g->reason != so[i].reason)) {
+            set_error("kc_group_run: narrow levels disagree between ranks (%d vs %d)", g->levels, so[i].levels);
+            return -EIO;
+          }
+          g = &so[i];
+          sent_local_[i] += so[i].sent;
+          status_new[i] = so[i].status_new;
+          status_err[i] = so[i].status_err;
+        }
+      }
+      bool any_fail = false;
+      for (size_t i = 0; i < nl; ++i) any_fail |= fail[i] != 0;
+      if (g) {
+        for (uint64_t w : g->widths) {
+          if ((int)widths.size() >= KC_MAX_LEVELS) {
+            set_error("kc_group_run: more than %d levels", KC_MAX_LEVELS);
+            return -ENOMEM;
+          }
+          widths.push_back(w);
+        }
+        level += g->levels;
+        sn_levels_ += (uint64_t)g->levels;
+        if (g->reason == SN_RUN && !any_fail) {
+          sn_batch = std::min(2 * sn_batch, SN_BATCH);
+          continue;                   // the next batch
+        }
+        if (g->reason == SN_STOP) sn_blocked = true;
+      }
+      sn_batch = 8;
+      // SN_STOP, SN_ERROR, SN_DONE or a failure: this level runs on the
+      // counted path, whose all-gather reports the error, the end or the
+      // failure as it always does
+    }
     // device rows (every local shard's kernels write its all-gather row, so
     // the gather's sync is the level's first: expand has none of its own)
     std::vector<uint64_t*> d_rows(nl, nullptr);
@@ -727,6 +875,9 @@ int Group::run(kc_result* res) {
       break;
     }
     widths.push_back(total);
+    // back to the narrow levels once the frontier shrinks well below their limit
+    if (sn_blocked && total * 4 <= (uint64_t)R * SN_MAX && total < prev_total) sn_blocked = false;
+    prev_total = total;
     if (last) break;
     std::vector<char> sunk(nl, 0);
     for (size_t i = 0; i < nl; ++i) {
@@ -804,6 +955,7 @@ int Group::run(kc_result* res) {
   sent_ = tot[2 * KC_NACTIONS + 3];
   res->nlevels = (int)widths.size();
   res->depth = res->nlevels;
+  res->narrow_levels = sn_levels_;
   for (size_t k = 0; k < widths.size(); ++k) res->level_width[k] = widths[k];
   res->complete = err == NONE && !(cfg_.max_levels && level >= cfg_.max_levels);
   if (err != NONE) KC_TRY(error_trace(err, level, res));
@@ -898,7 +1050,9 @@ int kc_group_create_rccl(kc_shard* s, const uint8_t* id, kc_group** out) {
   KC_NCCL_TRY(api->comm_init_rank(&comm, sh->world(), uid, sh->rank()));
   std::unique_ptr<RcclComm> rc(new RcclComm(sh, comm));
   KC_TRY(rc->make_sink());
-  *out = new kc_group{std::unique_ptr<Group>(new Group({sh}, std::move(rc), sh->config()))};
+  std::unique_ptr<Group> g(new Group({sh}, std::move(rc), sh->config()));
+  KC_TRY(g->setup());
+  *out = new kc_group{std::move(g)};
   return 0;
 }
 
@@ -911,8 +1065,9 @@ int kc_group_create_host(kc_shard* s, const kc_host_comm* comm, kc_group** out) 
   }
   ShardBase* sh = s->impl.get();
   KC_HIP_TRY(hipSetDevice(sh->device()));
-  *out = new kc_group{std::unique_ptr<Group>(
-      new Group({sh}, std::unique_ptr<Comm>(new HostComm(sh, *comm)), sh->config()))};
+  std::unique_ptr<Group> g(new Group({sh}, std::unique_ptr<Comm>(new HostComm(sh, *comm)), sh->config()));
+  KC_TRY(g->setup());
+  *out = new kc_group{std::move(g)};
   return 0;
 }
 
@@ -929,8 +1084,9 @@ int kc_group_create_local(kc_shard** shards, int nshards, kc_group** out) {
     }
     v.push_back(sh);
   }
-  *out = new kc_group{std::unique_ptr<Group>(
-      new Group(v, std::unique_ptr<Comm>(new LocalComm(v)), v[0]->config()))};
+  std::unique_ptr<Group> g(new Group(v, std::unique_ptr<Comm>(new LocalComm(v)), v[0]->config()));
+  KC_TRY(g->setup());
+  *out = new kc_group{std::move(g)};
   return 0;
 }
 

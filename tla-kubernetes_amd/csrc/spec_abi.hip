@@ -251,9 +251,18 @@ int kc_spec_fp_selfcheck(const kc_model_config* cfg, const uint64_t* tuple) {
     const typename M::Plan pl = M::plan(s, f);
     const uint64_t fold = M::fp_fold(s);
     int bad = 0;
+    // the loop-free slot lookup (KC_LOCATE_SWAR) agrees with locate(), the
+    // top byte (the dealt parent's index in k_claim) left alone
+    const uint64_t cum = M::CUM_OK ? M::plan_cum(pl.counts | (0xa5ull << 56)) : 0;
+    if (M::CUM_OK && (cum >> 56) != 0xa5) ++bad;
     for (int t = 0; t < pl.total; ++t) {
       int slot, j, who;
       M::locate(pl, t, slot, j);
+      if (M::CUM_OK) {
+        int s2, j2;
+        M::locate_cum(cum, t, s2, j2);
+        bad += (s2 != slot) + (j2 != j);
+      }
       typename M::State x;
       M::apply(s, slot, j, f, x, who);
       if (M::fingerprint_succ(s, fold, x, who) != M::fingerprint(x)) ++bad;

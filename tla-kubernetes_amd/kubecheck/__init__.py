@@ -115,6 +115,8 @@ class CheckResult:
     cand_buffer_peak_bytes: int = 0
     deferred_states: int = 0       # frontier states rebuilt inside k_claim (deferred frontier)
     defer_fallback: bool = False   # the run was redone on the materialising path
+    defer_redo_level: int = 0      # ... starting from this level (1 = Init; 0 = no redo)
+    narrow_levels: int = 0         # levels run by the device-driven narrow kernel
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
@@ -143,7 +145,8 @@ def _result(r: KcResult) -> CheckResult:
         frontier_peak_hbm_bytes=r.frontier_peak_hbm_bytes,
         seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")},
         cand_overflow_records=r.cand_overflow_records, cand_buffer_peak_bytes=r.cand_buffer_peak_bytes,
-        deferred_states=r.deferred_states, defer_fallback=bool(r.defer_fallback))
+        deferred_states=r.deferred_states, defer_fallback=bool(r.defer_fallback),
+        defer_redo_level=int(r.defer_redo_level), narrow_levels=int(r.narrow_levels))
 
 
 class ModelChecker:

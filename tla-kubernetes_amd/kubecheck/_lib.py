@@ -60,6 +60,7 @@ class KcResult(C.Structure):
         ("seen_flush_seconds", C.c_double), ("seen_merge_seconds", C.c_double), ("seen_check_seconds", C.c_double),
         ("cand_overflow_records", C.c_uint64), ("cand_buffer_peak_bytes", C.c_uint64),
         ("deferred_states", C.c_uint64), ("defer_fallback", C.c_uint64),
+        ("defer_redo_level", C.c_uint64), ("narrow_levels", C.c_uint64),
     ]
 
 

@@ -281,6 +281,7 @@ class NativeShardedChecker:
             "act_gen": {a: int(r.act_gen[i]) for i, a in enumerate(ACTIONS)},
             "act_dist": {a: int(r.act_dist[i]) for i, a in enumerate(ACTIONS)},
             "seconds": float(r.seconds), "error": None, "complete": bool(r.complete),
+            "narrow_levels": int(r.narrow_levels),
         }
         assert len(out["act_gen"]) == na
         if r.err_kind:
@@ -602,7 +603,7 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     for _ in range(args.steps):
         res = mc.run()
         sent += 0 if native else mc.records_sent
-        if not res["complete"] or res["error"]:
+        if (not res["complete"] and not kw.get("max_levels")) or res["error"]:
             raise RuntimeError(f"sharded check incomplete: error={res['error']} depth={res['depth']}")
     torch.cuda.synchronize()
     dist.barrier()
@@ -650,7 +651,8 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (the model's Init states; no external input)",
-            "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}",
+            "config": {"workload": desc, "model": f"nc={kw['nc']},np={kw['np']},ns={kw['ns']}"
+                       + (f",max_levels={kw['max_levels']}" if kw.get("max_levels") else ""),
                        "distinct": res["distinct"], "generated": res["generated"],
                        "depth": res["depth"], "golden_check": golden,
                        "path": ("sharded, native C++ level loop over RCCL (kc_group_run)" if native else

@@ -3,7 +3,10 @@ seconds per check and microseconds per BFS level, with R ranks emulated on
 one GPU (LocalComm) and with RCCL at world 1 (KC_RCCL_FORCE=1 keeps the
 world-1 collectives on RCCL), next to the single-GPU engine.
 
-  python tools/shard_levels.py [--np2]"""
+  python tools/shard_levels.py [--np2] [--ab]
+
+--ab adds the same runs with KC_SNARROW=0 (no device-driven narrow levels:
+every level on the counted path)."""
 import json
 import os
 import sys
@@ -39,14 +42,20 @@ def main():
     models = [("model1", {}, 5)]
     if "--np2" in sys.argv:
         models.append(("np2", dict(np=2, keep_trace=False), 2))
+    modes = [("", None)] + ([("_counted", "0")] if "--ab" in sys.argv else [])
     for name, kw, reps in models:
         out[f"{name}_engine"] = timed(lambda: ModelChecker(ModelConfig(**kw)), reps)
-        for R in (1, 2, 8):
-            out[f"{name}_emulated_R{R}"] = timed(lambda: NativeShardedChecker(ModelConfig(**kw), emulate=R), reps)
-        os.environ["KC_RCCL_FORCE"] = "1"
-        out[f"{name}_rccl_world1"] = timed(lambda: NativeShardedChecker(ModelConfig(**kw), 0, 1), reps)
-        del os.environ["KC_RCCL_FORCE"]
-        print(json.dumps({k: v for k, v in out.items() if k.startswith(name)}), flush=True)
+        for tag, sn in modes:
+            if sn is not None:
+                os.environ["KC_SNARROW"] = sn
+            for R in (1, 2, 8):
+                out[f"{name}_emulated_R{R}{tag}"] = timed(
+                    lambda: NativeShardedChecker(ModelConfig(**kw), emulate=R), reps)
+            os.environ["KC_RCCL_FORCE"] = "1"
+            out[f"{name}_rccl_world1{tag}"] = timed(lambda: NativeShardedChecker(ModelConfig(**kw), 0, 1), reps)
+            del os.environ["KC_RCCL_FORCE"]
+            os.environ.pop("KC_SNARROW", None)
+            print(json.dumps({k: v for k, v in out.items() if k.startswith(name)}), flush=True)
 
 
 if __name__ == "__main__":
