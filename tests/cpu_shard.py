@@ -37,7 +37,8 @@ class CpuShard:
             self.frontier.append(t)
             self.pkeys[0].append(KEY_INIT | k)
             if self.spec.check_invariants(t) is not None:
-                self.init_err = min(self.init_err, (self.rank << 60) | ((len(self.frontier) - 1) << 16) | 0x12)
+                # (HipShard's key: the Init state's index in TLC's order, then the rank)
+                self.init_err = min(self.init_err, (k << 16) | (self.rank << 8) | 0x12)
         self.n_init = len(self.frontier)
         self.init_key = self.init_err
         return len(self.frontier)

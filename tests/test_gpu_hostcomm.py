@@ -100,6 +100,8 @@ def test_errors_and_traces(results, fixtures, oracle, key, name, kind):
         assert r["error_action"] == fx["err_action"]
     if name == "lost_update":
         assert r["error_invariant"] == "NoLostUpdate"
+    if name == "variant5":       # the first Init state in TLC's order, whichever rank owns it
+        assert r["trace"] == fx["trace"]
     # the walk-back crossed ranks (broadcast); the trace is a real behaviour
     kw = {"nc2": dict(nc=2), "ns0": dict(ns=0)}.get(name, {})
     cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1),

@@ -307,6 +307,17 @@ def test_native_lost_update_invariant(fixtures, R):
         assert r["trace"] == fx["trace"]
 
 
+@pytest.mark.parametrize("R", [2, 3, 9])
+def test_native_init_violation_tlc_order(fixtures, R):
+    # variant 5: EVERY Init state violates OnlyOneVersion; the one reported
+    # is the first in TLC's Init order whichever rank owns it,
+    # the same state the oracle and the single-GPU engine report
+    fx = fixtures["variant5"]
+    r = native(R, variant=5)
+    assert r["error"] == "invariant" and r["error_level"] == 1
+    assert r["trace"] == fx["trace"]
+
+
 @pytest.mark.parametrize("R", [1, 3])
 def test_native_init_violation_max_levels_1(fixtures, R):
     # an Init state's invariant violation (variant 5) is level 1's error even

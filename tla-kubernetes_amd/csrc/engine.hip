@@ -132,10 +132,11 @@ k_counters_restore(Counters* __restrict__ C, const CtrStripe* __restrict__ prev,
 __global__ void k_claimset_fps(const ClaimEntry* __restrict__ t, uint64_t nslots,
                                unsigned long long* __restrict__ out, uint64_t cap,
                                unsigned long long* __restrict__ n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nslots && t[i].fp) {
-    const unsigned long long k = atomicAdd(n, 1ull);
-    if (k < cap) out[k] = t[i].fp;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (t[i].fp) {
+      const unsigned long long k = atomicAdd(n, 1ull);
+      if (k < cap) out[k] = t[i].fp;
+    }
   }
 }
 __global__ void k_adjacent_min_gap(const unsigned long long* __restrict__ s, uint64_t n,
@@ -691,7 +692,7 @@ class EngineT final : public EngineBase {
     if (!rc) {
       (void)hipMemsetAsync(d_n, 0, 8, st_);
       (void)hipMemcpyAsync(d_n + 1, &gap, 8, hipMemcpyHostToDevice, st_);
-      hipLaunchKernelGGL(k_claimset_fps, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_,
+      hipLaunchKernelGGL(k_claimset_fps, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_,
                          cs_.t, cs_.nslots, a, cnt, d_n);
       (void)hipMemcpyAsync(&n, d_n, 8, hipMemcpyDeviceToHost, st_);
       if (hipStreamSynchronize(st_) != hipSuccess || n > cnt) {
@@ -730,7 +731,7 @@ class EngineT final : public EngineBase {
     KC_TRY(cold_.all_keys(keys));
     uint64_t* hk = reinterpret_cast<uint64_t*>(sp_arena_);
     KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
-    hipLaunchKernelGGL(k_claimset_keys, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_, cs_.t,
+    hipLaunchKernelGGL(k_claimset_keys, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t,
                        cs_.nslots, hk, hot_limit_, d_spctr_ + 1);
     KC_HIP_TRY(hipMemcpyAsync(h_spctr_, d_spctr_, 16, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
@@ -1334,7 +1335,7 @@ class EngineT final : public EngineBase {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t* keys = reinterpret_cast<uint64_t*>(sp_arena_);
     KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
-    hipLaunchKernelGGL(k_claimset_keys, dim3((unsigned)((cs_.nslots + 255) / 256)), dim3(256), 0, st_, cs_.t,
+    hipLaunchKernelGGL(k_claimset_keys, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t,
                        cs_.nslots, keys, hot_limit_, d_spctr_ + 1);
     KC_HIP_TRY(hipMemcpyAsync(h_spctr_, d_spctr_, 16, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));

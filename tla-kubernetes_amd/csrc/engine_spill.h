@@ -133,22 +133,25 @@ __global__ void k_spill_apply(const uint64_t* __restrict__ qkey, const uint32_t*
 // the cold tier) into a dense array; *count = how many.
 __global__ void k_claimset_keys(const ClaimEntry* __restrict__ t, uint64_t nslots, uint64_t* __restrict__ out,
                                 uint64_t cap, unsigned long long* __restrict__ count) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool live = false;
-  uint64_t fp = 0;
-  if (i < nslots) {
-    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
-    fp = e.x;
-    live = fp != 0ull && e.y != kClaimRetired;
-  }
-  const unsigned long long b = __ballot(live);
-  const int lane = (int)(threadIdx.x & 63);
-  unsigned long long base = 0;
-  if (lane == 0 && b) base = atomicAdd(count, (unsigned long long)__popcll(b));
-  base = __shfl(base, 0, 64);
-  if (live) {
-    const uint64_t k = base + (uint64_t)__popcll(b & ((1ull << lane) - 1));
-    if (k < cap) out[k] = cold_key(fp);
+  // (grid-stride; the bound is uniform per wave, so the ballot sees every lane)
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < nslots; i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + threadIdx.x;
+    bool live = false;
+    uint64_t fp = 0;
+    if (i < nslots) {
+      const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(t + i);
+      fp = e.x;
+      live = fp != 0ull && e.y != kClaimRetired;
+    }
+    const unsigned long long b = __ballot(live);
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned long long base = 0;
+    if (lane == 0 && b) base = atomicAdd(count, (unsigned long long)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (live) {
+      const uint64_t k = base + (uint64_t)__popcll(b & ((1ull << lane) - 1));
+      if (k < cap) out[k] = cold_key(fp);
+    }
   }
 }
 

@@ -30,8 +30,8 @@ uint64_t next_pow2(uint64_t x) {
 __global__ void k_fpset_rehash(const unsigned long long* __restrict__ old, uint64_t old_slots,
                                unsigned long long* __restrict__ nw, uint64_t new_buckets,
                                unsigned long long* __restrict__ fail) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < old_slots) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < old_slots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long fp = old[i];
     if (fp && fpset_insert(nw, new_buckets, fp) < 0) atomicAdd(fail, 1ull);
   }
@@ -84,8 +84,7 @@ int DevFpset::reserve(uint64_t extra, hipStream_t st) {
   KC_HIP_TRY(hipMemsetAsync(ns, 0, nb * 64, st));
   KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
   const uint64_t old_slots = capacity();
-  const unsigned grid = (unsigned)((old_slots + 255) / 256);
-  hipLaunchKernelGGL(k_fpset_rehash, dim3(grid), dim3(256), 0, st, slots, old_slots, ns, nb, d_fail);
+  hipLaunchKernelGGL(k_fpset_rehash, dim3(table_grid(old_slots)), dim3(256), 0, st, slots, old_slots, ns, nb, d_fail);
   KC_HIP_TRY(hipGetLastError());
   unsigned long long fail = 0;
   KC_HIP_TRY(hipMemcpyAsync(&fail, d_fail, sizeof fail, hipMemcpyDeviceToHost, st));
@@ -120,19 +119,22 @@ __global__ void __launch_bounds__(256) k_claimset_clear(ClaimEntry* __restrict__
 __global__ void k_claimset_rehash(const ClaimEntry* __restrict__ old, uint64_t old_slots,
                                   ClaimEntry* __restrict__ nw, uint64_t new_slots,
                                   unsigned long long* __restrict__ fail) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= old_slots) return;
-  const ClaimEntry e = old[i];
-  if (!e.fp) return;
-  uint64_t k = bucket_of(e.fp, new_slots);
-  for (uint64_t probe = 0; probe < new_slots; ++probe) {
-    if (nw[k].fp == 0ull && atomicCAS(&nw[k].fp, 0ull, e.fp) == 0ull) {
-      nw[k].nclaim = e.nclaim;
-      return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < old_slots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const ClaimEntry e = old[i];
+    if (!e.fp) continue;
+    uint64_t k = bucket_of(e.fp, new_slots);
+    bool placed = false;
+    for (uint64_t probe = 0; probe < new_slots; ++probe) {
+      if (nw[k].fp == 0ull && atomicCAS(&nw[k].fp, 0ull, e.fp) == 0ull) {
+        nw[k].nclaim = e.nclaim;
+        placed = true;
+        break;
+      }
+      k = (k + 1 == new_slots) ? 0 : k + 1;
     }
-    k = (k + 1 == new_slots) ? 0 : k + 1;
+    if (!placed) atomicAdd(fail, 1ull);
   }
-  atomicAdd(fail, 1ull);
 }
 
 __global__ void k_claimset_insert_list(const uint64_t* __restrict__ fps, uint64_t n,
@@ -209,7 +211,7 @@ int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
   }
   KC_HIP_TRY(hipMemsetAsync(nt, 0, ns * sizeof(ClaimEntry), st));
   KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_claimset_rehash, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_claimset_rehash, dim3(table_grid(nslots)), dim3(256), 0, st,
                      t, nslots, nt, ns, d_fail);
   KC_HIP_TRY(hipGetLastError());
   unsigned long long fail = 0;
@@ -471,8 +473,8 @@ k_part_scatter(const uint64_t* __restrict__ fps, uint64_t n, uint32_t world, uin
 
 __global__ void k_compact_fps(const unsigned long long* __restrict__ slots, uint64_t nslots,
                               unsigned long long* __restrict__ out, unsigned long long* __restrict__ n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nslots && slots[i]) out[atomicAdd(n, 1ull)] = slots[i];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x)
+    if (slots[i]) out[atomicAdd(n, 1ull)] = slots[i];
 }
 __global__ void k_min_gap(const unsigned long long* __restrict__ s, uint64_t n,
                           unsigned long long* __restrict__ out) {
@@ -704,7 +706,7 @@ int kc_fpset_check_fps(kc_fpset* s, uint64_t* min_gap_out, double* prob_out) {
   if (!rc) {
     (void)hipMemsetAsync(d_n, 0, 8, st);
     (void)hipMemcpyAsync(d_n + 1, &gap, 8, hipMemcpyHostToDevice, st);
-    hipLaunchKernelGGL(k_compact_fps, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_compact_fps, dim3(table_grid(nslots)), dim3(256), 0, st,
                        s->fs.slots, nslots, d_a, d_n);
     (void)hipMemcpyAsync(&n, d_n, 8, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);

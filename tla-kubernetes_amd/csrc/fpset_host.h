@@ -8,6 +8,14 @@
 
 namespace kc {
 
+// Grid of a grid-stride pass over a table of n entries (256 lanes per
+// workgroup): at most 65,536 workgroups, so a table of 2^33+ slots does not
+// ask for more than 2^32 lanes in one launch.
+inline unsigned table_grid(uint64_t n) {
+  const uint64_t g = (n + 255) / 256;
+  return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
+}
+
 struct DevFpset {
   unsigned long long* slots = nullptr;  // nbuckets * 8 u64
   uint64_t nbuckets = 0;

@@ -41,10 +41,10 @@
 // fingerprint's top bits from the fold (no owner projection), and slot
 // lookup by byte-parallel compares of cumulative counts (locate_cum)
 #ifndef KC_OWN0_FOLD
-#define KC_OWN0_FOLD 0
+#define KC_OWN0_FOLD 1
 #endif
 #ifndef KC_LOCATE_SWAR
-#define KC_LOCATE_SWAR 0
+#define KC_LOCATE_SWAR 1
 #endif
 
 namespace kc {

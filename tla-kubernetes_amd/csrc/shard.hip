@@ -511,8 +511,11 @@ class ShardT final : public ShardBase {
       keys.push_back(KEY_INIT | (uint64_t)k);
       fps.push_back(fp);
       cand_ += (uint64_t)M::plan(s, flags_).total;
+      // an Init-state violation's key orders by the Init state's index in
+      // TLC's order (k << 16; the rank in bits 8-15), so the minimum over
+      // the ranks is the first violating Init state TLC would report
       if (M::check(s, flags_.inv_mask) >= 0 && init_err_ == ~0ull)
-        init_err_ = ((uint64_t)rank_ << 60) | ((uint64_t)(mine.size() - 1) << 16) | 0x12;
+        init_err_ = ((uint64_t)k << 16) | ((uint64_t)rank_ << 8) | 0x12;
     }
     n_ = mine.size();
     init_key_ = init_err_;

@@ -994,6 +994,15 @@ int Group::error_trace(uint64_t err, int level, kc_result* res) {
   std::vector<int> path;
   int r = (int)(err >> 60), lvl = level;
   uint64_t idx = (err >> 16) & KEY44;
+  if (kind == 0x12) {          // an Init state: its index in TLC's order is in the key
+    int act = -1, self = -1, inv = -1;
+    KC_TRY(local_[0]->replay((int)idx, path, kind, pos, trace_, &act, &self, &inv));
+    res->err_kind = E_INVARIANT;
+    res->err_invariant = inv;
+    res->err_level = 1;
+    res->trace_len = (int)trace_.size();
+    return 0;
+  }
   while (lvl > 1) {
     uint64_t key = 0;
     KC_TRY(query_parent(r, lvl, idx, &key));

@@ -518,6 +518,10 @@ class ShardedModelChecker:
     def _error(self, err: int, level: int) -> dict:
         kind = err & 0xff
         rank, pidx, pos = err >> 60, (err >> 16) & M44, (err >> 8) & 0xff
+        if kind == 0x12:     # an Init state: its index in TLC's order is in the key
+            s = self.spec.init()[pidx]
+            return {"error_level": 1, "error": "invariant", "error_invariant": self.spec.check_invariants(s),
+                    "trace": [[int(x) for x in s]], "trace_len": 1}
         path = []            # successor ordinals from an Init state
         r, idx, lvl = rank, pidx, level
         while lvl > 1:
