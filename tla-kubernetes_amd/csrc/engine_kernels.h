@@ -212,12 +212,21 @@ __device__ __forceinline__ void push_candidate(unsigned int* sh_rc, uint64_t til
 // per launch at RCCL world 1, r02i).
 constexpr int CLAIM_LDS_SH = 1792;
 static_assert(CLAIM_LDS_SH % CLAIM_TILE == 0, "whole entries per lane in the compaction");
+// (KC_LDS_LOWBITS: the slot from the fingerprint's low 32 bits — the
+// Zobrist fold, uniform in every bit on both paths — with no 64-bit
+// multiply; A/B switch, 0 = the remixed slot of rounds 1-3)
+#ifndef KC_LDS_LOWBITS
+#define KC_LDS_LOWBITS 1
+#endif
 template <int NT = CLAIM_LDS>
 __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int* sh_key,
                                          uint64_t fp, unsigned int lk) {
-  unsigned int h = NT == CLAIM_LDS
-                       ? (unsigned int)((fp * 0xd6e8feb86659fd93ull) >> (64 - CLAIM_LDS_BITS))
-                       : (unsigned int)(((fp * 0xd6e8feb86659fd93ull) >> 32) * (uint64_t)NT >> 32);
+  unsigned int h;
+  if (KC_LDS_LOWBITS)
+    h = NT == CLAIM_LDS ? (unsigned int)fp & (CLAIM_LDS - 1) : __umulhi((unsigned int)fp, (unsigned int)NT);
+  else
+    h = NT == CLAIM_LDS ? (unsigned int)((fp * 0xd6e8feb86659fd93ull) >> (64 - CLAIM_LDS_BITS))
+                        : (unsigned int)(((fp * 0xd6e8feb86659fd93ull) >> 32) * (uint64_t)NT >> 32);
   for (int p = 0; p < NT; ++p) {
     unsigned long long e = __hip_atomic_load(&sh_fp[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (e == 0ull) {

@@ -44,10 +44,21 @@ __host__ __device__ __forceinline__ uint64_t normalize_fp(uint64_t fp) {
   return fp ? fp : 1ull;
 }
 
+// KC_BUCKET_LOWBITS (A/B build switch): the bucket from the fingerprint's
+// low 59 bits — the Zobrist fold, uniform on every path; the top bits are
+// the sharded path's owner bits, which must not pick the bucket — with no
+// remixing multiply (0: rounds 1-3's multiply-shift on a remixed fp)
+#ifndef KC_BUCKET_LOWBITS
+#define KC_BUCKET_LOWBITS 0
+#endif
 __device__ __forceinline__ uint64_t bucket_of(uint64_t fp, uint64_t nbuckets) {
+#if KC_BUCKET_LOWBITS
+  return __umul64hi(fp << 5, nbuckets);
+#else
   // multiply-shift on a remixed fp: owner sharding uses the fp's top bits,
   // so the bucket index must not be a function of those bits alone.
   return __umul64hi(fp * 0x9e3779b97f4a7c15ull, nbuckets);
+#endif
 }
 __device__ __forceinline__ uint64_t batch_slot(uint64_t fp, uint64_t mask) {
   uint64_t h = fp ^ (fp >> 29);

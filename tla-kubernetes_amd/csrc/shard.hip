@@ -463,6 +463,7 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     KC_HIP_TRY(hipMalloc(&d_ctr_, sizeof(Counters)));
     KC_HIP_TRY(hipHostMalloc(&h_ctr_, sizeof(Counters)));
+    KC_HIP_TRY(hipHostMalloc(&h_exp_, kCtrHead));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));     // (zeroed by k_head_reset every level)
     KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
@@ -558,7 +559,7 @@ class ShardT final : public ShardBase {
       // nothing to claim; a device row still gets its status words
       if (d_row)
         hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, (uint64_t)0, (uint32_t)world_,
-                           d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                           d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
                            d_row, status_new, status_err, (int)level1, dev_init_err_);
       dev_empty_ = d_row == nullptr;
       dev_zero_ = true;
@@ -619,7 +620,7 @@ class ShardT final : public ShardBase {
     }
     if (world_ > 1 && cells <= OWNER_SMALL_SCAN) {
       hipLaunchKernelGGL(k_owner_scan_small, dim3(1), dim3(1024), 0, st_, cnt_, off_, n_, (uint32_t)world_,
-                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
                          d_row, status_new, status_err, (int)level1, dev_init_err_);
     } else {
       if (world_ > 1) {
@@ -629,7 +630,7 @@ class ShardT final : public ShardBase {
         KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
       }
       hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
-                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_ctr_),
+                         d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
                          d_row, status_new, status_err, (int)level1, dev_init_err_);
     }
     KC_HIP_TRY(hipGetLastError());
@@ -648,7 +649,9 @@ class ShardT final : public ShardBase {
       ++claim_launches_;
     }
     claim_parents_ += n_;
-    if (h_ctr_->overflow || h_ctr_->batch_used) {
+    // (expand's head has a pinned copy of its own, h_exp_: a caller with
+    // nothing to gather reads it only after insert's sync)
+    if (h_exp_->overflow || h_exp_->batch_used) {
       set_error("kc_shard_expand: successor overflow or full table");
       return -ENOMEM;
     }
@@ -656,8 +659,8 @@ class ShardT final : public ShardBase {
       counts[o] = h_owner_base_[o];
       send_total_ += counts[o];
     }
-    if (h_ctr_->err_key != ~0ull && !init_violated)
-      *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_ctr_->err_key);
+    if (h_exp_->err_key != ~0ull && !init_violated)
+      *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_exp_->err_key);
     return 0;
   }
 
@@ -993,6 +996,7 @@ class ShardT final : public ShardBase {
                     (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (h_exp_) (void)hipHostFree(h_exp_);
     if (h_owner_base_) (void)hipHostFree(h_owner_base_);
     for (void* p : {(void*)d_snc_, (void*)d_sns_, (void*)sn_send_, (void*)sn_recv_})
       if (p) (void)hipFree(p);
@@ -1033,6 +1037,7 @@ class ShardT final : public ShardBase {
   uint64_t* d_owner_base_ = nullptr;   // per-owner record totals (device / pinned host)
   uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;
+  Counters* h_exp_ = nullptr;          // pinned: expand's level head (kCtrHead bytes)
   uint64_t n_ = 0, next_n_ = 0, send_total_ = 0, gen_init_ = 0;
   uint64_t cand_ = 0, next_cand_ = 0, cand_total_ = 0;   // successors of the frontier
   uint64_t init_err_ = ~0ull;

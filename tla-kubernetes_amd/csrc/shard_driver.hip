@@ -189,6 +189,9 @@ class Comm {
   // of i); every slot is slot_bytes.  The same transfers every level,
   // whatever the ranks' device state, so they always match.
   virtual int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot_bytes) = 0;
+  // one rank in one process and every collective the identity: the level
+  // loop needs no gather (Group::run's solo levels)
+  virtual bool trivial() const { return false; }
 };
 
 class LocalComm final : public Comm {
@@ -278,6 +281,7 @@ class LocalComm final : public Comm {
     return 0;
   }
   int broadcast(int, uint64_t*) override { return 0; }   // the driver read it from the local root
+  bool trivial() const override { return s_.size() == 1; }
   int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
     out.assign(v[0].size(), 0);
     for (const auto& x : v)
@@ -382,6 +386,7 @@ class RcclComm final : public Comm {
     KC_NCCL_TRY(rccl()->group_end());
     return 0;
   }
+  bool trivial() const override { return trivial_; }
   int broadcast(int root, uint64_t* v) override {
     if (trivial_) return 0;
     KC_TRY(scratch(1));
@@ -601,6 +606,9 @@ class Group {
     sn_on_ = !(sn && sn[0] == '0');
     const char* sc = getenv("KC_SN_SLOT");
     sn_cap_ = sc && atoi(sc) > 0 ? (uint32_t)atoi(sc) : SN_SLOT_DEFAULT;
+    // KC_SOLO=0: a world-1 group runs the gather path too (A/B)
+    const char* so = getenv("KC_SOLO");
+    solo_off_ = so && so[0] == '0';
   }
   // The narrow levels' buffers, allocated with the group (a failure here is
   // the caller's before any collective of a run).
@@ -675,6 +683,7 @@ class Group {
   uint64_t* h_fail_ = nullptr;         // pinned: failure words copied into device rows
   int fault_rank_ = -1, fault_level_ = 0, fault_stage_ = 0;
   bool sn_on_ = true;
+  bool solo_off_ = false;
   uint32_t sn_cap_ = SN_SLOT_DEFAULT;
 };
 
@@ -738,6 +747,7 @@ int Group::run(kc_result* res) {
   int sn_batch = 8;
   uint64_t prev_total = ~0ull;
   std::vector<ShardBase::SNOut> so(nl);
+  const bool solo = R == 1 && nl == 1 && comm_->trivial() && !solo_off_;
   for (;;) {
     const bool last = cfg_.max_levels && level >= cfg_.max_levels;
     if (sn_on_ && !last && !sn_blocked) {
@@ -805,6 +815,40 @@ int Group::run(kc_result* res) {
       // SN_STOP, SN_ERROR, SN_DONE or a failure: this level runs on the
       // counted path, whose all-gather reports the error, the end or the
       // failure as it always does
+    }
+    if (solo) {
+      // One rank and nothing to gather or exchange: one host sync per level
+      // (insert's).  Expand's flags, error key and timing are read after it
+      // (its own pinned head, h_exp_); its error belongs to the next level's
+      // status as on the gather path.  An Init violation is already this
+      // level's status (init_error), so the level-1 shortcut is not needed.
+      if (fail[0]) return group_failed(local_[0]->rank(), fail_word(0), fail, fail_msg);
+      err = status_err[0];
+      const uint64_t total = status_new[0];
+      if (err != NONE || total == 0) {
+        --level;
+        break;
+      }
+      widths.push_back(total);
+      if (sn_blocked && total * 4 <= (uint64_t)SN_MAX && total < prev_total) sn_blocked = false;
+      prev_total = total;
+      if (last) break;
+      uint64_t n_new = 0, e2 = NONE, c0 = 0;
+      e1[0] = NONE;
+      inject(0, level, 0);
+      if (!fail[0]) note(0, local_[0]->expand_dev(status_new[0], status_err[0], level == 1, nullptr));
+      inject(0, level, 2);
+      if (!fail[0]) note(0, local_[0]->insert(nullptr, 0, &n_new, &e2));
+      if (!fail[0]) note(0, local_[0]->expand_done(&c0, &e1[0]));
+      if (!fail[0]) note(0, local_[0]->advance());
+      status_new[0] = fail[0] ? 0 : n_new;
+      status_err[0] = fail[0] ? NONE : std::min(e1[0], e2);
+      ++level;
+      if ((int)widths.size() >= KC_MAX_LEVELS) {
+        set_error("kc_group_run: more than %d levels", KC_MAX_LEVELS);
+        return -ENOMEM;
+      }
+      continue;
     }
     // device rows (every local shard's kernels write its all-gather row, so
     // the gather's sync is the level's first: expand has none of its own)

@@ -6,7 +6,9 @@ world-1 collectives on RCCL), next to the single-GPU engine.
   python tools/shard_levels.py [--np2] [--ab]
 
 --ab adds the same runs with KC_SNARROW=0 (no device-driven narrow levels:
-every level on the counted path)."""
+every level on the counted path).  Every run also reports RCCL world 1 with
+its identity collectives (the solo levels: one host sync per level) and the
+one-rank emulation with KC_SOLO=0 (the gather path at world 1)."""
 import json
 import os
 import sys
@@ -54,6 +56,11 @@ def main():
             os.environ["KC_RCCL_FORCE"] = "1"
             out[f"{name}_rccl_world1{tag}"] = timed(lambda: NativeShardedChecker(ModelConfig(**kw), 0, 1), reps)
             del os.environ["KC_RCCL_FORCE"]
+            out[f"{name}_world1_solo{tag}"] = timed(lambda: NativeShardedChecker(ModelConfig(**kw), 0, 1), reps)
+            os.environ["KC_SOLO"] = "0"
+            out[f"{name}_emulated_R1_nosolo{tag}"] = timed(
+                lambda: NativeShardedChecker(ModelConfig(**kw), emulate=1), reps)
+            del os.environ["KC_SOLO"]
             os.environ.pop("KC_SNARROW", None)
             print(json.dumps({k: v for k, v in out.items() if k.startswith(name)}), flush=True)
 
