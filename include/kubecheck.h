@@ -212,7 +212,8 @@ typedef struct {
   uint64_t frontier_segment_states;   /* 0 = 2^22 */
   const char *spill_dir;
   int trace_host;
-  /* Seen-set spill (single-GPU engine; TLC's OffHeapDiskFPSet role,
+  /* Seen-set spill (single-GPU engine, and every rank of the sharded loop
+   * for its own share of the fingerprints; TLC's OffHeapDiskFPSet role,
    * MC.out:5).  seen_hbm_bytes > 0 caps the HBM the seen-set uses: a fixed
    * hot ClaimSet (<= half of it), scratch, and the HBM directories and
    * filters of the cold tier.  When the hot table fills, its fingerprints are

@@ -28,6 +28,8 @@ CASES = [
     {"name": "variant2", "kw": {"variant": 2}},
     {"name": "variant5", "kw": {"variant": 5}},
     {"name": "ns0", "kw": {"ns": 0}},
+    # each process's seen-set under a 3 MiB HBM budget (shard.hip spill_*)
+    {"name": "seen_spill", "kw": {"seen_hbm_bytes": 3 << 20}},
     {"name": "lost_update", "kw": {"variant": 1, "invariants": 7}},
     {"name": "fault_pack", "kw": {}, "env": {"KC_FAULT": "1:7:1"}, "all_ranks": True},
     {"name": "fault_expand_hostrows", "kw": {}, "env": {"KC_FAULT": "0:9:0", "KC_DEVROW": "0"}, "all_ranks": True},
@@ -77,6 +79,16 @@ def test_model1_exact(results, fixtures):
         assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
         assert r["act_gen"] == fx["act_gen"]
         assert r["records_sent"] > 0          # records really crossed processes
+
+
+def test_seen_spill_exact(results, fixtures):
+    world, res = results
+    fx = fixtures["model1"]
+    r = res["seen_spill"][0]
+    assert "exception" not in r, r.get("exception")
+    assert r["complete"] and r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+    assert r["seen_flushes"] >= world and r["seen_cold_hits"] > 0
 
 
 def test_np2_prefix_exact(results, fixtures):

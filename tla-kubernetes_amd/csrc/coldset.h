@@ -83,6 +83,7 @@ struct ColdStats {
   uint64_t merges = 0, merged_keys = 0, disk_written = 0, disk_read = 0, windows_skipped = 0;
   uint64_t cached_runs = 0, cached_keys = 0, cache_bytes = 0, cache_uploaded = 0;
   uint64_t filter_tests = 0, filter_passed = 0;   // query x run pairs a filter saw / let through
+  uint64_t merge_probes = 0;                       // (query set, run) pairs read as a streaming merge
   // host wall time: pinning buffers, CPU merges, directory/filter builds
   // (incl. the copy of a new run), writing runs to files
   double pin_seconds = 0, merge_seconds = 0, meta_seconds = 0, evict_seconds = 0;
@@ -99,6 +100,10 @@ class ColdSet {
     int merge_threads = 16;
     int bloom_bits = 10;           // target filter bits per key (0 = no filters)
     bool cache_keys = true;        // copy the newest runs' keys into what HBM budget is left
+    // a host run probed by m >= n / merge_div sorted queries is read once,
+    // sequentially, by k_cold_merge_probe instead of ~1.2 random 64-B reads
+    // per query (0 = never; KC_COLD_MERGE_DIV overrides)
+    int merge_div = 16;
   };
   ColdSet() = default;
   ~ColdSet();
@@ -147,6 +152,7 @@ class ColdSet {
   std::vector<ColdRun> runs_;      // oldest first
   uint64_t keys_ = 0, host_used_ = 0, disk_used_ = 0, meta_used_ = 0, peak_meta_ = 0;
   uint64_t merges_ = 0, merged_keys_ = 0, disk_written_ = 0, disk_read_ = 0, windows_skipped_ = 0;
+  uint64_t merge_probes_ = 0;                  // (query set, run) pairs probed by the streaming merge
   uint64_t file_seq_ = 0, id_ = 0;
   uint64_t* stage_[2] = {nullptr, nullptr};   // pinned staging windows (disk runs)
   uint64_t stage_keys_ = 0;

@@ -940,11 +940,12 @@ class EngineT final : public EngineBase {
       res->seen_check_seconds = sp_check_seconds_;
       if (cfg_.verbose)
         fprintf(stderr, "kubecheck seen-set spill: %.3f s host (flushes %.3f: pin %.3f merge %.3f meta+copy %.3f files %.3f;"
-                        " checks %.3f), %llu flushes, %llu runs (%llu with %llu keys in HBM), %llu merges, %.1f GB uploaded\n",
+                        " checks %.3f), %llu flushes, %llu runs (%llu with %llu keys in HBM), %llu merges, %.1f GB uploaded,"
+                        " %llu streaming merge-probes\n",
                 sp_seconds_, sp_flush_seconds_, cst.pin_seconds, cst.merge_seconds, cst.meta_seconds, cst.evict_seconds,
                 sp_check_seconds_, (unsigned long long)sp_flushes_, (unsigned long long)cst.runs,
                 (unsigned long long)cst.cached_runs, (unsigned long long)cst.cached_keys,
-                (unsigned long long)cst.merges, cst.cache_uploaded / 1e9);
+                (unsigned long long)cst.merges, cst.cache_uploaded / 1e9, (unsigned long long)cst.merge_probes);
     }
     if (q_) {
       kc_squeue_stats qs;

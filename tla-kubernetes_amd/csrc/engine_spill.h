@@ -105,8 +105,25 @@ __global__ void __launch_bounds__(256) k_spill_queries(const typename M::State* 
   }
 }
 
+// Re-tag fp's hot slot "level 0" (a claim of ~0 reads as old from every
+// later level) and as already in the cold tier (flushes skip it).  False if
+// fp is not in the table, which the protocol never produces.
+__device__ __forceinline__ bool claimset_retire(ClaimEntry* __restrict__ cs, uint64_t nslots, uint64_t fp) {
+  uint64_t s = bucket_of(fp, nslots);
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    const unsigned long long f = cs[s].fp;
+    if (f == fp) {
+      cs[s].nclaim = kClaimRetired;
+      return true;
+    }
+    if (f == 0ull) break;
+    s = (s + 1 == nslots) ? 0 : s + 1;
+  }
+  return false;
+}
+
 // Winners found in the cold tier lose (see the file comment).
-__global__ void k_spill_apply(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qloc,
+static __global__ void k_spill_apply(const uint64_t* __restrict__ qkey, const uint32_t* __restrict__ qloc,
                               const uint8_t* __restrict__ found, uint64_t m, uint32_t* __restrict__ newmask,
                               uint32_t* __restrict__ tile_total, ClaimEntry* __restrict__ cs, uint64_t nslots,
                               Counters* __restrict__ C) {
@@ -115,23 +132,13 @@ __global__ void k_spill_apply(const uint64_t* __restrict__ qkey, const uint32_t*
   const uint32_t loc = qloc[i];
   atomicAnd(&newmask[loc >> 5], ~(1u << (loc & 31)));
   atomicSub(&tile_total[loc >> 13], 1u);              // tile = parent / 256
-  const uint64_t fp = cold_unkey(qkey[i]);
-  uint64_t s = bucket_of(fp, nslots);
-  for (uint64_t probe = 0; probe < nslots; ++probe) {
-    const unsigned long long f = cs[s].fp;
-    if (f == fp) {
-      cs[s].nclaim = kClaimRetired;
-      return;
-    }
-    if (f == 0ull) break;
-    s = (s + 1 == nslots) ? 0 : s + 1;
-  }
-  atomicAdd(&C->overflow, 1ull);                      // a winner's fp is always in the hot table
+  if (!claimset_retire(cs, nslots, cold_unkey(qkey[i])))
+    atomicAdd(&C->overflow, 1ull);                    // a winner's fp is always in the hot table
 }
 
 // Flush: the cold key of every live hot slot (retired slots are already in
 // the cold tier) into a dense array; *count = how many.
-__global__ void k_claimset_keys(const ClaimEntry* __restrict__ t, uint64_t nslots, uint64_t* __restrict__ out,
+static __global__ void k_claimset_keys(const ClaimEntry* __restrict__ t, uint64_t nslots, uint64_t* __restrict__ out,
                                 uint64_t cap, unsigned long long* __restrict__ count) {
   // (grid-stride; the bound is uniform per wave, so the ballot sees every lane)
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < nslots; i0 += (uint64_t)gridDim.x * blockDim.x) {

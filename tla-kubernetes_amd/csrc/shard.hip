@@ -31,10 +31,13 @@
 
 #include <algorithm>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "../../include/kubecheck.h"
+#include "coldset.h"
 #include "engine_kernels.h"
+#include "engine_spill.h"
 #include "engine_util.h"
 #include "fpset_host.h"
 #include "kc_common.h"
@@ -432,6 +435,67 @@ k_shard_emit(const typename M::State* __restrict__ cur, uint64_t n_local, uint32
 }
 constexpr unsigned SHARD_TAIL_BLOCKS = 64;    // emit grids up to this size run the level tail themselves
 
+// ---- seen-set spill (cfg.seen_hbm_bytes > 0), per rank: the engine's hot
+// ClaimSet + cold runs (coldset.h, engine_spill.h) over this rank's share of
+// the fingerprints.  After a level's settle passes and scans, its winners
+// w.r.t. the hot table are checked against the cold tier in windows of
+// emit positions [w0, w1): cold key + location (own successor: parent << 5 |
+// position; received record: bit 63 | record index).
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_spill_queries(const typename M::State* __restrict__ cur, uint64_t n_local, uint32_t lblocks, Flags f,
+                      const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets, uint64_t n,
+                      const unsigned long long* __restrict__ rfp, const uint32_t* __restrict__ isnew,
+                      const uint32_t* __restrict__ ioff, const Counters* __restrict__ C, uint64_t w0, uint64_t w1,
+                      uint64_t* __restrict__ qkey, uint64_t* __restrict__ qloc) {
+  if (blockIdx.x < lblocks) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_local) return;
+    uint32_t mask = newmask[i];
+    if (!mask) return;
+    const uint64_t o = offsets[i];
+    if (o >= w1 || o + (uint64_t)__builtin_popcount(mask) <= w0) return;
+    const typename M::State s = load_state<M>(cur, i);
+    const typename M::Plan pl = M::plan(s, f);
+    const uint64_t fold = M::fp_fold(s);
+    const uint32_t proj = M::owner_proj(s);
+    for (uint64_t pos = o; mask; mask &= mask - 1, ++pos) {
+      if (pos < w0 || pos >= w1) continue;
+      const int t = __ffs(mask) - 1;
+      int slot, j;
+      M::locate(pl, t, slot, j);
+      typename M::State x;
+      int who;
+      M::apply(s, slot, j, f, x, who);
+      // (the fingerprint k_claim claimed: owner bits included, as at every world)
+      qkey[pos - w0] = cold_key(M::template fingerprint_succ<1>(s, fold, x, who, proj));
+      qloc[pos - w0] = (i << 5) | (uint64_t)t;
+    }
+    return;
+  }
+  const uint64_t r = (uint64_t)(blockIdx.x - lblocks) * blockDim.x + threadIdx.x;
+  if (r >= n || !isnew[r]) return;
+  const uint64_t pos = C->chunk_base + ioff[r];
+  if (pos < w0 || pos >= w1) return;
+  qkey[pos - w0] = cold_key(rfp[r]);
+  qloc[pos - w0] = (1ull << 63) | r;
+}
+// Winners found in the cold tier lose: their newmask bit or isnew flag is
+// cleared and their hot slot retired (engine_spill.h claimset_retire).
+__global__ void k_shard_spill_apply(const uint64_t* __restrict__ qkey, const uint64_t* __restrict__ qloc,
+                                    const uint8_t* __restrict__ found, uint64_t m, uint32_t* __restrict__ newmask,
+                                    uint32_t* __restrict__ isnew, ClaimEntry* __restrict__ cs, uint64_t nslots,
+                                    Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m || !found[i]) return;
+  const uint64_t loc = qloc[i];
+  if (loc >> 63)
+    isnew[loc & ~(1ull << 63)] = 0u;
+  else
+    atomicAnd(&newmask[loc >> 5], ~(1u << (loc & 31)));
+  if (!claimset_retire(cs, nslots, cold_unkey(qkey[i]))) atomicAdd(&C->overflow, 1ull);
+}
+
 template <class M>
 class ShardT final : public ShardBase {
   using State = typename M::State;
@@ -441,7 +505,9 @@ class ShardT final : public ShardBase {
   ShardT(const kc_model_config& cfg, int rank, int world)
       : cfg_(cfg), rank_(rank), world_(world) {
     flags_ = flags_of(cfg);
-    cfg_.spill_dir = nullptr;      // (the engine's frontier spill; the caller's string is not kept)
+    spill_ = cfg.seen_hbm_bytes > 0;
+    if (cfg.spill_dir) spill_dir_ = cfg.spill_dir;   // (the seen-set's disk tier)
+    cfg_.spill_dir = nullptr;      // (the caller's string is not kept)
   }
   ~ShardT() override { release(); }
 
@@ -492,7 +558,9 @@ class ShardT final : public ShardBase {
   int init(uint64_t* n_local) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     const uint64_t fp_slots = cfg_.fpset_slots ? cfg_.fpset_slots : (1ull << 20);
-    if (cs_.t && cs_.capacity() >= fp_slots) {
+    if (spill_) {
+      KC_TRY(spill_setup());
+    } else if (cs_.t && cs_.capacity() >= fp_slots) {
       KC_TRY(cs_.clear(st_));
     } else {
       KC_TRY(cs_.init(fp_slots, st_));
@@ -538,6 +606,7 @@ class ShardT final : public ShardBase {
     }
     KC_HIP_TRY(hipStreamSynchronize(st_));
     cs_.count = n_;
+    distinct_ = n_;
     *n_local = n_;
     return 0;
   }
@@ -570,7 +639,16 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_expand: frontier wider than 2^32 states");
       return -ENOMEM;
     }
-    KC_TRY(cs_.reserve(cand_, st_));
+    if (spill_) {
+      // the level's claims (own successors and received records: about
+      // cand_ successors together, of which the last level's fraction
+      // filled hot slots) go into the fixed hot table; flush it first when
+      // they might take it past 1/2 load
+      const uint64_t need = std::min<uint64_t>(cand_, (uint64_t)((double)cand_ * sp_ratio_ * 1.25) + 4096);
+      if (cs_.count > 0 && cs_.count + need > hot_limit_) KC_TRY(spill_flush());
+    } else {
+      KC_TRY(cs_.reserve(cand_, st_));
+    }
     const uint64_t tiles = (n_ + CLAIM_TILE - 1) / CLAIM_TILE;
     KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
     KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
@@ -750,7 +828,7 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_insert: more than 2^31 records or parents in one level");
       return -ENOMEM;
     }
-    KC_TRY(cs_.reserve(cand_ + n, st_));     // count excludes this level's local inserts (<= cand_)
+    if (!spill_) KC_TRY(cs_.reserve(cand_ + n, st_));     // count excludes this level's local inserts (<= cand_)
     const uint32_t succ_level = (uint32_t)level_ + 1;
     const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
     const unsigned rgrid = (unsigned)((n + 255) / 256);
@@ -774,24 +852,11 @@ class ShardT final : public ShardBase {
                        cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
                        flag_, isnew_, d_ctr_, ovf_);
     // positions: this rank's own winners first, then the records'
-    if (n_) KC_TRY(grow_buffer(offsets_, offsets_cap_, n_, false, st_));
-    if (n_ <= SHARD_SMALL_SCAN && n <= SHARD_SMALL_SCAN) {
-      hipLaunchKernelGGL(k_shard_scan_small, dim3(1), dim3(1024), 0, st_, newmask_, n_, offsets_, isnew_, n, ioff_,
-                         d_ctr_);
-    } else {
-      size_t tmp_bytes = 0;
-      if (n_) {
-        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)n_, st_));
-        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)n_, st_));
-      }
-      if (n) {
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
-        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
-      }
-      hipLaunchKernelGGL(k_shard_base, dim3(1), dim3(64), 0, st_, offsets_, newmask_, n_, ioff_, isnew_, n, d_ctr_);
+    KC_TRY(scan_winners(n));
+    if (spill_) {
+      bool changed = false;
+      KC_TRY(spill_check(n, tiles, rgrid, &changed));
+      if (changed) KC_TRY(scan_winners(n));
     }
     // capacity: at most one new state per own successor and per record
     const uint64_t bound = cand_ + n;
@@ -814,9 +879,173 @@ class ShardT final : public ShardBase {
     next_n_ = h_ctr_->level_new;
     next_cand_ = h_ctr_->cand_total - cand_total_;
     cand_total_ = h_ctr_->cand_total;
-    cs_.count += next_n_;
+    if (!spill_) cs_.count += next_n_;   // (spill: spill_check counted the hot slots)
+    distinct_ += next_n_;
     if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
     *n_new = next_n_;
+    return 0;
+  }
+
+  // Exclusive scans of the own winners' newmask popcounts (offsets_) and the
+  // records' isnew flags (ioff_); C->chunk_base / level_new = the totals.
+  int scan_winners(uint64_t n) {
+    if (n_) KC_TRY(grow_buffer(offsets_, offsets_cap_, n_, false, st_));
+    if (n_ <= SHARD_SMALL_SCAN && n <= SHARD_SMALL_SCAN) {
+      hipLaunchKernelGGL(k_shard_scan_small, dim3(1), dim3(1024), 0, st_, newmask_, n_, offsets_, isnew_, n, ioff_,
+                         d_ctr_);
+    } else {
+      size_t tmp_bytes = 0;
+      if (n_) {
+        const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> newcnt(newmask_, NewCount());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, newcnt, offsets_, (int)n_, st_));
+      }
+      if (n) {
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, isnew_, ioff_, (int)n, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, isnew_, ioff_, (int)n, st_));
+      }
+      hipLaunchKernelGGL(k_shard_base, dim3(1), dim3(64), 0, st_, offsets_, newmask_, n_, ioff_, isnew_, n, d_ctr_);
+    }
+    return 0;
+  }
+
+  // ---- seen-set spill (cfg.seen_hbm_bytes > 0; the engine's scheme,
+  // engine.hip spill_setup/spill_flush/spill_check, with whole levels: the
+  // sharded level cannot be cut into chunks without cutting every rank's).
+  // Budget B per rank: the hot ClaimSet takes the largest power-of-two table
+  // of <= B/2 bytes, flushed before a level whose claims might take it past
+  // 1/2 load (a level may go on to 7/8: an estimate, not a bound, decides
+  // the flush); one arena serves the flush (up to 7/8 of the slots' keys) and
+  // the level's cold check (q_max_ queries per window); the rest is the cold
+  // runs' directories and filters.
+  int spill_setup() {
+    if (!cs_.t) {
+      const uint64_t B = cfg_.seen_hbm_bytes;
+      uint64_t ns = 1ull << 12;
+      while (ns * 2 * sizeof(ClaimEntry) <= B / 2) ns *= 2;
+      KC_TRY(cs_.init(ns, st_));
+      hot_limit_ = ns / 2;
+      hot_hard_ = ns / 8 * 7;
+      uint64_t arena = hot_hard_ * 8;
+      q_max_ = std::max<uint64_t>(256, arena / 48 / 256 * 256);
+      size_t tmp = 0;
+      {
+        hipcub::DoubleBuffer<uint64_t> k(nullptr, nullptr);
+        hipcub::DoubleBuffer<uint64_t> v(nullptr, nullptr);
+        KC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, v, (int)q_max_, 0, 64, st_));
+      }
+      sp_qtmp_bytes_ = tmp;
+      arena = std::max<uint64_t>(arena, q_max_ * 33 + tmp + 1024);
+      sp_arena_bytes_ = arena;
+      KC_HIP_TRY(hipMalloc(&sp_arena_, arena));
+      KC_HIP_TRY(hipMalloc(&d_spctr_, 64));
+      KC_HIP_TRY(hipHostMalloc(&h_spctr_, 64));
+      const uint64_t used = ns * sizeof(ClaimEntry) + arena;
+      if (used + (1ull << 20) > B) {
+        set_error("kc_shard: seen_hbm_bytes %llu too small (hot table + scratch need %llu B)",
+                  (unsigned long long)B, (unsigned long long)used);
+        return -EINVAL;
+      }
+      ColdSet::Config cc;
+      cc.device = cfg_.device;
+      cc.meta_hbm_bytes = B - used;
+      cc.host_bytes = cfg_.seen_host_bytes;
+      cc.dir = spill_dir_;
+      const char* wk = getenv("KC_COLD_WINDOW");      // disk-run staging window (keys); tests shrink it
+      if (wk && atoll(wk) > 0) cc.window_keys = (uint64_t)atoll(wk);
+      const char* bb = getenv("KC_COLD_BLOOM_BITS");  // filter bits per key (0 = no filters; A/B)
+      if (bb) cc.bloom_bits = atoi(bb);
+      const char* ck = getenv("KC_COLD_CACHE");       // KC_COLD_CACHE=0: no HBM copies of run keys (A/B)
+      cc.cache_keys = !(ck && ck[0] == '0');
+      KC_TRY(cold_.init(cc));
+    } else {
+      KC_TRY(cs_.clear(st_));
+    }
+    cold_.clear();
+    sp_flushes_ = sp_queries_ = 0;
+    sp_ratio_ = 1.0;
+    KC_HIP_TRY(hipMemsetAsync(d_spctr_, 0, 64, st_));
+    return 0;
+  }
+
+  // Hot table -> one sorted cold run; the table starts over empty.
+  int spill_flush() {
+    uint64_t* keys = reinterpret_cast<uint64_t*>(sp_arena_);
+    KC_HIP_TRY(hipMemsetAsync(d_spctr_ + 1, 0, 8, st_));
+    hipLaunchKernelGGL(k_claimset_keys, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t, cs_.nslots, keys,
+                       hot_hard_, d_spctr_ + 1);
+    KC_HIP_TRY(hipMemcpyAsync(h_spctr_, d_spctr_, 16, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const uint64_t c = h_spctr_[1];
+    if (c > hot_hard_) {
+      set_error("kc_shard: hot seen-set holds %llu > %llu fingerprints", (unsigned long long)c,
+                (unsigned long long)hot_hard_);
+      return -EIO;
+    }
+    if (c) {
+      // sorted in place, the hot table (cleared right after) lending the
+      // alternate buffer and the temporary storage
+      uint64_t* alt = reinterpret_cast<uint64_t*>(cs_.t);
+      const uint64_t tab = cs_.nslots * sizeof(ClaimEntry);
+      const uint64_t off = (c * 8 + 255) / 256 * 256;
+      hipcub::DoubleBuffer<uint64_t> kb(keys, alt);
+      size_t tb = 0;
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, kb, (int)c, 0, 64, st_));
+      if (off + tb > tab) {
+        set_error("kc_shard: seen-set flush sort needs %llu B > %llu", (unsigned long long)(off + tb),
+                  (unsigned long long)tab);
+        return -ENOMEM;
+      }
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortKeys(reinterpret_cast<uint8_t*>(cs_.t) + off, tb, kb, (int)c, 0, 64,
+                                                   st_));
+      KC_TRY(cold_.add_run(kb.Current(), c, st_));
+    }
+    KC_TRY(cs_.clear(st_));
+    cs_.count = 0;
+    ++sp_flushes_;
+    return 0;
+  }
+
+  // The level's winners w.r.t. the hot table (C->level_new after the first
+  // scans) against the cold tier; those found lose.  *changed: some did.
+  int spill_check(uint64_t n, unsigned tiles, unsigned rgrid, bool* changed) {
+    *changed = false;
+    KC_HIP_TRY(hipMemcpyAsync(h_spctr_ + 2, &d_ctr_->level_new, 8, hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    const uint64_t m = h_spctr_[2];
+    cs_.count += m;                   // the hot slots this level filled
+    sp_queries_ += m;
+    if (cand_) sp_ratio_ = std::min(1.0, (double)m / (double)cand_);
+    if (cs_.count > hot_hard_) {
+      set_error("kc_shard: one level put %llu fingerprints into a hot seen-set of %llu slots; raise seen_hbm_bytes",
+                (unsigned long long)m, (unsigned long long)cs_.nslots);
+      return -ENOMEM;
+    }
+    if (m == 0 || cold_.empty()) return 0;
+    uint64_t* qk = reinterpret_cast<uint64_t*>(sp_arena_);
+    uint64_t* qk2 = qk + q_max_;
+    uint64_t* ql = qk2 + q_max_;
+    uint64_t* ql2 = ql + q_max_;
+    uint8_t* found = reinterpret_cast<uint8_t*>(ql2 + q_max_);
+    uint8_t* tmp = found + (q_max_ + 255) / 256 * 256;
+    const unsigned lb = n_ ? tiles : 0u;
+    for (uint64_t w0 = 0; w0 < m; w0 += q_max_) {
+      const uint64_t w1 = std::min(m, w0 + q_max_), c = w1 - w0;
+      hipLaunchKernelGGL(k_shard_spill_queries<M>, dim3(std::max(lb + rgrid, 1u)), dim3(256), 0, st_, cur_, n_, lb,
+                         flags_, newmask_, offsets_, n, rfp_, isnew_, ioff_, d_ctr_, w0, w1, qk, ql);
+      hipcub::DoubleBuffer<uint64_t> kb(qk, qk2);
+      hipcub::DoubleBuffer<uint64_t> vb(ql, ql2);
+      size_t tb = sp_qtmp_bytes_;
+      KC_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kb, vb, (int)c, 0, 64, st_));
+      KC_HIP_TRY(hipMemsetAsync(found, 0, c, st_));
+      KC_TRY(cold_.probe(kb.Current(), c, found, d_spctr_, st_));
+      hipLaunchKernelGGL(k_shard_spill_apply, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, st_, kb.Current(),
+                         vb.Current(), found, c, newmask_, isnew_, cs_.t, cs_.nslots, d_ctr_);
+      KC_HIP_TRY(hipGetLastError());
+    }
+    *changed = true;
     return 0;
   }
 
@@ -924,6 +1153,7 @@ class ShardT final : public ShardBase {
       w = k < (uint32_t)KC_MAX_LEVELS ? h.lwidths[k] : 0;
     }
     cs_.count += h.new_total;
+    distinct_ += h.new_total;
     level_ = (int)h.level;
     n_ = h.n;
     cand_ = h.cand;
@@ -977,8 +1207,21 @@ class ShardT final : public ShardBase {
     }
     r->init = gen_init_;
     r->generated = gen;                 // successors generated by this rank's parents
-    r->distinct = cs_.count;
+    r->distinct = distinct_;
     r->fpset_slots = cs_.capacity();
+    if (spill_) {
+      ColdStats cst;
+      cold_.stats(&cst);
+      unsigned long long hits = 0;
+      KC_HIP_TRY(hipMemcpy(&hits, d_spctr_, 8, hipMemcpyDeviceToHost));
+      r->seen_flushes = sp_flushes_;
+      r->seen_cold_fps = cst.keys;
+      r->seen_cold_runs = cst.runs;
+      r->seen_cold_queries = sp_queries_;
+      r->seen_cold_hits = hits;
+      r->seen_merges = cst.merges;
+      r->seen_disk_bytes = cst.disk_written;
+    }
     r->fpset_probes = h_ctr_->probes();
     r->batch_inserts = h_ctr_->settles();
     r->nlevels = level_;
@@ -1001,6 +1244,9 @@ class ShardT final : public ShardBase {
     for (void* p : {(void*)d_snc_, (void*)d_sns_, (void*)sn_send_, (void*)sn_recv_})
       if (p) (void)hipFree(p);
     if (h_snc_) (void)hipHostFree(h_snc_);
+    if (sp_arena_) (void)hipFree(sp_arena_);
+    if (d_spctr_) (void)hipFree(d_spctr_);
+    if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
     if (st_ && own_st_) (void)hipStreamDestroy(st_);
@@ -1058,6 +1304,18 @@ class ShardT final : public ShardBase {
   uint64_t sn_n0_ = 0;
   double claim_ms_ = 0;
   uint64_t claim_launches_ = 0, claim_parents_ = 0;
+  uint64_t distinct_ = 0;           // new states this rank owns (cs_.count is the hot table's, spilling)
+  // seen-set spill
+  bool spill_ = false;
+  std::string spill_dir_;
+  ColdSet cold_;
+  uint64_t hot_limit_ = 0, hot_hard_ = 0, q_max_ = 0;
+  uint8_t* sp_arena_ = nullptr;
+  uint64_t sp_arena_bytes_ = 0;
+  size_t sp_qtmp_bytes_ = 0;
+  unsigned long long *d_spctr_ = nullptr, *h_spctr_ = nullptr;   // [0] cold hits, [1] flush count, [2] m
+  uint64_t sp_flushes_ = 0, sp_queries_ = 0;
+  double sp_ratio_ = 1.0;           // hot slots filled per successor, last level
 };
 
 std::unique_ptr<ShardBase> make_shard(const kc_model_config& cfg, int rank, int world) {

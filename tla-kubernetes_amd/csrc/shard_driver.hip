@@ -613,6 +613,10 @@ class Group {
   // The narrow levels' buffers, allocated with the group (a failure here is
   // the caller's before any collective of a run).
   int setup() {
+    // (a seen-set that spills takes the counted path at every level: its
+    // cold check runs between the settle passes and the emit.  Every rank
+    // runs with the same configuration, so they all decide alike.)
+    if (cfg_.seen_hbm_bytes) sn_on_ = false;
     if (!sn_on_) return 0;
     for (auto* s : local_) KC_TRY(s->sn_setup(sn_cap_));
     return 0;
@@ -985,10 +989,24 @@ int Group::run(kc_result* res) {
     mine[i].push_back(r.distinct);
     mine[i].push_back(sent_local_[i]);
     mine[i].push_back(fail[i] ? 1 : 0);
+    // seen-set spill (summed over the ranks)
+    for (uint64_t v : {r.seen_flushes, r.seen_cold_fps, r.seen_cold_runs, r.seen_cold_queries, r.seen_cold_hits,
+                       r.seen_merges, r.seen_disk_bytes})
+      mine[i].push_back(v);
   }
   std::vector<uint64_t> tot;
   KC_TRY(comm_->all_reduce_sum(mine, tot));
   if (tot[2 * KC_NACTIONS + 4]) return group_failed(-1, 0, fail, fail_msg);
+  {
+    const uint64_t* sp = tot.data() + 2 * KC_NACTIONS + 5;
+    res->seen_flushes = sp[0];
+    res->seen_cold_fps = sp[1];
+    res->seen_cold_runs = sp[2];
+    res->seen_cold_queries = sp[3];
+    res->seen_cold_hits = sp[4];
+    res->seen_merges = sp[5];
+    res->seen_disk_bytes = sp[6];
+  }
   for (int a = 0; a < KC_NACTIONS; ++a) {
     res->act_gen[a] = tot[a];
     res->act_dist[a] = tot[KC_NACTIONS + a];

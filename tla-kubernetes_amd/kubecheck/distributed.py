@@ -283,6 +283,10 @@ class NativeShardedChecker:
             "seconds": float(r.seconds), "error": None, "complete": bool(r.complete),
             "narrow_levels": int(r.narrow_levels),
         }
+        if self.cfg.seen_hbm_bytes:      # per-rank seen-set spill, summed over the ranks
+            out.update(seen_flushes=int(r.seen_flushes), seen_cold_fps=int(r.seen_cold_fps),
+                       seen_cold_runs=int(r.seen_cold_runs), seen_cold_queries=int(r.seen_cold_queries),
+                       seen_cold_hits=int(r.seen_cold_hits))
         assert len(out["act_gen"]) == na
         if r.err_kind:
             tw = self.spec.tuple_words
