@@ -9,7 +9,8 @@ seen-set's and to the golden counts:
 
 * Model_1 equals MC.out (totals, depth, widths, per-action counts) through
   the host tier, the file tier (small staging windows: many windows, most
-  skipped), and with the Bloom filters off (every query reads the runs);
+  skipped), with the Bloom filters off (every query reads the runs), and
+  with every host run read by the streaming merge-probe;
 * every error kind, with its trace, state for state against the in-HBM run;
 * the NP=2 model's first 55 levels through the file tier;
 * the full NP=2 model (740,607,995 states) with its seen-set capped at 4 GiB
@@ -51,7 +52,7 @@ def model1_ref():
     return r, gap
 
 
-@pytest.mark.parametrize("tier", ["host", "disk", "no_filter", "host_budget_no_dir"])
+@pytest.mark.parametrize("tier", ["host", "disk", "no_filter", "host_budget_no_dir", "merge_probe"])
 def test_seen_spill_model1(model1_ref, mcout, fixtures, tmp_path, monkeypatch, tier):
     ref, ref_gap = model1_ref
     kw = dict(seen_hbm_bytes=4 * MiB)
@@ -60,6 +61,9 @@ def test_seen_spill_model1(model1_ref, mcout, fixtures, tmp_path, monkeypatch, t
         monkeypatch.setenv("KC_COLD_WINDOW", "4096")
     if tier == "no_filter":
         monkeypatch.setenv("KC_COLD_BLOOM_BITS", "0")
+    if tier == "merge_probe":   # every host run probed by the streaming merge (coldset.hip), none cached in HBM
+        monkeypatch.setenv("KC_COLD_MERGE_DIV", "100000000")
+        monkeypatch.setenv("KC_COLD_CACHE", "0")
     if tier == "host_budget_no_dir":
         kw.update(seen_host_bytes=256 << 10)
         with pytest.raises(KubecheckError) as e:
@@ -80,8 +84,8 @@ def test_seen_spill_model1(model1_ref, mcout, fixtures, tmp_path, monkeypatch, t
     if tier == "disk":
         assert s["disk_bytes"] > 0
         assert os.listdir(tmp_path) == []       # spill files removed with the engine
-    if tier == "no_filter":
-        assert s["filter_tests"] == 0
+    if tier in ("no_filter", "merge_probe"):
+        assert s["filter_tests"] == 0          # (the streaming merge reads whole runs, no filters)
     else:
         assert 0 < s["filter_passed"] < s["filter_tests"]
 

@@ -37,13 +37,19 @@ def _same(a, b):
         assert a.get(k) == b.get(k), k
 
 
-@pytest.mark.parametrize("R,budget,tier", [(2, 4 * MiB, "host"), (4, 3 * MiB, "host"), (2, 4 * MiB, "disk")])
+@pytest.mark.parametrize("R,budget,tier", [(2, 4 * MiB, "host"), (4, 3 * MiB, "host"), (2, 4 * MiB, "disk"),
+                                           (2, 4 * MiB, "windows"), (3, 4 * MiB, "merge_probe")])
 def test_shard_seen_spill_model1(fixtures, mcout, tmp_path, monkeypatch, R, budget, tier):
     ref = native(R)
     kw = dict(seen_hbm_bytes=budget)
     if tier == "disk":
         kw.update(seen_host_bytes=128 << 10, spill_dir=str(tmp_path))
         monkeypatch.setenv("KC_COLD_WINDOW", "4096")
+    if tier == "windows":       # each level's cold check in windows of 256 queries (last to first)
+        monkeypatch.setenv("KC_SEEN_QMAX", "256")
+    if tier == "merge_probe":   # every host run probed by the streaming merge, none cached in HBM
+        monkeypatch.setenv("KC_COLD_MERGE_DIV", "100000000")
+        monkeypatch.setenv("KC_COLD_CACHE", "0")
     r = native(R, **kw)
     _same(r, ref)
     fx = fixtures["model1"]

@@ -14,7 +14,8 @@ enum KernelKind { KK_EXPAND = 0, KK_RESOLVE = 1, KK_SCAN = 2, KK_EMIT = 3, KK_CO
 // diagnostic-only ablation timings (KC_ABLATE=1 in the environment): extra
 // launches of cut-down k_claim / k_emit variants on scratch buffers, printed to stderr
 enum AblateKind { KA_LDS = KK_COUNT, KA_COMPUTE = KK_COUNT + 1, KA_PLAN = KK_COUNT + 2,
-                  KA_E1 = KK_COUNT + 3, KA_E2 = KK_COUNT + 4, KA_E3 = KK_COUNT + 5, KA_TOTAL = KK_COUNT + 6 };
+                  KA_E1 = KK_COUNT + 3, KA_E2 = KK_COUNT + 4, KA_E3 = KK_COUNT + 5,
+                  KA_FPCHEAP = KK_COUNT + 6, KA_NOAPPLY = KK_COUNT + 7, KA_TOTAL = KK_COUNT + 8 };
 // the narrow-level kernel (engine_narrow.h): levels it ran, launches, time
 constexpr int KK_NARROW = KA_TOTAL;
 constexpr int KK_ALL = KA_TOTAL + 1;

@@ -482,6 +482,16 @@ class EngineT final : public EngineBase {
                                cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                                succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
+          timed(KA_FPCHEAP, [&] {
+            hipLaunchKernelGGL((k_claim<M, 4>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
+          });
+          timed(KA_NOAPPLY, [&] {
+            hipLaunchKernelGGL((k_claim<M, 5>), dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start,
+                               cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                               succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
+          });
         }
         timed(KK_RESOLVE, [&] {
           hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
@@ -653,9 +663,11 @@ class EngineT final : public EngineBase {
     finish(res, t0, n);
     if (ablate_) {
       fprintf(stderr, "kubecheck ablate: claim %.2f ms | successors+LDS %.2f ms | successors only %.2f ms | plan only %.2f ms | settle %.2f | emit %.2f ms"
-              " | emit-no-plan %.2f | emit-no-plan-no-check %.2f | emit-parent-only %.2f\n",
+              " | emit-no-plan %.2f | emit-no-plan-no-check %.2f | emit-parent-only %.2f"
+              " | successors, XOR fingerprint %.2f | fingerprints, no apply %.2f\n",
               ktime_ms_[KK_EXPAND], ktime_ms_[KA_LDS], ktime_ms_[KA_COMPUTE], ktime_ms_[KA_PLAN], ktime_ms_[KK_RESOLVE],
-              ktime_ms_[KK_EMIT], ktime_ms_[KA_E1], ktime_ms_[KA_E2], ktime_ms_[KA_E3]);
+              ktime_ms_[KK_EMIT], ktime_ms_[KA_E1], ktime_ms_[KA_E2], ktime_ms_[KA_E3], ktime_ms_[KA_FPCHEAP],
+              ktime_ms_[KA_NOAPPLY]);
       KC_HIP_TRY(hipMemcpy(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost));
       fprintf(stderr, "kubecheck claim outcomes (KC_DIAG builds): old %llu lost %llu cur %llu new %llu\n",
               h_ctr_->claim_out(0), h_ctr_->claim_out(1), h_ctr_->claim_out(2), h_ctr_->claim_out(3));

@@ -369,7 +369,9 @@ __global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, F
 
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
 // KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only,
-// 3 = plan + fold only (no successor).
+// 3 = plan + fold only (no successor), 4 = successors with an XOR of their
+// words for a fingerprint (2 - 4: the fingerprint's cost), 5 = fingerprints
+// of the parent with one word perturbed, no apply (2 - 5: apply's cost).
 // Occupancy: the LDS table (24 KB) allows 6 workgroups = 6 waves per SIMD;
 // the claims are latency-bound random probes, so the register budget is
 // pinned to match (one wave less measured +15 ms per NP=2 check).
@@ -590,10 +592,26 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         M::locate(pl, t, slot, j);
       typename M::State x;
       int who;
-      M::apply(s, slot, j, f, x, who);
-      const uint64_t fp = OWN ? M::template fingerprint_succ<1>(s, fold, x, who, sh_proj[KC_LP])
-                              : M::template fingerprint_succ<0>(s, fold, x, who);
-      if (ABL == 2) {
+      if (ABL == 5) {
+#pragma unroll
+        for (int k = 0; k < M::W; ++k) x.w[k] = s.w[k];
+        who = slot % M::A;
+#pragma unroll
+        for (int k = 0; k < M::A; ++k)
+          if (k == who) x.w[1 + k] ^= (uint64_t)(j + 1) << (slot & 31);
+      } else {
+        M::apply(s, slot, j, f, x, who);
+      }
+      uint64_t fp;
+      if (ABL == 4) {
+        fp = 0;
+#pragma unroll
+        for (int k = 0; k < M::W; ++k) fp ^= x.w[k] << k;
+      } else {
+        fp = OWN ? M::template fingerprint_succ<1>(s, fold, x, who, sh_proj[KC_LP])
+                 : M::template fingerprint_succ<0>(s, fold, x, who);
+      }
+      if (ABL == 2 || ABL == 4 || ABL == 5) {
         acc ^= fp;
         continue;
       }

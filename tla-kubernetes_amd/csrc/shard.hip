@@ -930,6 +930,8 @@ class ShardT final : public ShardBase {
       hot_hard_ = ns / 8 * 7;
       uint64_t arena = hot_hard_ * 8;
       q_max_ = std::max<uint64_t>(256, arena / 48 / 256 * 256);
+      const char* qm = getenv("KC_SEEN_QMAX");        // queries per cold-check window (tests: many windows)
+      if (qm && atoll(qm) >= 256) q_max_ = std::min<uint64_t>(q_max_, (uint64_t)atoll(qm) / 256 * 256);
       size_t tmp = 0;
       {
         hipcub::DoubleBuffer<uint64_t> k(nullptr, nullptr);
@@ -1031,8 +1033,12 @@ class ShardT final : public ShardBase {
     uint8_t* found = reinterpret_cast<uint8_t*>(ql2 + q_max_);
     uint8_t* tmp = found + (q_max_ + 255) / 256 * 256;
     const unsigned lb = n_ ? tiles : 0u;
-    for (uint64_t w0 = 0; w0 < m; w0 += q_max_) {
-      const uint64_t w1 = std::min(m, w0 + q_max_), c = w1 - w0;
+    // windows from the last to the first: a winner that loses clears its
+    // bit, which would shift the positions of its parent's later winners,
+    // so every window is taken before any lower one changes
+    const uint64_t nwin = (m + q_max_ - 1) / q_max_;
+    for (uint64_t wi = nwin; wi-- > 0;) {
+      const uint64_t w0 = wi * q_max_, w1 = std::min(m, w0 + q_max_), c = w1 - w0;
       hipLaunchKernelGGL(k_shard_spill_queries<M>, dim3(std::max(lb + rgrid, 1u)), dim3(256), 0, st_, cur_, n_, lb,
                          flags_, newmask_, offsets_, n, rfp_, isnew_, ioff_, d_ctr_, w0, w1, qk, ql);
       hipcub::DoubleBuffer<uint64_t> kb(qk, qk2);

@@ -14,6 +14,9 @@ step spill_tests
 timeout -k 10 700 python -u -m pytest tests/test_gpu_shard_seenspill.py tests/test_gpu_seenspill.py -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/spill_tests.log 2>&1 || { echo SPILL_TESTS_FAIL; tail -40 $O/spill_tests.log; exit 1; }
 tail -3 $O/spill_tests.log
 grep "NP=2" $O/spill_tests.log
+step ablate
+KC_ABLATE=1 timeout -k 10 300 python -u tools/exp_run.py --np 2 --runs 2 > $O/ablate.log 2>&1 || { echo ABLATE_FAIL; tail -20 $O/ablate.log; exit 1; }
+grep "ablate" $O/ablate.log
 step ab
 L=tla-kubernetes_amd/kubecheck/lib
 bash tools/gpu_r03_ab_lib.sh ${TAG}_ab $L/libkubecheck.so $L/libkubecheck_ldsmix.so $L/libkubecheck_bucketlow.so || exit 1
