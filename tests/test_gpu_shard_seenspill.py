@@ -38,7 +38,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("R,budget,tier", [(2, 4 * MiB, "host"), (4, 3 * MiB, "host"), (2, 4 * MiB, "disk"),
-                                           (2, 4 * MiB, "windows"), (3, 4 * MiB, "merge_probe")])
+                                           (2, 4 * MiB, "windows"), (3, 3 * MiB, "merge_probe")])
 def test_shard_seen_spill_model1(fixtures, mcout, tmp_path, monkeypatch, R, budget, tier):
     ref = native(R)
     kw = dict(seen_hbm_bytes=budget)
