@@ -23,6 +23,9 @@ bash tools/gpu_r03_ab_lib.sh ${TAG}_ab $L/libkubecheck.so $L/libkubecheck_ldsmix
 step levels
 timeout -k 10 300 python -u tools/shard_levels.py --np2 > $O/shard_levels.log 2>&1 || { echo LEVELS_FAIL; tail -30 $O/shard_levels.log; exit 1; }
 tail -2 $O/shard_levels.log
+step redo
+timeout -k 10 300 python -u tools/redo_cost.py > $O/redo_cost.log 2>&1 || { echo REDO_FAIL; tail -20 $O/redo_cost.log; exit 1; }
+tail -1 $O/redo_cost.log
 step merge_ab
 for div in 0 16; do
   PYTHONPATH=$R/tla-kubernetes_amd KC_COLD_MERGE_DIV=$div timeout -k 10 200 python -u -c "
