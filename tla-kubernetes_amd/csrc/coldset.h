@@ -102,8 +102,9 @@ class ColdSet {
     bool cache_keys = true;        // copy the newest runs' keys into what HBM budget is left
     // a host run probed by m >= n / merge_div sorted queries is read once,
     // sequentially, by k_cold_merge_probe instead of ~1.2 random 64-B reads
-    // per query (0 = never; KC_COLD_MERGE_DIV overrides)
-    int merge_div = 16;
+    // per query (0 = never, the default: no gain measured on NP=2 under a
+    // 4 GiB seen-set; KC_COLD_MERGE_DIV overrides)
+    int merge_div = 0;
   };
   ColdSet() = default;
   ~ColdSet();

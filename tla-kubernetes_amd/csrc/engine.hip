@@ -874,24 +874,33 @@ class EngineT final : public EngineBase {
       return -EINVAL;
     }
     std::vector<std::pair<uint64_t, uint8_t>> chain;
-    for (;;) {
-      unsigned long long p = 0;
-      uint8_t o = 0;
-      if (cfg_.trace_host) {
-        KC_HIP_TRY(hipStreamSynchronize(st_));
-        p = parent_[g];
-        o = ord_[g];
-      } else {
-        KC_HIP_TRY(hipMemcpy(&p, parent_ + g, 8, hipMemcpyDeviceToHost));
-        KC_HIP_TRY(hipMemcpy(&o, ord_ + g, 1, hipMemcpyDeviceToHost));
+    if (cfg_.trace_host) {
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      for (;;) {
+        const unsigned long long p = parent_[g];
+        chain.push_back({g, ord_[g]});
+        if (p == ~0ull) break;
+        g = p;
+        if (chain.size() > KC_MAX_LEVELS + 2) {
+          set_error("kubecheck: corrupt parent chain");
+          return -EIO;
+        }
       }
-      chain.push_back({g, o});
-      if (p == ~0ull) break;
-      g = p;
-      if (chain.size() > KC_MAX_LEVELS + 2) {
+    } else {
+      // one lane walks the chain in HBM, one readback (instead of two
+      // synchronous 8-B copies per level: the time to a counterexample)
+      constexpr uint32_t cap = KC_MAX_LEVELS + 3;
+      if (!h_chain_) KC_HIP_TRY(hipHostMalloc(&h_chain_, (cap + 1) * 8));
+      hipLaunchKernelGGL(k_parent_chain, dim3(1), dim3(64), 0, st_, parent_, ord_, (uint64_t)g, h_chain_ + 1, cap,
+                         h_chain_);
+      KC_HIP_TRY(hipGetLastError());
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      const uint64_t len = h_chain_[0];
+      if (len == 0 || len > cap) {
         set_error("kubecheck: corrupt parent chain");
         return -EIO;
       }
+      for (uint64_t k = 0; k < len; ++k) chain.push_back({h_chain_[1 + k] >> 8, (uint8_t)(h_chain_[1 + k] & 0xff)});
     }
     std::reverse(chain.begin(), chain.end());
     out.clear();
@@ -991,6 +1000,8 @@ class EngineT final : public EngineBase {
                     (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
+    if (h_chain_) (void)hipHostFree(h_chain_);
+    h_chain_ = nullptr;
     if (h_last_) (void)hipHostFree(h_last_);
     if (d_ns_) (void)hipFree(d_ns_);
     if (d_snap_) (void)hipFree(d_snap_);
@@ -1753,6 +1764,7 @@ class EngineT final : public EngineBase {
   uint64_t scan_cap_ = 0;
   Counters* d_ctr_ = nullptr;
   Counters* h_ctr_ = nullptr;
+  uint64_t* h_chain_ = nullptr;        // pinned: [0] length, then the parent chain (k_parent_chain)
   std::vector<hipEvent_t> ev_pool_;
   std::vector<int> ev_kind_;
   size_t ev_used_ = 0;

@@ -367,6 +367,28 @@ __global__ void __launch_bounds__(256) k_materialize(DeferArgs df, uint64_t n, F
   }
 }
 
+// The parent chain of global state g (TLC's trace-file walk), on the
+// device: one lane follows the parent pointers from g back to its Init
+// state; out[k] = state index << 8 | ordinal, *len = the chain's length
+// (0: longer than cap, a corrupt chain).  Writes pinned host memory.
+static __global__ void k_parent_chain(const unsigned long long* __restrict__ parent, const uint8_t* __restrict__ ord,
+                                      uint64_t g, uint64_t* __restrict__ out, uint32_t cap,
+                                      uint64_t* __restrict__ len) {
+  if (threadIdx.x != 0) return;
+  uint32_t k = 0;
+  for (;;) {
+    if (k >= cap) {
+      *len = 0;
+      return;
+    }
+    const unsigned long long p = parent[g];
+    out[k++] = (g << 8) | (uint64_t)ord[g];
+    if (p == ~0ull) break;
+    g = p;
+  }
+  *len = k;
+}
+
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
 // KC_ABLATE=1): 1 = successors + LDS dedup only, 2 = successors only,
 // 3 = plan + fold only (no successor), 4 = successors with an XOR of their

@@ -40,6 +40,9 @@
 // A/B build switches of the successor loop (k_claim): the single-GPU
 // fingerprint's top bits from the fold (no owner projection), and slot
 // lookup by byte-parallel compares of cumulative counts (locate_cum)
+#ifndef KC_FP_MIX
+#define KC_FP_MIX 2
+#endif
 #ifndef KC_OWN0_FOLD
 #define KC_OWN0_FOLD 1
 #endif
@@ -277,14 +280,14 @@ struct Model {
   }
 
   // IsUnboundPVC over a set of U elements (:444-446): PVC identity, no spec
-  KC_HD static uint64_t unbound(uint64_t set) {
+  // — a fixed subset of U, so one AND
+  static constexpr uint64_t unbound_mask() {
     uint64_t r = 0;
-    for (uint64_t x = set; x; x &= x - 1) {
-      const int u = ctz(x);
-      if (u_id(u) == ID_PVC && !u_spec(u)) r |= 1ull << u;
-    }
+    for (int u = 0; u < U && u < 64; ++u)
+      if (((u >> (A + 1)) & 1) == ID_PVC && !((u >> A) & 1)) r |= 1ull << u;
     return r;
   }
+  KC_HD static uint64_t unbound(uint64_t set) { return set & unbound_mask(); }
   // apiState' = {IF IsVersionOf(o, X) THEN Read(o, c) ELSE o : o \in apiState}
   // restricted to the U bits in `sel`
   KC_HD static uint64_t read_map(uint64_t api, uint64_t sel, int c) {
@@ -717,11 +720,19 @@ struct Model {
     for (int i = 1; i < W_RAW; ++i) r = (k == i) ? salt_c(i) : r;
     return r;
   }
+  // KC_FP_MIX (A/B build switch): 2 = two 64-bit multiplies (the default),
+  // 1 = one, between two xor-shifts (still a bijection of the word)
   KC_HD static uint64_t mix_salted(uint64_t z) {
+#if KC_FP_MIX == 1
+    z ^= z >> 32;
+    z *= 0xd6e8feb86659fd93ull;
+    return z ^ (z >> 29);
+#else
     z *= 0xbf58476d1ce4e5b9ull;
     z ^= z >> 31;
     z *= 0x94d049bb133111ebull;
     return z ^ (z >> 29);
+#endif
   }
   KC_HD static uint64_t word_mix(uint64_t w, int k) { return mix_salted(w ^ salt(k)); }
   KC_HD static uint64_t fp_fold(const State& s) {
