@@ -1135,7 +1135,7 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL(k_sn_recv<M>, dim3(rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_, d_ctr_);
     hipLaunchKernelGGL(k_sn_claim<M>, dim3(SN_CWG + rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_,
                        cs_.t, cs_.nslots, d_ctr_);
-    hipLaunchKernelGGL(k_sn_emit<M>, dim3(SN_PWG + rgrid), dim3(SN_THREADS), 0, st_, cur_, next_, flags_, lev, d_snc_,
+    hipLaunchKernelGGL(k_sn_emit<M>, dim3(SN_EWG + rgrid), dim3(SN_THREADS), 0, st_, cur_, next_, flags_, lev, d_snc_,
                        d_sns_, sn_recv_, pkeys_, d_ctr_);
     KC_HIP_TRY(hipGetLastError());
     return 0;

@@ -66,6 +66,8 @@ constexpr int SN_XWG = SN_MAX * SN_SUB / SN_THREADS;
 constexpr int SN_ESUB = 4;                                   // k_sn_claim lanes per parent
 constexpr int SN_CWG = SN_MAX * SN_ESUB / SN_THREADS;
 constexpr int SN_PWG = SN_MAX / SN_THREADS;                  // lane = parent kernels
+constexpr int SN_EMSUB = 4;                                  // k_sn_emit lanes per parent (own new states)
+constexpr int SN_EWG = SN_MAX * SN_EMSUB / SN_THREADS;
 constexpr uint64_t SN_CAND_MAX = 32768;                      // own successors of a narrow level
 constexpr int SN_MAX_R = 16;
 constexpr uint32_t SN_SLOT_MAX = 4096;                       // records per peer slot (upper bound)
@@ -76,7 +78,7 @@ constexpr int SN_NLT = 3;
 constexpr int SN_LT_PROBES = 256;
 constexpr int SN_BATCH = 32;                                 // levels enqueued per host sync
 static_assert((uint64_t)SN_MAX * 32 < (1u << 20), "keys: parent 13 bits, t 5 bits");
-static_assert(SN_PWG + SN_MAX_R * SN_SLOT_MAX / SN_THREADS < 512 &&
+static_assert(SN_EWG + SN_MAX_R * SN_SLOT_MAX / SN_THREADS < 512 &&
               SN_CAND_MAX + (uint64_t)SN_MAX_R * SN_SLOT_MAX < (1u << 20), "k_sn_emit's arrival word");
 
 enum SNReason : int { SN_RUN = 0, SN_ERROR = 1, SN_DONE = 2, SN_STOP = 3 };
@@ -560,11 +562,14 @@ k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, co
   if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&stripe(C).probes, probes);
 }
 
-// grid SN_PWG + ceil(world * cap / SN_THREADS): the new states (own in
+// grid SN_EWG + ceil(world * cap / SN_THREADS): the new states (own in
 // parent order, then the records' by sender and slot order), each at its
 // position: a workgroup sums the new-state counts before its own first (at
 // most 8192 parents and 15 x 4096 records: cheaper than a scan launch).
-// The last workgroup to finish closes the level.
+// Own new states: SN_EMSUB adjacent lanes per parent, lane `sub` taking the
+// parent's new states of rank sub, sub + SN_EMSUB, ... (a narrow level's
+// time is one lane's serial chain: measured 11.4 us per Model_1 level with
+// one lane per parent).  The last workgroup to finish closes the level.
 template <class M>
 __global__ void __launch_bounds__(SN_THREADS)
 k_sn_emit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bufB, Flags f, uint32_t lev,
@@ -588,8 +593,8 @@ k_sn_emit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
     sh_sum[0] = sh_sum[1] = 0;
   }
   __syncthreads();
-  const bool own = blockIdx.x < (unsigned)SN_PWG;
-  const uint64_t rfirst = own ? 0 : (uint64_t)(blockIdx.x - SN_PWG) * SN_THREADS;   // flattened record index
+  const bool own = blockIdx.x < (unsigned)SN_EWG;
+  const uint64_t rfirst = own ? 0 : (uint64_t)(blockIdx.x - SN_EWG) * SN_THREADS;   // flattened record index
   auto rec_new = [&](uint64_t g) -> uint32_t {          // 1 if flattened record g is a new state
     const uint32_t s = (uint32_t)(g / cap), k = (uint32_t)(g % cap);
     if (s >= world || s == rank) return 0u;
@@ -597,7 +602,7 @@ k_sn_emit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
   };
   // [0]: new states before this workgroup's first; [1] (records): all own new states
   {
-    const uint64_t pend = own ? (uint64_t)blockIdx.x * SN_THREADS : n;
+    const uint64_t pend = own ? (uint64_t)blockIdx.x * (SN_THREADS / SN_EMSUB) : n;
     uint32_t a = 0, r = 0;
     for (uint64_t j = threadIdx.x; j < pend && j < n; j += SN_THREADS) a += (uint32_t)__builtin_popcount(sc->newmask[j]);
     if (!own)
@@ -616,16 +621,21 @@ k_sn_emit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
     cand += (unsigned long long)M::plan(x, f).total;
   };
   if (own) {
-    const uint64_t i = (uint64_t)blockIdx.x * SN_THREADS + threadIdx.x;
+    const uint64_t gl = (uint64_t)blockIdx.x * SN_THREADS + threadIdx.x;
+    const uint64_t i = gl / SN_EMSUB;
+    const uint32_t sub = (uint32_t)(gl % SN_EMSUB);
     uint32_t m = i < n ? sc->newmask[i] : 0u;
     uint32_t total;
-    const uint32_t e = sn_block_scan((uint32_t)__builtin_popcount(m), lds, total);
+    // the parent's count once (its lane 0), its base to all its lanes
+    const uint32_t e0 = sn_block_scan(sub == 0 ? (uint32_t)__builtin_popcount(m) : 0u, lds, total);
+    const uint32_t e = (uint32_t)__shfl((int)e0, (int)((threadIdx.x & 63u) & ~(uint32_t)(SN_EMSUB - 1)), 64);
     wnew = total;
+    for (uint32_t k = 0; k < sub && m; ++k) m &= m - 1;      // skip to the lane's first rank
     if (m) {
       const State s = load_state<M>(cur, i);
       const typename M::Plan pl{sc->pcnt[i], 0, -1, -1};
-      uint64_t o = (uint64_t)sh_sum[0] + e;
-      for (; m; m &= m - 1, ++o) {
+      uint64_t o = (uint64_t)sh_sum[0] + e + sub;
+      while (m) {
         const int t = __ffs(m) - 1;
         int slot, j;
         M::locate(pl, t, slot, j);
@@ -633,6 +643,8 @@ k_sn_emit(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
         M::apply(s, slot, j, f, x);
         const uint64_t act = (uint64_t)M::slot_action(s, slot);
         emit(x, o, ((uint64_t)rank << 60) | (i << 16) | ((uint64_t)t << 8) | act, act);
+        for (int k = 0; k < SN_EMSUB && m; ++k) m &= m - 1;  // the lane's next rank
+        o += SN_EMSUB;
       }
     }
   } else {
