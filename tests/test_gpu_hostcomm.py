@@ -30,6 +30,7 @@ CASES = [
     {"name": "ns0", "kw": {"ns": 0}},
     # each process's seen-set under a 3 MiB HBM budget (shard.hip spill_*)
     {"name": "seen_spill", "kw": {"seen_hbm_bytes": 3 << 20}},
+    {"name": "np2_40_seen_spill", "kw": {"np": 2, "max_levels": 40, "seen_hbm_bytes": 16 << 20}},
     {"name": "lost_update", "kw": {"variant": 1, "invariants": 7}},
     {"name": "fault_pack", "kw": {}, "env": {"KC_FAULT": "1:7:1"}, "all_ranks": True},
     {"name": "fault_expand_hostrows", "kw": {}, "env": {"KC_FAULT": "0:9:0", "KC_DEVROW": "0"}, "all_ranks": True},
@@ -94,9 +95,12 @@ def test_seen_spill_exact(results, fixtures):
 def test_np2_prefix_exact(results, fixtures):
     _, res = results
     fx = fixtures["np2_40levels"]
-    r = res["np2_40"][0]
-    assert r["level_width"] == fx["level_width"] and not r["complete"]
-    assert r["act_gen"] == fx["act_gen"]
+    for name in ("np2_40", "np2_40_seen_spill"):
+        r = res[name][0]
+        assert "exception" not in r, r.get("exception")
+        assert r["level_width"] == fx["level_width"] and not r["complete"], name
+        assert r["act_gen"] == fx["act_gen"], name
+    assert res["np2_40_seen_spill"][0]["seen_flushes"] >= 2
 
 
 @pytest.mark.parametrize("key,name,kind", [("nc2", "nc2", "assertion"), ("variant2", "variant2", "invariant"),

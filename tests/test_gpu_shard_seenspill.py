@@ -91,3 +91,27 @@ def test_shard_seen_spill_np2_full_r4(fixtures):
     assert r["seen_flushes"] > 4 and r["seen_cold_hits"] > 0
     print(f"\nNP=2 sharded R=4, seen-set 1 GiB per rank: {r['seconds']:.2f} s, flushes {r['seen_flushes']}, "
           f"cold fps {r['seen_cold_fps']}, queries {r['seen_cold_queries']}, hits {r['seen_cold_hits']}")
+
+
+def test_shard_seen_spill_np2_lost_update(fixtures):
+    # NP=2's resourceVersion race (variant 1, NoLostUpdate; BASELINE config
+    # 5) through 2 ranks whose seen-sets hold 2 MiB each: the error, its level
+    # and its trace are the unbounded sharded run's and the oracle's
+    kw = dict(np=2, variant=1, invariants=7)
+    ref = native(2, **kw)
+    r = native(2, **kw, seen_hbm_bytes=2 * MiB)
+    fx = fixtures["np2_variant1_lost_update"]
+    assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate"
+    assert (r["error_level"], r["trace_len"]) == (fx["err_level"], fx["trace_len"])
+    _same(r, ref)
+    assert r["seen_flushes"] >= 2 and r["seen_cold_hits"] > 0
+
+
+def test_shard_seen_spill_np2_prefix(fixtures):
+    # NP=2's first 40 levels (1.7M states) at 2 ranks under 16 MiB each:
+    # several flushes per rank and cold checks in several windows a level
+    fx = fixtures["np2_40levels"]
+    r = native(2, np=2, max_levels=40, keep_trace=False, seen_hbm_bytes=16 * MiB)
+    assert r["level_width"] == fx["level_width"]
+    assert r["act_gen"] == fx["act_gen"] and r["act_dist"] == fx["act_dist"]
+    assert r["seen_flushes"] >= 4 and r["seen_cold_hits"] > 0
