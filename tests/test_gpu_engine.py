@@ -304,18 +304,25 @@ def test_deferred_capacity_estimate_redo(fixtures, monkeypatch):
     assert (r0.level_width, r0.act_gen, r0.act_dist) == (r.level_width, r.act_gen, r.act_dist)
 
 
+@pytest.mark.parametrize("direct", ["1", "0"])
 @pytest.mark.parametrize("key,kw", [("variant3", dict(variant=3)), ("variant2", dict(variant=2))])
-def test_deferred_error_redone_exactly(fixtures, monkeypatch, key, kw):
-    # an error on a deferred wide level (Model_1 on the wide path): the run
-    # is redone on the materialising path from the level the error belongs
-    # to — an Assert is found among the level's own parents (that level),
-    # an invariant among the states the level rebuilt (the previous level's
-    # emit would have found it) — trace state for state
+def test_deferred_error_redone_exactly(fixtures, monkeypatch, key, kw, direct):
+    # an error on a deferred wide level (Model_1 on the wide path).  An
+    # Assert is found among the level's own parents: the run is redone on
+    # the materialising path from that level.  An invariant violation among
+    # the states the level rebuilt (the previous level's emit would have
+    # found it) is reported directly — the lowest rebuilt index, counters and
+    # ClaimSet put back as that emit left them (KC_DEFER_DIRECT=0: redone from
+    # the previous level instead).  Trace state for state either way.
+    monkeypatch.setenv("KC_DEFER_DIRECT", direct)
     fx = fixtures[key]
     with ModelChecker(ModelConfig(chunk_states=1 << 20, **kw)) as mc:
         r = mc.run()
-    assert r.defer_fallback
-    assert r.defer_redo_level == fx["err_level"] - (1 if r.error == "invariant" else 0)
+    if key == "variant2" and direct == "1":
+        assert r.error == "invariant" and not r.defer_fallback and r.defer_redo_level == 0
+    else:
+        assert r.defer_fallback
+        assert r.defer_redo_level == fx["err_level"] - (1 if r.error == "invariant" else 0)
     assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
     assert [list(map(int, t)) for t in r.trace] == fx["trace"]
     # every partial count as the exact (materialising) path reports it
@@ -323,8 +330,26 @@ def test_deferred_error_redone_exactly(fixtures, monkeypatch, key, kw):
     with ModelChecker(ModelConfig(chunk_states=1 << 20, **kw)) as mc:
         e = mc.run()
     assert not e.defer_fallback and e.deferred_states == 0
-    for k in ("distinct", "generated", "level_width", "act_gen", "act_dist", "outdeg_hist", "error_level"):
+    for k in ("distinct", "generated", "depth", "level_width", "act_gen", "act_dist", "outdeg_hist", "error_level",
+              "error_invariant", "trace_len", "complete", "queue_left"):
         assert getattr(r, k) == getattr(e, k), k
+    assert [list(map(int, t)) for t in r.trace] == [list(map(int, t)) for t in e.trace]
+
+
+def test_deferred_invariant_np2_lost_update(fixtures, monkeypatch):
+    # NP=2's resourceVersion race (NoLostUpdate, depth 25) found among a
+    # deferred level's rebuilt states: reported without a redo, everything
+    # as the materialising path reports it
+    fx = fixtures["np2_variant1_lost_update"]
+    r = run(np=2, variant=1, invariants=7)
+    assert r.error_invariant == "NoLostUpdate" and not r.defer_fallback
+    assert (r.error_level, r.trace_len) == (fx["err_level"], fx["trace_len"])
+    monkeypatch.setenv("KC_DEFER", "0")
+    e = run(np=2, variant=1, invariants=7)
+    for k in ("distinct", "generated", "depth", "level_width", "act_gen", "act_dist", "outdeg_hist", "error_level",
+              "trace_len"):
+        assert getattr(r, k) == getattr(e, k), k
+    assert [list(map(int, t)) for t in r.trace] == [list(map(int, t)) for t in e.trace]
 
 
 def test_deferred_trace_in_host_memory(fixtures):

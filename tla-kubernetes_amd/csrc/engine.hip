@@ -84,6 +84,7 @@ k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ new
       C->overflow = 0;
       C->batch_used = 0;
       C->defer_flags = 0;
+      C->defer_inv_n = 0;
     }
   }
 }
@@ -98,6 +99,7 @@ __global__ void k_level_reset(Counters* __restrict__ C) {
     C->overflow = 0;
     C->batch_used = 0;
     C->defer_flags = 0;
+    C->defer_inv_n = 0;
   }
 }
 
@@ -192,6 +194,8 @@ class EngineT final : public EngineBase {
     pc_pass_ = !(dp && dp[0] == '0');
     const char* dr = getenv("KC_DEFER_REDO");      // KC_DEFER_REDO=0: an anomaly redoes the run from Init
     redo_on_ = !(dr && dr[0] == '0');
+    const char* dd = getenv("KC_DEFER_DIRECT");    // KC_DEFER_DIRECT=0: invariant anomalies are redone too (A/B)
+    defer_direct_ = !(dd && dd[0] == '0');
     const char* ds = getenv("KC_DEFER_SLACK");
     if (ds && atof(ds) > 0) defer_slack_ = atof(ds);
     if (defer_) tscan_ = true;    // the link emit takes the tile offsets
@@ -581,6 +585,17 @@ class EngineT final : public EngineBase {
         // the previous level's error (its emit would have found it); the
         // rest (Assert / deadlock keys of this level's parents, a capacity
         // estimate too small) are this level's
+        if (c.defer_flags == DF_INVARIANT && !c.overflow && !c.batch_used && defer_direct_) {
+          // an invariant violation among this level's rebuilt states and
+          // nothing else: reported as the previous level's emit would have
+          // (no redo), unless the snapshots it needs are missing
+          const int rc = report_deferred_invariant(res, level, level_gidx, n);
+          if (rc < 0) return rc;
+          if (rc == 0) {
+            finish(res, t0, 0);
+            return 0;
+          }
+        }
         const int X = (c.defer_flags & DF_INVARIANT) ? level - 1 : level;
         const uint64_t dc_here = c.cand_total - cand_total;
         if (!redo_from(X, level, mat, dc_here, res, n, level_gidx, cand, prev_gidx, cand_total, ratio)) return kDeferRetry;
@@ -1200,6 +1215,46 @@ class EngineT final : public EngineBase {
   int succ_lv_[3] = {-1, -1, -1};
   int exact_until_ = 0;               // levels <= this run on the exact path (after a redo)
   bool redo_on_ = true;               // KC_DEFER_REDO=0: an anomaly redoes the run from Init
+  bool defer_direct_ = true;          // KC_DEFER_DIRECT=0: an invariant anomaly is redone too
+
+  // Level L's k_claim rebuilt a state violating an invariant (and found
+  // nothing else): the error TLC reports is the first such state of level L
+  // in BFS order, the lowest rebuilt index (defer_inv_n).  The materialising
+  // path finds it in level L - 1's emit and stops there, so the result is
+  // put back as that emit left it: counters of level L - 1 (its k_advance
+  // snapshot) with level L's per-action distinct counts (counted here by the
+  // rebuild), level L's claims of level L + 1 dropped from the ClaimSet, L - 1
+  // levels expanded; the trace is the path to the state through the parent
+  // pointers.  1: not possible here (the caller redoes from L - 1).
+  int report_deferred_invariant(kc_result* res, int L, uint64_t level_gidx, uint64_t n) {
+    if (!cfg_.keep_trace || headcopy_ || !d_snap_ || L < 2 || snap_lv_[(L - 1) % 3] != L - 1) return 1;
+    unsigned long long inv_n = 0;
+    KC_HIP_TRY(hipMemcpy(&inv_n, &d_ctr_->defer_inv_n, 8, hipMemcpyDeviceToHost));
+    if (!inv_n) return 1;
+    const uint64_t idx = ~(uint64_t)inv_n;
+    if (idx >= n) {
+      set_error("kubecheck: deferred invariant index %llu past the level's %llu states", (unsigned long long)idx,
+                (unsigned long long)n);
+      return -EIO;
+    }
+    KC_TRY(counter_snap(L));
+    hipLaunchKernelGGL(k_counters_restore, dim3(1), dim3(64), 0, st_, d_ctr_, d_snap_[(L - 1) % 3].s,
+                       d_snap_[L % 3].s);
+    hipLaunchKernelGGL(k_claimset_drop, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t, cs_.nslots,
+                       (uint32_t)L + 1);
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    std::vector<State> path;
+    KC_TRY(path_to(level_gidx + idx, path));
+    res->err_kind = E_INVARIANT;
+    res->err_invariant = M::check(path.back(), flags_.inv_mask);
+    res->err_level = L;
+    res->nlevels = L - 1;
+    res->level_width[L - 1] = 0;
+    trace_ = path;
+    res->trace_len = (int)path.size();
+    return 0;
+  }
 
   // The counters after level `lv` (end of a narrow run, or the start) into
   // snapshot lv mod 3.

@@ -58,7 +58,8 @@ struct Counters {
   unsigned long long level_new;   // sharded insert: new states of the level (local + records)
   unsigned long long emit_done;   // sharded insert: emit workgroups done (the last one reads the totals)
   unsigned long long defer_flags; // deferred frontier (DeferArgs): DF_* bits of the level
-  unsigned long long head_pad[8];
+  unsigned long long defer_inv_n; // ... ~(lowest index of a rebuilt state violating an invariant); 0 = none
+  unsigned long long head_pad[7];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -338,7 +339,10 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
   typename M::State s;
   M::apply(gp, slot, j, f, s);
   store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
-  if (M::check(s, f.inv_mask) >= 0) atomicOr(&C->defer_flags, DF_INVARIANT);
+  if (M::check(s, f.inv_mask) >= 0) {
+    atomicOr(&C->defer_flags, DF_INVARIANT);
+    atomicMax(&C->defer_inv_n, ~(unsigned long long)i);   // the level's first violator in BFS order
+  }
   atomicAdd(&sh_actd[M::slot_action(gp, slot) * AS + (threadIdx.x & (AS - 1))], 1u);
   return s;
 }

@@ -1,9 +1,11 @@
 """Time-to-counterexample with the deferred frontier:
-NP=2 with the seeded resourceVersion race (variant 1, NoLostUpdate) fails on
-a deferred level and is redone from that level on the materialising path
-(engine.hip run / redo_from).  Compared with a clean check of the same model
-to the same depth (variant 0, max_levels = the error's depth) and with the
-whole run on the materialising path (KC_DEFER=0).
+NP=2 with the seeded resourceVersion race (variant 1, NoLostUpdate) fails
+among a deferred level's rebuilt states: reported directly (engine.hip
+report_deferred_invariant), or with KC_DEFER_DIRECT=0 redone from the
+previous level on the materialising path (redo_from).  Compared with a clean
+check of the same model to the same depth (variant 0, max_levels = the
+error's depth) and with the whole run on the materialising path
+(KC_DEFER=0).
 
   python tools/redo_cost.py [--reps 3]"""
 import argparse
@@ -50,11 +52,15 @@ def main():
     r_m, t_mat = timed(bug, a.reps, {"KC_DEFER": "0"})
     assert (r_m.error_level, r_m.trace_len) == (r.error_level, r.trace_len)
     assert [list(map(int, x)) for x in r_m.trace] == [list(map(int, x)) for x in r.trace]
+    r_r, t_redo = timed(bug, a.reps, {"KC_DEFER_DIRECT": "0"})
+    assert [list(map(int, x)) for x in r_r.trace] == [list(map(int, x)) for x in r.trace]
     _, t_clean = timed(dict(np=2, invariants=7, max_levels=depth), a.reps)
-    out = {"error_level": depth, "trace_len": r.trace_len, "redo_level": r.defer_redo_level,
-           "ms_deferred_with_redo": round(t_bug * 1e3, 2), "ms_materialising": round(t_mat * 1e3, 2),
-           "ms_clean_to_depth": round(t_clean * 1e3, 2),
-           "redo_over_clean": round(t_bug / t_clean, 3), "materialising_over_clean": round(t_mat / t_clean, 3)}
+    out = {"error_level": depth, "trace_len": r.trace_len, "redo_level_direct": r.defer_redo_level,
+           "redo_level_redo": r_r.defer_redo_level,
+           "ms_deferred_direct": round(t_bug * 1e3, 2), "ms_deferred_with_redo": round(t_redo * 1e3, 2),
+           "ms_materialising": round(t_mat * 1e3, 2), "ms_clean_to_depth": round(t_clean * 1e3, 2),
+           "direct_over_clean": round(t_bug / t_clean, 3), "redo_over_clean": round(t_redo / t_clean, 3),
+           "materialising_over_clean": round(t_mat / t_clean, 3)}
     print(json.dumps(out))
 
 
