@@ -79,6 +79,7 @@ k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ new
       host[4] = C->cand_total;
       host[5] = C->level_new;
       host[7] = C->defer_flags;
+      host[8] = C->defer_inv_n;        // (Counters::defer_inv_n of the pinned copy)
       C->err_key = ~0ull;
       C->chunk_base = 0;
       C->overflow = 0;
@@ -1228,8 +1229,8 @@ class EngineT final : public EngineBase {
   // pointers.  1: not possible here (the caller redoes from L - 1).
   int report_deferred_invariant(kc_result* res, int L, uint64_t level_gidx, uint64_t n) {
     if (!cfg_.keep_trace || headcopy_ || !d_snap_ || L < 2 || snap_lv_[(L - 1) % 3] != L - 1) return 1;
-    unsigned long long inv_n = 0;
-    KC_HIP_TRY(hipMemcpy(&inv_n, &d_ctr_->defer_inv_n, 8, hipMemcpyDeviceToHost));
+    // (k_advance copied it with the level head and reset it)
+    const unsigned long long inv_n = h_ctr_->defer_inv_n;
     if (!inv_n) return 1;
     const uint64_t idx = ~(uint64_t)inv_n;
     if (idx >= n) {

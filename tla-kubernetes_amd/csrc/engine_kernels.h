@@ -59,6 +59,7 @@ struct Counters {
   unsigned long long emit_done;   // sharded insert: emit workgroups done (the last one reads the totals)
   unsigned long long defer_flags; // deferred frontier (DeferArgs): DF_* bits of the level
   unsigned long long defer_inv_n; // ... ~(lowest index of a rebuilt state violating an invariant); 0 = none
+                                  // (word 8: k_advance copies it to the host with the head)
   unsigned long long head_pad[7];
   CtrStripe s[CTR_STRIPES];
 
@@ -103,6 +104,8 @@ struct Counters {
 // cand_total, level_new, emit_done, defer_flags): what the host reads back
 // after every level
 constexpr size_t kCtrHead = 8 * sizeof(unsigned long long);
+static_assert(offsetof(Counters, defer_flags) == 7 * 8 && offsetof(Counters, defer_inv_n) == 8 * 8,
+              "k_advance's host copy indexes the head words");
 // defer_flags: a rebuilt frontier state violates an invariant; a level's
 // links or trace entries did not fit the capacity the host estimated
 constexpr unsigned long long DF_INVARIANT = 1, DF_CAPACITY = 2;
