@@ -113,8 +113,11 @@ def test_shard_seen_spill_np2_lost_update(fixtures, R):
 def test_shard_seen_spill_np2_prefix(fixtures):
     # NP=2's first 40 levels (1.7M states) at 2 ranks under 16 MiB each:
     # several flushes per rank and cold checks in several windows a level
+    # (per-action distinct counts follow the ranks' claim order, not the
+    # oracle's FIFO order: compared with the unbounded run at 2 ranks)
     fx = fixtures["np2_40levels"]
     r = native(2, np=2, max_levels=40, keep_trace=False, seen_hbm_bytes=16 * MiB)
+    ref = native(2, np=2, max_levels=40, keep_trace=False)
     assert r["level_width"] == fx["level_width"]
-    assert r["act_gen"] == fx["act_gen"] and r["act_dist"] == fx["act_dist"]
+    assert r["act_gen"] == fx["act_gen"] and r["act_dist"] == ref["act_dist"]
     assert r["seen_flushes"] >= 4 and r["seen_cold_hits"] > 0
