@@ -258,7 +258,7 @@ struct ShardArgs {
   uint32_t world = 1, rank = 0;
   uint32_t spread = CLAIM_SPREAD; // tile order strided by `spread` (spread_tile); 0 = block order
   uint32_t* repmask = nullptr;   // [n]: remote representatives of each parent
-  uint32_t* cnt = nullptr;       // [world][n]: remote representatives per owner and parent
+  uint8_t* cnt = nullptr;        // [world][n]: remote representatives per owner and parent (<= 32: 8 bits)
   CandOvf ovf;
 };
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
@@ -753,7 +753,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   if (SH && live) {
     sh.repmask[i] = sh_rep[threadIdx.x];
     for (uint32_t o = 0; o < sh.world; ++o)
-      sh.cnt[(uint64_t)o * n + i] = (sh_cnt[(o >> 2) * CLAIM_TILE + threadIdx.x] >> (8 * (o & 3))) & 0xffu;
+      sh.cnt[(uint64_t)o * n + i] = (uint8_t)((sh_cnt[(o >> 2) * CLAIM_TILE + threadIdx.x] >> (8 * (o & 3))) & 0xffu);
   }
   unsigned long long pw = probes;
 #pragma unroll

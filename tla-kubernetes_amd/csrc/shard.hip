@@ -110,7 +110,8 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
   }
 }
 
-// Records per owner from the owner-major exclusive scan of cnt[world][n].
+// Records per owner from the owner-major exclusive scan of cnt[world][n]
+// (8-bit counts: a parent has at most 32 successors).
 // Owner totals (world > 1; 0 at world 1) into tot and straight into pinned
 // host memory, with the level head (error key, overflow flags): what the
 // host reads after expand, with no copy launches.
@@ -142,7 +143,7 @@ __global__ void k_head_reset(Counters* __restrict__ C, unsigned long long* __res
 // memory: totals, status_new, status_err (level 1: an Init-state invariant
 // key, 0x12, found by expand takes the status slot, as Group::run does), and
 // the failure word.
-__device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+__device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, const uint8_t* __restrict__ cnt,
                                              uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
                                              const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
                                              unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
@@ -176,13 +177,18 @@ __device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, c
   host_tot[o] = v;
   if (row && o < world) row[o] = v;
 }
-__global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+__global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint8_t* __restrict__ cnt,
                                uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
                                const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
                                unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
                                uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err) {
   owner_totals(off, cnt, n, world, tot, C, host_tot, host_head, row, status_new, status_err, level1, init_err);
 }
+
+// 8-bit per-owner counts widened for the owner-major scan
+struct Widen8 {
+  __host__ __device__ __forceinline__ uint32_t operator()(uint8_t v) const { return v; }
+};
 
 // Record flags: 0 = out, 1 = candidate, 2 = inserted its fp, 3 = displacer.
 enum : unsigned int { RF_OUT = 0, RF_CAND = 1, RF_INSERTER = 2, RF_DISPLACER = 3 };
@@ -291,7 +297,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 // launches and the totals launch).
 constexpr uint64_t OWNER_SMALL_SCAN = 16384;
 __global__ void __launch_bounds__(1024)
-k_owner_scan_small(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off, uint64_t n, uint32_t world,
+k_owner_scan_small(const uint8_t* __restrict__ cnt, uint32_t* __restrict__ off, uint64_t n, uint32_t world,
                    uint64_t* __restrict__ tot, const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
                    unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row, uint64_t status_new,
                    uint64_t status_err, int level1, uint64_t init_err) {
@@ -300,7 +306,7 @@ k_owner_scan_small(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off,
   uint32_t carry = 0, total = 0;
   for (uint64_t b = 0; b < cells; b += blockDim.x) {
     const uint64_t i = b + threadIdx.x;
-    const uint32_t v = i < cells ? cnt[i] : 0u;
+    const uint32_t v = i < cells ? (uint32_t)cnt[i] : 0u;
     const uint32_t e = block_exclusive_scan(v, lds, total);
     if (i < cells) off[i] = carry + e;
     carry += total;
@@ -703,9 +709,10 @@ class ShardT final : public ShardBase {
     } else {
       if (world_ > 1) {
         size_t tmp_bytes = 0;
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt_, off_, (int)cells, st_));
+        const hipcub::TransformInputIterator<uint32_t, Widen8, const uint8_t*> cnt32(cnt_, Widen8());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt32, off_, (int)cells, st_));
         KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
-        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt_, off_, (int)cells, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt32, off_, (int)cells, st_));
       }
       hipLaunchKernelGGL(k_owner_totals, dim3(1), dim3(64), 0, st_, off_, cnt_, n_, (uint32_t)world_,
                          d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
@@ -1269,7 +1276,8 @@ class ShardT final : public ShardBase {
   unsigned long long* pkeys_ = nullptr;
   uint64_t pk_cap_ = 0;
   // expand: owner counts / scan, remote representatives, local claim tiles
-  uint32_t *cnt_ = nullptr, *off_ = nullptr, *repmask_ = nullptr, *newmask_ = nullptr, *offsets_ = nullptr;
+  uint8_t* cnt_ = nullptr;
+  uint32_t *off_ = nullptr, *repmask_ = nullptr, *newmask_ = nullptr, *offsets_ = nullptr;
   uint64_t cnt_cap_ = 0, off_cap_ = 0, rm_cap_ = 0, mask_cap_ = 0, offsets_cap_ = 0;
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;
   unsigned long long* rec_fp_ = nullptr;
