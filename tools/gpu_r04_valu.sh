@@ -24,7 +24,7 @@ for f in glob.glob(O + "/p1/**/*counter_collection.csv", recursive=True):
         n = r["Kernel_Name"]
         if "k_claim" not in n and "k_emit" not in n:
             continue
-        m = re.search(r"k_claim<[^,]*, (\d)", n)
+        m = re.search(r"k_claim<kc::Model<[^>]*>, (\d)", n)
         k = ("k_claim ABL" + m.group(1)) if m else re.sub(r"\(.*$", "", n)[:60]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, v in sorted(agg.items()):
