@@ -171,6 +171,15 @@ constexpr int CLAIM_TILE = 256;
 #ifndef KC_CLAIM_BATCH
 #define KC_CLAIM_BATCH 2
 #endif
+// KC_CLAIM_PIPE (default 1; 0 for A/B): the CASes of a group's
+// representatives whose first slot read empty are issued back to back as
+// well, before any result is used (one round trip for the group's inserts
+// instead of one each).  Same box, NP=2: k_claim 103.2-103.9 ms per check
+// against 103.9-105.3 (profiles/r04p_claim_pipe_ab.txt); with groups of 3
+// 105.4 (not kept).
+#ifndef KC_CLAIM_PIPE
+#define KC_CLAIM_PIPE 1
+#endif
 constexpr int CLAIM_LDS_BITS = 11;
 constexpr int CLAIM_LDS = 1 << CLAIM_LDS_BITS;   // entries (fp 8 B + key 4 B)
 // Candidate records (claimants whose claim may win): fp + tile-local key
@@ -719,6 +728,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         eq[q] = claimset_first(cs, iq[q]);
       }
     }
+#if KC_CLAIM_PIPE
+    unsigned long long cq[KC_CLAIM_BATCH];     // CAS results (~0: no CAS issued)
+#pragma unroll
+    for (int q = 0; q < KC_CLAIM_BATCH; ++q) {
+      const int k = k0 + q * CLAIM_TILE;
+      cq[q] = ~0ull;
+      if (k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank) && eq[q].x == 0ull)
+        cq[q] = atomicCAS(&cs[iq[q]].fp, 0ull, fpq[q]);
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < KC_CLAIM_BATCH; ++q) {
       const int k = k0 + q * CLAIM_TILE;
@@ -736,8 +755,21 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         }
       }
       ++probes;
+#if KC_CLAIM_PIPE
+      int r;
+      const uint64_t claim = make_claim(level, kbase | (pidx << 8) | t);
+      if (cq[q] == 0ull) {                        // this lane's CAS inserted fp (fingerprints are never ~0)
+        __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r = CL_NEW;
+      } else {
+        ulonglong2 e = eq[q];
+        if (cq[q] != ~0ull) e = make_ulonglong2(cq[q], 0ull);   // another claimant's fp took the slot first
+        r = claimset_claim_store_from(cs, nbuckets, fp, claim, level, iq[q], e);
+      }
+#else
       const int r = claimset_claim_store_from(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level,
                                               iq[q], eq[q]);
+#endif
       KC_DIAG_OUT(r);
       if (r == CL_NEW)
         atomicOr(&sh_cur[lp], 1u << t);
