@@ -145,6 +145,38 @@ def roofline_bfs(times, res, S):
     }
 
 
+def op_rate_roofline(kclaim_ms: float, probes: int, inserts: int) -> dict:
+    """The roofline that bounds k_claim: its random
+    memory OPERATIONS, each priced at the rate it runs at alone on this GPU
+    (tools/microbench/pmc_calib.hip, profiles/r02b_pmc_calibration.json:
+    random 16-B load, random 64-bit CAS, random agent-scope 8-B store over a
+    32 GiB table).  Per check: every ClaimSet probe is one first-slot load;
+    every inserted state one CAS and one claim store (the STORE-claim
+    protocol).  `serial_ms` is what those operations take one
+    kind after another at the isolated rates; frac = serial_ms / kernel time
+    (> 1: the kernel overlaps the three kinds beyond their isolated sum)."""
+    cal = {"probe": 44.93e9, "cas": 17.11e9, "store": 22.21e9}
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02b_pmc_calibration.json")) as fh:
+            sh = json.load(fh)["shapes"]
+        cal = {"probe": sh["c_rand_load16"]["G_per_s"] * 1e9, "cas": sh["c_rand_cas_new"]["G_per_s"] * 1e9,
+               "store": sh["c_rand_store_agent"]["G_per_s"] * 1e9}
+    except (OSError, ValueError, KeyError):
+        pass
+    t = kclaim_ms * 1e-3
+    serial = probes / cal["probe"] + inserts / cal["cas"] + inserts / cal["store"]
+    return {"bound": "random-op rate", "kernel": "k_claim", "kernel_ms": round(kclaim_ms, 3),
+            "probes": int(probes), "probes_per_s": round(probes / t, 1) if t else 0.0,
+            "probe_peak_per_s": cal["probe"], "probe_frac": round(probes / t / cal["probe"], 4) if t else 0.0,
+            "cas": int(inserts), "cas_per_s": round(inserts / t, 1) if t else 0.0, "cas_peak_per_s": cal["cas"],
+            "cas_frac": round(inserts / t / cal["cas"], 4) if t else 0.0,
+            "claim_stores": int(inserts), "stores_per_s": round(inserts / t, 1) if t else 0.0,
+            "store_peak_per_s": cal["store"], "store_frac": round(inserts / t / cal["store"], 4) if t else 0.0,
+            "serial_ms": round(serial * 1e3, 3), "frac": round(serial / t, 4) if t else 0.0,
+            "source": "profiles/r02b_pmc_calibration.json (isolated rates, 32 GiB table); inserts = the "
+                      "check's new states (each one CAS + one claim store), probes = kc_result.fpset_probes"}
+
+
 def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     summary for this workload (profiles/<round>_<workload>_rocprof_summary.json,
@@ -346,6 +378,8 @@ def bench_single(args, kw, desc):
         # k_claim streams its parents (S B each); everything else it reads is a random probe
         stream = acc["parents"] * S / max(times["expand"][1], 1) if roof["kernel"] == "k_claim" else 0.0
         set_traffic(roof, *pmc_traffic(args.workload, roof["kernel"], stream))
+        if roof["kernel"] == "k_claim":
+            roof["op_rate"] = op_rate_roofline(times["expand"][0], acc["probes"], acc["new"])
         out["roofline"] = roof
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items() if v[0] > 0}
         if narrow[1]:

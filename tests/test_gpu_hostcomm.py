@@ -37,6 +37,16 @@ CASES = [
     # a failure after the all-gather, as if the exchange buffers could not be
     # grown: the rank still takes part in the exchange through its sink
     {"name": "fault_grow", "kw": {}, "env": {"KC_FAULT": "1:7:3"}, "all_ranks": True},
+    # a failure found at the end of a narrow batch (sn_end) on one rank: the
+    # failed process follows its peers into the next batch, whose first level
+    # stops every rank (it used to leave for the gather alone)
+    {"name": "fault_narrow_end", "kw": {}, "env": {"KC_FAULT": "1:12:4"}, "all_ranks": True},
+    # round 5: every level on the counted path, so every level after the
+    # first is a deferred frontier and its records go through the staging
+    # segments across processes
+    {"name": "model1_counted", "kw": {}, "env": {"KC_SNARROW": "0"}},
+    {"name": "lost_update_counted", "kw": {"variant": 1, "invariants": 7}, "env": {"KC_SNARROW": "0"}},
+    {"name": "np2_lost_update", "kw": {"np": 2, "variant": 1, "invariants": 7}},
 ]
 
 
@@ -128,9 +138,25 @@ def test_errors_and_traces(results, fixtures, oracle, key, name, kind):
         assert any(list(map(int, x)) == b for _, x in succ)
 
 
+def test_deferred_counted_levels(results, fixtures):
+    _, res = results
+    fx = fixtures["model1"]
+    r = res["model1_counted"][0]
+    assert "exception" not in r, r.get("exception")
+    assert r["complete"] and r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"])
+    assert r["act_gen"] == fx["act_gen"]
+    assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+    for name, key in (("lost_update_counted", "variant1_lost_update"), ("np2_lost_update", "np2_variant1_lost_update")):
+        r, fk = res[name][0], fixtures[key]
+        assert "exception" not in r, r.get("exception")
+        assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate", name
+        assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), name
+
+
 def test_fault_stops_every_rank(results):
     world, res = results
-    for name in ("fault_pack", "fault_expand_hostrows", "fault_grow"):
+    for name in ("fault_pack", "fault_expand_hostrows", "fault_grow", "fault_narrow_end"):
         got = res[name]
         assert sorted(got) == list(range(world)), name
         for rk, r in got.items():

@@ -342,3 +342,74 @@ def test_native_init_violation_max_levels_1(fixtures, R):
     # when level 1 is never expanded
     r = native(R, variant=5, max_levels=1)
     assert r["error"] == "invariant" and r["error_level"] == 1 and r["trace_len"] == 1
+
+
+# --- round 5: record staging and the deferred frontier on the counted path
+@pytest.mark.parametrize("R", [1, 2, 3])
+def test_native_counted_deferred(fixtures, monkeypatch, R):
+    # KC_SNARROW=0: every level on the counted path, so every level after the
+    # first runs on a deferred frontier (links only; the next expand rebuilds
+    # the states and finds their invariant violations there) and, with R > 1,
+    # packs its records through the tiles' staging segments
+    monkeypatch.setenv("KC_SNARROW", "0")
+    fx = fixtures["model1"]
+    r = native(R)
+    assert r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["act_gen"] == fx["act_gen"]
+    # (per-action distinct counts follow each state's first discoverer: TLC's
+    # at R = 1; at R > 1 the rank-major claim order picks another copy)
+    if R == 1:
+        assert r["act_dist"] == fx["act_dist"]
+    assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+    for key, kw, kind in (("nc2", dict(nc=2), "assertion"), ("variant2", dict(variant=2), "invariant"),
+                          ("variant3", dict(variant=3), "assertion"), ("ns0", dict(ns=0), "deadlock"),
+                          ("variant4", dict(variant=4), "invariant"),
+                          ("variant1_lost_update", dict(variant=1, invariants=7), "invariant")):
+        fk = fixtures[key]
+        r = native(R, **kw)
+        assert r["error"] == kind, key
+        assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), key
+        if R == 1:
+            assert r["trace"] == fk["trace"], key
+
+
+@pytest.mark.parametrize("R", [1, 3])
+def test_native_np2_lost_update_deferred(fixtures, R):
+    # NP=2's NoLostUpdate violation at depth 25 is found on a wide (counted,
+    # deferred) level: as the next expand rebuilds level 25's states
+    fk = fixtures["np2_variant1_lost_update"]
+    r = native(R, np=2, variant=1, invariants=7)
+    assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate"
+    assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"])
+    if R == 1:
+        assert r["trace"] == fk["trace"]
+
+
+def test_native_np2_prefix_switches(fixtures, monkeypatch):
+    # the NP=2 40-level prefix at 4 emulated ranks with each round-5 path
+    # switched off in turn (materialising emit, k_shard_pack, per-parent
+    # scans, one tile per settle workgroup): counts equal to the oracle's, and
+    # every per-action distinct count equal across the variants (the same
+    # claims win whichever path built, packed or positioned the states)
+    fx = fixtures["np2_40levels"]
+    runs = {}
+    for name, env in (("default", {}), ("sdefer0", {"KC_SDEFER": "0"}), ("stage0", {"KC_STAGE": "0"}),
+                      ("tscan0", {"KC_SHARD_TSCAN": "0"}), ("tp1", {"KC_SETTLE_TP": "1"}),
+                      ("tp4", {"KC_SETTLE_TP": "4"})):
+        for k in ("KC_SDEFER", "KC_STAGE", "KC_SHARD_TSCAN", "KC_SETTLE_TP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        mc = NativeShardedChecker(ModelConfig(np=2, max_levels=40), emulate=4)
+        try:
+            r = mc.run()
+            r["records_sent"] = mc.records_sent
+        finally:
+            mc.close()
+        assert r["level_width"] == fx["level_width"] and not r["complete"], name
+        assert r["act_gen"] == fx["act_gen"] and r["distinct"] == fx["distinct"], name
+        runs[name] = r
+    for name, r in runs.items():
+        assert r["act_dist"] == runs["sdefer0"]["act_dist"], name
+        assert r["records_sent"] == runs["sdefer0"]["records_sent"], name

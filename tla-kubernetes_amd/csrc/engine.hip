@@ -181,6 +181,12 @@ class EngineT final : public EngineBase {
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
     tscan_reg_ = !(tr && tr[0] == '0');
+    // KC_SETTLE_TP: claim tiles per settle workgroup (1, 2, 4 or 8)
+    const char* tp = getenv("KC_SETTLE_TP");
+    if (tp) {
+      const int v = atoi(tp);
+      settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
+    }
     const char* eo = getenv("KC_EMIT_OCC");
     if (eo) emit_occ_ = atoi(eo);
     const char* hc = getenv("KC_HEADCOPY");
@@ -498,16 +504,7 @@ class EngineT final : public EngineBase {
                                succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
         }
-        timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
-                             cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
-                             (uint32_t*)nullptr, tiles, claim_args_.ovf);
-          hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
-                             tscan_ ? ttot_ : (uint32_t*)nullptr);
-          hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start,
-                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, tscan_ ? ttot_ : (uint32_t*)nullptr);
-        });
+        timed(KK_RESOLVE, [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr); });
         if (tscan_) {
           timed(KK_SCAN, [&] {
             hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
@@ -1616,16 +1613,7 @@ class EngineT final : public EngineBase {
                              cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level, abl_mask_, rcount_, rec_fp_,
                              rec_lk_, newmask_, d_ctr_, claim_args_);
         });
-        timed(KK_RESOLVE, [&] {
-          hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, m, start,
-                             cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
-                             (uint32_t*)nullptr, tiles, claim_args_.ovf);
-          hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, m, start, cs_.t,
-                             cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
-                             spill_ ? ttot_ : (uint32_t*)nullptr);
-          hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, m, start,
-                             cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, 0u, spill_ ? ttot_ : (uint32_t*)nullptr);
-        });
+        timed(KK_RESOLVE, [&] { launch_settle(m, start, tiles, succ_level, spill_ ? ttot_ : (uint32_t*)nullptr); });
         if (spill_) {
           // the tile-count path: the cold check clears winners and recounts tiles
           timed(KK_SCAN, [&] {
@@ -1808,6 +1796,34 @@ class EngineT final : public EngineBase {
   bool tscan_ = false, headcopy_ = false;
   int narrow_batch_ = NARROW_BATCH;
   int tscan_reg_ = 1;   // KC_TSCAN_REG=0: k_tile_scan's loop path (levels > 65,536 tiles) at any width
+  int settle_tp_ = SETTLE_TP_DEFAULT;   // claim tiles per settle workgroup (KC_SETTLE_TP)
+  // settle passes A and B of a chunk's tiles (k_settle_rec, or k_settle_mt
+  // with settle_tp_ tiles per workgroup), then the overflow list's pass B
+  void launch_settle(uint64_t cn, uint64_t start, unsigned tiles, uint32_t succ_level, uint32_t* ttot) {
+    if (settle_tp_ == 1) {
+      hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
+                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                         (uint32_t*)nullptr, tiles, claim_args_.ovf);
+      hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t, cs_.nslots,
+                         succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u, ttot);
+    } else {
+#define KC_SETTLE_MT(TP)                                                                                          \
+  if (settle_tp_ == TP) {                                                                                         \
+    const unsigned tb = (tiles + TP - 1) / TP;                                                                    \
+    hipLaunchKernelGGL((k_settle_mt<0, TP>), dim3(tb + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,   \
+                       cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,            \
+                       (uint32_t*)nullptr, tiles, claim_args_.ovf);                                                \
+    hipLaunchKernelGGL((k_settle_mt<1, TP>), dim3(tb), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t, cs_.nslots,     \
+                       succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u, ttot, tiles, claim_args_.ovf); \
+  }
+      KC_SETTLE_MT(2)
+      KC_SETTLE_MT(4)
+      KC_SETTLE_MT(8)
+#undef KC_SETTLE_MT
+    }
+    hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
+                       cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
+  }
   int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;
   uint64_t ttot_cap_ = 0, toff_cap_ = 0;

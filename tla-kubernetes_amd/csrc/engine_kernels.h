@@ -17,6 +17,7 @@
 
 #include "fpset_dev.h"
 #include "kubeapi_spec.h"
+#include "record.h"
 
 namespace kc {
 
@@ -60,7 +61,8 @@ struct Counters {
   unsigned long long defer_flags; // deferred frontier (DeferArgs): DF_* bits of the level
   unsigned long long defer_inv_n; // ... ~(lowest index of a rebuilt state violating an invariant); 0 = none
                                   // (word 8: k_advance copies it to the host with the head)
-  unsigned long long head_pad[7];
+  unsigned long long defer_err;   // sharded deferred frontier: min invariant key of the rebuilt states (~0 = none)
+  unsigned long long head_pad[6];
   CtrStripe s[CTR_STRIPES];
 
   unsigned long long act_gen(int a) const { return sum(&CtrStripe::act_gen, a); }
@@ -100,15 +102,18 @@ struct Counters {
     return t;
   }
 };
-// bytes of the per-level head (err_key, chunk_base, overflow, batch_used,
-// cand_total, level_new, emit_done, defer_flags): what the host reads back
-// after every level
-constexpr size_t kCtrHead = 8 * sizeof(unsigned long long);
-static_assert(offsetof(Counters, defer_flags) == 7 * 8 && offsetof(Counters, defer_inv_n) == 8 * 8,
-              "k_advance's host copy indexes the head words");
+// bytes of the per-level head (every word before the stripes: err_key ...
+// defer_err and the padding): what the host reads back after a level.  The
+// engine's k_advance writes its pinned copy word by word (words 0-5, 7, 8);
+// a head copy (hipMemcpy of kCtrHead bytes) takes all of them.
+constexpr size_t kCtrHead = 16 * sizeof(unsigned long long);
+static_assert(offsetof(Counters, defer_flags) == 7 * 8 && offsetof(Counters, defer_inv_n) == 8 * 8 &&
+                  offsetof(Counters, defer_err) == 9 * 8 && offsetof(Counters, s) == kCtrHead,
+              "k_advance's host copy indexes the head words; kCtrHead covers the whole head");
 // defer_flags: a rebuilt frontier state violates an invariant; a level's
-// links or trace entries did not fit the capacity the host estimated
-constexpr unsigned long long DF_INVARIANT = 1, DF_CAPACITY = 2;
+// links or trace entries did not fit the capacity the host estimated; (the
+// sharded k_claim) a tile's records did not fit the staging buffer
+constexpr unsigned long long DF_INVARIANT = 1, DF_CAPACITY = 2, DF_STAGE = 4;
 __device__ __forceinline__ CtrStripe& stripe(Counters* C) {
   return C->s[blockIdx.x & (CTR_STRIPES - 1)];
 }
@@ -132,6 +137,30 @@ __device__ __forceinline__ void store_state(typename M::State* __restrict__ p, u
   ulonglong2* v = reinterpret_cast<ulonglong2*>(p + i);
 #pragma unroll
   for (int k = 0; k < M::W / 2; ++k) v[k] = make_ulonglong2(s.w[2 * k], s.w[2 * k + 1]);
+}
+// A record (record.h): the successor's key, then its bit-packed canonical
+// state; 48 B for NP = 2.
+template <class M>
+__device__ __forceinline__ void load_record(const Record<M>* __restrict__ in, uint64_t i,
+                                            typename M::State& x, uint64_t& key) {
+  const ulonglong2* v = reinterpret_cast<const ulonglong2*>(in + i);
+  uint64_t r[Record<M>::RW];
+#pragma unroll
+  for (int k = 0; k < Record<M>::RW / 2; ++k) {
+    const ulonglong2 q = v[k];
+    r[2 * k] = q.x;
+    r[2 * k + 1] = q.y;
+  }
+  record_unpack<M>(r, x, key);
+}
+template <class M>
+__device__ __forceinline__ void store_record(Record<M>* __restrict__ out, uint64_t i, const typename M::State& x,
+                                             uint64_t key) {
+  uint64_t w[Record<M>::RW];
+  record_pack<M>(x, key, w);
+  ulonglong2* v = reinterpret_cast<ulonglong2*>(out + i);
+#pragma unroll
+  for (int k = 0; k < Record<M>::RW / 2; ++k) v[k] = make_ulonglong2(w[2 * k], w[2 * k + 1]);
 }
 
 // ------------------------------------------------------------------------
@@ -269,6 +298,20 @@ struct ShardArgs {
   uint32_t* repmask = nullptr;   // [n]: remote representatives of each parent
   uint8_t* cnt = nullptr;        // [world][n]: remote representatives per owner and parent (<= 32: 8 bits)
   CandOvf ovf;
+  // Record staging (round 5; stage != nullptr): each tile writes its remote
+  // representatives' records itself, grouped by owner and in (parent,
+  // position) order within an owner, into a segment of the staging buffer
+  // it reserves with one atomic; tcnt / stoff let k_shard_gather move the
+  // segments into the owner-grouped send buffer in tile order: the order
+  // k_shard_pack produced from the per-parent owner scan, with neither the
+  // re-expansion nor the scan.  A tile whose segment does not fit sets
+  // DF_STAGE and stages nothing; the host then packs that level the old way
+  // (repmask / cnt are written either way).
+  void* stage = nullptr;                      // Record<M>[stage_cap]
+  unsigned long long* stage_cur = nullptr;    // records reserved this level
+  uint64_t stage_cap = 0;
+  uint32_t* tcnt = nullptr;                   // [world][tiles]: records per owner and tile
+  unsigned long long* stoff = nullptr;        // [tiles]: the tile's first staging record (~0: none staged)
 };
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
 // workgroups resident together (~1,536: 6 per CU) work on tiles spread over
@@ -315,6 +358,10 @@ __device__ __forceinline__ unsigned int act_sum(const unsigned int* sh, unsigned
 }
 struct DeferArgs {
   const void* prev = nullptr;                 // the previous frontier (State*); nullptr: cur holds the states
+  // sharded k_claim (SH): link[i] >> 63 set = frontier state i is received
+  // record link[i] & ~(1 << 63) of the previous level (prev_rec, Record<M>*);
+  // else parent index << 8 | position in the previous frontier, as above
+  const void* prev_rec = nullptr;
   const unsigned long long* parent = nullptr; // trace: global parent index per state (keep_trace) ...
   const uint8_t* ord = nullptr;               // ... and successor position
   const unsigned long long* link = nullptr;   // or, without a trace: parent index << 8 | position
@@ -356,6 +403,42 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
     atomicMax(&C->defer_inv_n, ~(unsigned long long)i);   // the level's first violator in BFS order
   }
   atomicAdd(&sh_actd[M::slot_action(gp, slot) * AS + (threadIdx.x & (AS - 1))], 1u);
+  return s;
+}
+
+// The sharded deferred frontier (round 5): rebuild frontier state i of rank
+// `rank` from its link — its own parent in the previous frontier, or a
+// record it received last level (kept in that level's receive buffer) —
+// store it, check the invariants (the key the materialising emit would have
+// made, into C->defer_err: an error of the previous level) and count its
+// action into sh_actd.
+template <class M, int AS = ACT_STRIPES>
+__device__ __forceinline__ typename M::State shard_rebuild(const DeferArgs& df, uint64_t i, const Flags& f,
+                                                           uint64_t rank, unsigned int* sh_actd,
+                                                           Counters* __restrict__ C) {
+  const unsigned long long lk = df.link[i];
+  typename M::State s;
+  uint64_t key;
+  int act;
+  if (lk >> 63) {
+    load_record<M>(reinterpret_cast<const Record<M>*>(df.prev_rec), lk & ~(1ull << 63), s, key);
+    act = (int)(key & 0xff);
+  } else {
+    const uint64_t pp = lk >> 8;
+    const int t = (int)(lk & 0xff);
+    const typename M::State gp = load_state<M>(reinterpret_cast<const typename M::State*>(df.prev), pp);
+    const typename M::Plan pl{df.prev_counts ? df.prev_counts[pp] : M::plan(gp, f).counts, 0, -1, -1};
+    int slot, j;
+    M::locate(pl, t, slot, j);
+    M::apply(gp, slot, j, f, s);
+    act = M::slot_action(gp, slot);
+    key = (rank << 60) | (pp << 16) | ((uint64_t)t << 8);
+  }
+  store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
+  if (M::check(s, f.inv_mask) >= 0) atomicMin(&C->defer_err, (key & ~0xffull) | E_INVARIANT);
+  // (a record's action byte indexes LDS: anything out of range would be a
+  // corrupt record, counted nowhere)
+  if ((unsigned)act < (unsigned)A_COUNT) atomicAdd(&sh_actd[act * AS + (threadIdx.x & (AS - 1))], 1u);
   return s;
 }
 
@@ -403,6 +486,112 @@ static __global__ void k_parent_chain(const unsigned long long* __restrict__ par
     g = p;
   }
   *len = k;
+}
+
+// Record staging of the sharded k_claim (ShardArgs::stage): after the claim
+// loop, with the per-parent remote masks (sh_rep) and per-owner counts
+// (sh_cnt, 4 x 8 bits per word) complete and the LDS table free.
+//   1. per owner, the exclusive prefix of the counts over the tile's parents
+//      (lane = parent; two owners per word in 16-bit halves: a tile has at
+//      most 256 x 32 records) -> pre[owner pair][parent] in the table's LDS;
+//   2. the tile's totals per owner, its segment reserved with one atomic,
+//      tcnt / stoff for k_shard_gather;
+//   3. each dealt lane (its parent's state, fold and plan still in
+//      registers) re-applies its parent's remote successors in position
+//      order and stores each record at segment base + owner base + parent
+//      prefix + its rank among the parent's records of that owner.
+// The fingerprint is recomputed for the owner (the claim loop had it in LDS
+// only); no parent is reloaded and nothing is planned again.
+template <class M, int NT>
+__device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, const typename M::State& s,
+                                              uint64_t fold, uint64_t counts, uint32_t lp, Flags f,
+                                              const unsigned int* sh_rep, const unsigned int* sh_cnt,
+                                              const uint32_t* sh_proj, unsigned long long* sh_fp,
+                                              unsigned int* sh_key, uint32_t tile, uint64_t pbase,
+                                              Counters* __restrict__ C) {
+  constexpr bool SWAR = KC_LOCATE_SWAR && M::CUM_OK;
+  static_assert(NT * 8 >= 8 * CLAIM_TILE * 4, "pre[] needs (world + 1) / 2 x 256 words (world <= 15)");
+  const uint32_t R = sh.world, npair = (R + 1) / 2;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(sh_fp);   // [npair][CLAIM_TILE]
+  unsigned int* wsum = sh_key;                          // [4 waves][8 pairs]
+  unsigned int* tt = sh_key + 32;                       // [0, 16): per-owner totals; [16, 32): owner bases
+  unsigned int* seg = sh_key + 64;                      // segment base, lo / hi (~0: none)
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (uint32_t w = 0; w < npair; ++w) {
+    const uint32_t o0 = 2 * w, o1 = 2 * w + 1;
+    uint32_t v = (sh_cnt[(o0 >> 2) * CLAIM_TILE + tid] >> (8 * (o0 & 3))) & 0xffu;
+    if (o1 < R) v |= ((sh_cnt[(o1 >> 2) * CLAIM_TILE + tid] >> (8 * (o1 & 3))) & 0xffu) << 16;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wv * 8 + w] = x;
+    pre[w * CLAIM_TILE + tid] = x - v;
+  }
+  __syncthreads();
+  for (uint32_t w = 0; w < npair; ++w) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < wv; ++k) b += wsum[k * 8 + w];
+    pre[w * CLAIM_TILE + tid] += b;
+  }
+  if (tid < R) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int k = 0; k < CLAIM_TILE / 64; ++k) a += wsum[k * 8 + (tid >> 1)];
+    tt[tid] = (a >> (16 * (tid & 1))) & 0xffffu;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t o = 0; o < R; ++o) {
+      tt[16 + o] = acc;
+      acc += tt[o];
+    }
+    unsigned long long b = acc ? atomicAdd(sh.stage_cur, (unsigned long long)acc) : 0ull;
+    if (acc && b + acc > sh.stage_cap) {
+      atomicOr(&C->defer_flags, DF_STAGE);
+      b = ~0ull;
+    }
+    seg[0] = (unsigned int)b;
+    seg[1] = (unsigned int)(b >> 32);
+    sh.stoff[tile] = b;
+  }
+  if (tid < R) sh.tcnt[(uint64_t)tid * gridDim.x + tile] = tt[tid];
+  __syncthreads();
+  const unsigned long long sb = (unsigned long long)seg[0] | ((unsigned long long)seg[1] << 32);
+  if (!live || sb == ~0ull) return;
+  uint32_t mask = sh_rep[lp];
+  if (!mask) return;
+  Record<M>* out = reinterpret_cast<Record<M>*>(sh.stage);
+  const typename M::Plan pl{counts, 0, -1, -1};
+  const uint32_t proj = sh_proj[lp];
+  uint64_t c0 = 0, c1 = 0;            // the parent's records so far per owner, 6 bits each (owners 0-9, 10-14)
+  for (; mask; mask &= mask - 1) {
+    const int t = __ffs(mask) - 1;
+    int slot, j;
+    if (SWAR)
+      M::locate_cum(counts, t, slot, j);
+    else
+      M::locate(pl, t, slot, j);
+    typename M::State x;
+    int who;
+    M::apply(s, slot, j, f, x, who);
+    const uint64_t fp = M::template fingerprint_succ<1>(s, fold, x, who, proj);
+    const uint32_t o = owner_of(fp, R);
+    uint32_t r;
+    if (o < 10) {
+      r = (uint32_t)(c0 >> (6 * o)) & 63u;
+      c0 += 1ull << (6 * o);
+    } else {
+      r = (uint32_t)(c1 >> (6 * (o - 10))) & 63u;
+      c1 += 1ull << (6 * (o - 10));
+    }
+    const uint64_t pos = sb + tt[16 + o] + ((pre[(o >> 1) * CLAIM_TILE + lp] >> (16 * (o & 1))) & 0xffffu) + r;
+    store_record<M>(out, pos, x,
+                    ((uint64_t)sh.rank << 60) | (pbase << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot));
+  }
 }
 
 // ABL (diagnostic builds of the same kernel, launched on scratch buffers when
@@ -499,12 +688,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   uint64_t fold = 0, counts = 0;
   int tot = 0;
   if (live) {
-    s = (!SH && df.prev) ? defer_rebuild<M, AS>(df, base + i, f, sh_actd, C) : load_state<M>(cur, i);
+    if (df.prev)
+      s = OWN ? shard_rebuild<M, AS>(df, base + i, f, sh.rank, sh_actd, C)     // (the sharded path, any world)
+              : defer_rebuild<M, AS>(df, base + i, f, sh_actd, C);
+    else
+      s = load_state<M>(cur, i);
     const typename M::Plan pl = M::plan(s, f);
-    if (!SH && df.counts_out) df.counts_out[base + i] = pl.counts;
+    if (df.counts_out) df.counts_out[base + i] = pl.counts;
     // (an LDS total, not a register live through the kernel: k_claim sits at
     // its 80-VGPR budget for 6 waves per SIMD)
-    if (!SH && df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
+    if (df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
     fold = M::fp_fold(s);
     if (OWN) sh_proj[threadIdx.x] = M::owner_proj(s);
     if (ABL == 0) {
@@ -780,6 +973,10 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
   }
   __syncthreads();
+  if (SH && sh.stage)
+    stage_records<M, NT>(sh, live, s, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
+                         sh_rep, sh_cnt, sh_proj, sh_fp, sh_key, tile,
+                         base + tile0 + (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x), C);
   if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
   if (live) newmask[i] = sh_cur[threadIdx.x];
   if (SH && live) {
@@ -795,7 +992,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const unsigned int v = act_sum<AS>(sh_act, threadIdx.x);
     if (v) atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)v);
   }
-  if (!SH && df.prev) {
+  if (df.prev) {
     if (threadIdx.x < A_COUNT) {
       const unsigned int v = act_sum<AS>(sh_actd, threadIdx.x);
       if (v) atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)v);
@@ -919,6 +1116,81 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
     }
   }
 }
+// TP consecutive tiles per workgroup (round 5, KC_SETTLE_TP; 1 = settle_tile):
+// a tile holds ~40 candidates on NP=2, so one workgroup per tile spends
+// most of its life being dispatched (2.9M tiles x 2 passes per check).  The
+// TP tiles' candidates are dealt to the 256 lanes together (all their
+// atomics still in flight at once, unlike a persistent loop over tiles,
+// DESIGN §7.3), and PASS 1 counts each tile's new states as settle_tile.
+template <int PASS, int TP>
+__device__ __forceinline__ void settle_tiles(uint32_t t0, uint32_t ntiles, uint64_t n, uint64_t base,
+                                             ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+                                             const unsigned int* __restrict__ rcount,
+                                             const unsigned long long* __restrict__ rec_fp,
+                                             unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask,
+                                             Counters* __restrict__ C, uint32_t rank,
+                                             uint32_t* __restrict__ tile_total) {
+  __shared__ unsigned int sh_cnt[TP + 1];
+  __shared__ unsigned int sh_tot[CLAIM_TILE / 64][TP];
+  unsigned newc[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) newc[j] = 0;
+  if (threadIdx.x == 0) {
+    unsigned a = 0;
+    for (int j = 0; j < TP; ++j) {
+      sh_cnt[j] = a;
+      a += t0 + j < ntiles ? rcount[t0 + j] : 0u;
+    }
+    sh_cnt[TP] = a;
+  }
+  if (PASS == 1 && tile_total) {
+    // read before any of this pass's bit sets (the barrier below orders them)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const uint64_t p = (uint64_t)(t0 + j) * CLAIM_TILE + threadIdx.x;
+      if (t0 + j < ntiles && p < n) newc[j] = (unsigned)__builtin_popcount(newmask[p]);
+    }
+  }
+  __syncthreads();
+  unsigned reads = 0;
+  const unsigned total = sh_cnt[TP];
+  for (unsigned k = threadIdx.x; k < total; k += CLAIM_TILE) {
+    int j = 0;
+#pragma unroll
+    for (int q = 1; q < TP; ++q)
+      if (k >= sh_cnt[q]) j = q;
+    const uint32_t tile = t0 + j;
+    const uint64_t r = (uint64_t)tile * CLAIM_RCAP + (k - sh_cnt[j]);
+    const int v = settle_record<PASS>(tile, rec_fp[r], &rec_lk[r], n, base, cs, nbuckets, level, newmask, C, rank);
+    reads += v ? 1u : 0u;
+    if (v == 2) {
+#pragma unroll
+      for (int q = 0; q < TP; ++q)
+        if (q == j) ++newc[q];
+    }
+  }
+  unsigned long long rw = reads;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
+  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
+  if (PASS == 1 && tile_total) {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      unsigned v = newc[j];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if ((threadIdx.x & 63) == 0) sh_tot[threadIdx.x >> 6][j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < TP && t0 + threadIdx.x < ntiles) {
+      unsigned t = 0;
+#pragma unroll
+      for (int w = 0; w < CLAIM_TILE / 64; ++w) t += sh_tot[w][threadIdx.x];
+      tile_total[t0 + threadIdx.x] = t;
+    }
+  }
+}
+
 // The same passes over the chunk's overflow list (after k_settle_rec<PASS>:
 // a PASS-1 winner then adds itself to its tile's count).
 template <int PASS>
@@ -949,6 +1221,7 @@ k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs
   settle_ovf_blocks<PASS>(blockIdx.x, gridDim.x, ovf, n, base, cs, nbuckets, level, newmask, C, rank, tile_total);
 }
 constexpr unsigned SETTLE_OVF_GRID = 1024;
+constexpr int SETTLE_TP_DEFAULT = 1;     // claim tiles per settle workgroup (engine KC_SETTLE_TP)
 // blocks of settle pass A's launch that take the overflow list (pass A needs
 // no counts, so its overflow work shares the tiles' launch; pass B's adds to
 // the tile counts the tile blocks compute, so it runs in a launch of its own)
@@ -976,9 +1249,33 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
 // is at most 2^27 parents, so the totals fit u32).  Each thread takes a
 // contiguous run of 16-B groups (4 tiles); up to TS_REG groups per thread
 // (T <= 65,536 tiles) stay in registers, all their loads in flight at once.
+// k_settle_rec with TP tiles per workgroup (PASS 0: the grid's blocks past
+// ceil(tiles / TP) take the overflow list, as k_settle_rec's past `tiles`)
+template <int PASS, int TP>
+static __global__ void __launch_bounds__(CLAIM_TILE)
+k_settle_mt(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
+            const unsigned int* __restrict__ rcount, const unsigned long long* __restrict__ rec_fp,
+            unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask, Counters* __restrict__ C,
+            uint32_t rank, uint32_t* __restrict__ tile_total, uint32_t tiles, CandOvf ovf) {
+  const uint32_t tb = (tiles + TP - 1) / TP;
+  if (PASS == 0 && blockIdx.x >= tb) {
+    settle_ovf_blocks<0>(blockIdx.x - tb, gridDim.x - tb, ovf, n, base, cs, nbuckets, level, newmask, C, rank,
+                         nullptr);
+    return;
+  }
+  settle_tiles<PASS, TP>(blockIdx.x * TP, tiles, n, base, cs, nbuckets, level, rcount, rec_fp, rec_lk, newmask, C,
+                         rank, tile_total);
+}
+
 constexpr int TSCAN_THREADS = 1024;
-static __global__ void __launch_bounds__(TSCAN_THREADS)
-k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off, int reg_ok) {
+// Marks of a tile scan (the sharded levels): the exclusive prefix at
+// positions m_k = k * stride for k = 0 .. nmark - 1, plus at `extra`, go to
+// LDS (mark[k], mark[nmark]); k * stride = T reads the total.  nmark <= 16.
+struct ScanMarks {
+  uint32_t stride = 0, nmark = 0, extra = ~0u;
+};
+__device__ __forceinline__ void tile_scan_body(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off,
+                                               int reg_ok, const ScanMarks& mk, unsigned int* sh_mark) {
   __shared__ unsigned int sh_w[TSCAN_THREADS / 64];
   const uint32_t G = (T + 3) / 4, per = (G + TSCAN_THREADS - 1) / TSCAN_THREADS;
   const uint32_t b = threadIdx.x * per, e = min(G, b + per);
@@ -1018,6 +1315,15 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
   unsigned int run = incl - sum;
   for (int w = 0; w < wv; ++w) run += sh_w[w];
   uint4* o4 = reinterpret_cast<uint4*>(off);
+  auto mark = [&](uint32_t c0, const unsigned int (&ex)[4]) {   // cells c0 .. c0 + 3 start at ex[]
+    if (!mk.nmark && mk.extra == ~0u) return;
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t c = c0 + q;
+      if (c >= T) break;
+      if (c == mk.extra) sh_mark[mk.nmark] = ex[q];
+      if (mk.stride && c % mk.stride == 0 && c / mk.stride < mk.nmark) sh_mark[c / mk.stride] = ex[q];
+    }
+  };
   auto put = [&](uint32_t g, const uint4& v) {
     uint4 r;
     r.x = run;
@@ -1026,6 +1332,8 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
     r.w = r.z + v.z;
     run = r.w + v.w;
     o4[g] = r;
+    const unsigned int ex[4] = {r.x, r.y, r.z, r.w};
+    mark(4 * g, ex);
   };
   if (inreg) {
 #pragma unroll
@@ -1034,7 +1342,22 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
   } else {
     for (uint32_t g = b; g < e; ++g) put(g, grp(g));
   }
-  if (threadIdx.x == TSCAN_THREADS - 1) off[T] = run;
+  if (threadIdx.x == TSCAN_THREADS - 1) {
+    off[T] = run;
+    // marks at T (the total): k * stride == T, or extra == T
+    if (mk.extra == T) sh_mark[mk.nmark] = run;
+    if (mk.stride && T % mk.stride == 0 && T / mk.stride < mk.nmark) sh_mark[T / mk.stride] = run;
+  }
+  __syncthreads();
+}
+// Exclusive prefix sum of the tiles' new-state counts (engine default; one
+// workgroup): off[t] = sum of tot[0..t), off[T] = the chunk's total (a chunk
+// is at most 2^27 parents, so the totals fit u32).  Each thread takes a
+// contiguous run of 16-B groups (4 tiles); up to TS_REG groups per thread
+// (T <= 65,536 tiles) stay in registers, all their loads in flight at once.
+static __global__ void __launch_bounds__(TSCAN_THREADS)
+k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__ off, int reg_ok) {
+  tile_scan_body(tot, T, off, reg_ok, ScanMarks{}, nullptr);
 }
 
 // popcount(newmask): the scan's input (new states per parent)

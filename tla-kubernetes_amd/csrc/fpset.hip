@@ -381,6 +381,63 @@ k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t start, uint64_t n,
   const unsigned long long b = __ballot(f != 0);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[2], (unsigned long long)__popcll(b));
 }
+// Windowed stress insert (KC_STRESS_WINDOW=<log2 slots per
+// window>, A/B): a super-batch of the insert stream is generated into
+// memory and bucketed by table window (bucket_of >> wbits: 2^27 slots =
+// 1 GiB) — per workgroup an LDS histogram, one atomic per (workgroup,
+// window) to reserve its ranges — so the inserts that follow sweep the table
+// one window after another instead of all of it at once (random CAS on a
+// <= 1 GB window ran 27 vs 19 G/s, profiles/r03d_random_probe.txt).  The
+// stream has no duplicates, so the order of the inserts changes nothing.
+constexpr int WIN_MAX = 1024;
+__global__ void __launch_bounds__(256)
+k_win_gen_count(uint64_t seed, uint64_t start, uint64_t n, uint64_t ns, int wbits, uint32_t nwin,
+                uint64_t* __restrict__ out, unsigned int* __restrict__ wcount) {
+  __shared__ unsigned int h[WIN_MAX];
+  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x) h[w] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint64_t fp = stress_insert_fp(seed, start + i);
+    out[i] = fp;
+    atomicAdd(&h[(uint32_t)(bucket_of(fp, ns) >> wbits)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x)
+    if (h[w]) atomicAdd(&wcount[w], h[w]);
+}
+// exclusive scan of the window counts into cursors (one workgroup)
+__global__ void k_win_cursor(const unsigned int* __restrict__ wcount, uint32_t nwin,
+                             unsigned long long* __restrict__ cursor) {
+  if (threadIdx.x != 0) return;
+  unsigned long long a = 0;
+  for (uint32_t w = 0; w < nwin; ++w) {
+    cursor[w] = a;
+    a += wcount[w];
+  }
+}
+__global__ void __launch_bounds__(256)
+k_win_scatter(const uint64_t* __restrict__ in, uint64_t n, uint64_t ns, int wbits, uint32_t nwin,
+              unsigned long long* __restrict__ cursor, uint64_t* __restrict__ out) {
+  __shared__ unsigned int h[WIN_MAX];
+  __shared__ unsigned long long base[WIN_MAX];
+  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x) h[w] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t fp = 0;
+  uint32_t w = 0, r = 0;
+  if (i < n) {
+    fp = in[i];
+    w = (uint32_t)(bucket_of(fp, ns) >> wbits);
+    r = atomicAdd(&h[w], 1u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nwin; k += blockDim.x)
+    if (h[k]) base[k] = atomicAdd(&cursor[k], (unsigned long long)h[k]);
+  __syncthreads();
+  if (i < n) out[base[w] + r] = fp;
+}
+
 // The same streams written to memory (the sharded stress exchanges them).
 __global__ void k_stress_gen(uint64_t seed, int kind, uint64_t n_ins, uint64_t start, uint64_t n,
                              uint64_t* __restrict__ out) {
@@ -756,11 +813,41 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   KC_HIP_TRY(hipEventCreate(&e1));
   KC_HIP_TRY(hipEventCreate(&e2));
   KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, STAT_BYTES, st));
+  // windowed inserts (A/B): KC_STRESS_WINDOW = log2 of the slots per window;
+  // KC_STRESS_SUPER = inserts per super-batch (default 4 batches)
+  const char* we = getenv("KC_STRESS_WINDOW");
+  const int wbits = we ? atoi(we) : 0;
+  const uint64_t ns = s->fs.nbuckets * 8;
+  const uint32_t nwin = wbits > 0 ? (uint32_t)((ns + (1ull << wbits) - 1) >> wbits) : 0;
+  const char* se = getenv("KC_STRESS_SUPER");
+  const uint64_t sb = se && atoll(se) > 0 ? (uint64_t)atoll(se) : 4 * batch;
+  uint64_t *wa = nullptr, *wb = nullptr;
+  unsigned int* wcnt = nullptr;
+  unsigned long long* wcur = nullptr;
+  const bool windowed = wbits > 0 && nwin >= 2 && nwin <= (uint32_t)WIN_MAX;
+  if (windowed) {
+    KC_HIP_TRY(hipMalloc(&wa, std::min(sb, n) * 8));
+    KC_HIP_TRY(hipMalloc(&wb, std::min(sb, n) * 8));
+    KC_HIP_TRY(hipMalloc(&wcnt, WIN_MAX * 4));
+    KC_HIP_TRY(hipMalloc(&wcur, WIN_MAX * 8));
+  }
   KC_HIP_TRY(hipEventRecord(e0, st));
-  for (uint64_t off = 0; off < n; off += batch) {
-    const uint64_t m = std::min(batch, n - off);
-    hipLaunchKernelGGL(k_stress_insert, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, seed,
-                       off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+  if (windowed) {
+    for (uint64_t off = 0; off < n; off += sb) {
+      const uint64_t m = std::min(sb, n - off);
+      const unsigned g = (unsigned)((m + 255) / 256);
+      KC_HIP_TRY(hipMemsetAsync(wcnt, 0, WIN_MAX * 4, st));
+      hipLaunchKernelGGL(k_win_gen_count, dim3(g), dim3(256), 0, st, seed, off, m, ns, wbits, nwin, wa, wcnt);
+      hipLaunchKernelGGL(k_win_cursor, dim3(1), dim3(64), 0, st, wcnt, nwin, wcur);
+      hipLaunchKernelGGL(k_win_scatter, dim3(g), dim3(256), 0, st, wa, m, ns, wbits, nwin, wcur, wb);
+      hipLaunchKernelGGL(k_insert_count, dim3(g), dim3(256), 0, st, wb, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+    }
+  } else {
+    for (uint64_t off = 0; off < n; off += batch) {
+      const uint64_t m = std::min(batch, n - off);
+      hipLaunchKernelGGL(k_stress_insert, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, seed,
+                         off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
+    }
   }
   KC_HIP_TRY(hipEventRecord(e1, st));
   for (uint64_t off = 0; off < n_lookup; off += batch) {
@@ -778,6 +865,8 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipEventDestroy(e2);
+  for (void* p : {(void*)wa, (void*)wb, (void*)wcnt, (void*)wcur})
+    if (p) (void)hipFree(p);
   s->fs.count += stats[0];
   if (insert_seconds) *insert_seconds = ms1 * 1e-3;
   if (lookup_seconds) *lookup_seconds = ms2 * 1e-3;

@@ -748,10 +748,14 @@ struct Model {
   // record to send) and siblings stay together for the LDS tile dedup.  For
   // R dividing 2^OWNER_BITS the owner depends on these bits only.  The other
   // 59 bits are the Zobrist fold, so two states collide only if their
-  // projections hash alike and 59 fold bits agree.  Two projections (the
-  // template parameter OWN of the fingerprint functions):
+  // projections hash alike and 59 fold bits agree.  The template parameter
+  // OWN of the fingerprint functions:
   //  * OWN = 0 (the single-GPU engine, and every fingerprint the C-ABI
-  //    reports): apiState and the first PVC controller's word;
+  //    reports): with KC_OWN0_FOLD (the default since round 4) no owner
+  //    bits at all — the fingerprint is the 63-bit fold (fp_final below), so
+  //    two states collide only if all 63 fold bits agree (~2^-63 per pair);
+  //    the fingerprint VALUES differ from round-3 builds.
+  //    With KC_OWN0_FOLD=0: apiState and the first PVC controller's word;
   //  * OWN = 1 (the sharded path, shard.hip): apiState and the listRequests
   //    objs words.  An action always rewrites its process's scalar word,
   //    but only APIStart changes apiState and only list replies change objs,

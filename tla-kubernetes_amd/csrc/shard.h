@@ -47,6 +47,22 @@ class ShardBase {
   virtual const kc_model_config& config() const = 0;
   // pack() without its own host sync (the caller orders the records' use)
   virtual void set_async_pack(bool on) = 0;
+  // ---- the deferred frontier (round 5; the native loop's counted levels):
+  // with it on, insert emits only links and parent keys, and the next
+  // level's expand rebuilds the states (from this rank's previous frontier
+  // or from the records this level received — the caller keeps the receive
+  // buffer passed to insert intact until the next expand).  An invariant
+  // violation among rebuilt states is an error of the level before: the
+  // device row carries it (expand_dev), and defer_error() reports it after
+  // expand_done.  materialize() builds a deferred frontier now (before a
+  // narrow batch or a max_levels stop; synchronous) and returns its
+  // invariant key the same way.  drop_last_insert() takes the last insert's
+  // new states back out of the distinct count (a world-1 run that learns of
+  // such an error only after it inserted the next level).
+  virtual void set_deferred(bool on) = 0;
+  virtual uint64_t defer_error() const = 0;
+  virtual int materialize(uint64_t* defer_err) = 0;
+  virtual void drop_last_insert() = 0;
   virtual int replay(int init_idx, const std::vector<int>& ords, int kind, int pos,
                      std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
                      int* err_inv) = 0;
@@ -64,6 +80,7 @@ class ShardBase {
     uint64_t status_new = 0;        // this rank's width of the next level
     uint64_t status_err = ~0ull;    // the previous level's errors (the counted loop's status_err)
     uint64_t sent = 0;              // records this rank sent to other ranks in the levels run
+    bool filled = false;            // sn_end read the batch's outcome (set even when it then fails)
   };
   virtual int sn_setup(uint32_t slot_cap) = 0;
   virtual uint64_t sn_slot_bytes() const = 0;

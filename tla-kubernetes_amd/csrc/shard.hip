@@ -49,21 +49,6 @@ namespace kc {
 
 constexpr uint64_t KEY_INIT = 0xFull << 60;   // parent key of an Init state (| init index)
 
-// A record (record.h): the successor's key, then its bit-packed canonical
-// state; 48 B for NP = 2.
-template <class M>
-__device__ __forceinline__ void load_record(const Record<M>* __restrict__ in, uint64_t i,
-                                            typename M::State& x, uint64_t& key) {
-  const ulonglong2* v = reinterpret_cast<const ulonglong2*>(in + i);
-  uint64_t r[Record<M>::RW];
-#pragma unroll
-  for (int k = 0; k < Record<M>::RW / 2; ++k) {
-    const ulonglong2 q = v[k];
-    r[2 * k] = q.x;
-    r[2 * k + 1] = q.y;
-  }
-  record_unpack<M>(r, x, key);
-}
 template <class M>
 __device__ __forceinline__ uint64_t record_key(const Record<M>* __restrict__ in, uint64_t i) {
   return in[i].w[0];
@@ -126,34 +111,42 @@ __device__ __forceinline__ void head_to_host(const Counters* __restrict__ C, uns
   h[3] = ld_agent(&C->batch_used);
   h[4] = ld_agent(&C->cand_total);
   h[5] = ld_agent(&C->level_new);
+  h[7] = ld_agent(&C->defer_flags);
+  h[9] = ld_agent(&C->defer_err);
 }
 // Level head reset at the start of expand (one launch instead of fills),
-// with the candidate overflow list's count.
-__global__ void k_head_reset(Counters* __restrict__ C, unsigned long long* __restrict__ ovf_count) {
+// with the candidate overflow list's count and the staging cursor.
+__global__ void k_head_reset(Counters* __restrict__ C, unsigned long long* __restrict__ ovf_count,
+                             unsigned long long* __restrict__ stage_cur) {
   if (threadIdx.x == 0) {
     C->err_key = ~0ull;
     C->chunk_base = 0;
     C->overflow = 0;
     C->batch_used = 0;
     C->emit_done = 0;
+    C->defer_flags = 0;
+    C->defer_err = ~0ull;
     *ovf_count = 0;
+    *stage_cur = 0;
   }
 }
 // row != nullptr (ShardBase::expand_dev): the all-gather row too, in device
 // memory: totals, status_new, status_err (level 1: an Init-state invariant
 // key, 0x12, found by expand takes the status slot, as Group::run does), and
 // the failure word.
-__device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, const uint8_t* __restrict__ cnt,
-                                             uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
-                                             const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
-                                             unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
-                                             uint64_t status_new, uint64_t status_err, int level1,
-                                             uint64_t init_err) {
-  const uint32_t o = threadIdx.x;
+// (thread o < 16: owner o's total v; thread 0 also the head and the status
+// words.  status_err takes the deferred frontier's invariant key, an error
+// of the level before, as the materialising emit would have reported it.)
+__device__ __forceinline__ void owner_row(uint32_t o, uint64_t v, uint32_t world, uint64_t* __restrict__ tot,
+                                          const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                                          unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
+                                          uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err) {
   if (o == 0) {
     head_to_host(C, host_head);
     if (row) {
       uint64_t se = status_err;
+      const uint64_t de = C->defer_err;
+      if (de < se) se = de;
       // an Init state's invariant violation is level 1's error, whatever
       // level 1's expansion found (an Assert of a lower-index Init state
       // must not hide it)
@@ -167,15 +160,24 @@ __device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, c
     }
   }
   if (o >= 16) return;
+  tot[o] = v;
+  host_tot[o] = v;
+  if (row && o < world) row[o] = v;
+}
+__device__ __forceinline__ void owner_totals(const uint32_t* __restrict__ off, const uint8_t* __restrict__ cnt,
+                                             uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
+                                             const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+                                             unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
+                                             uint64_t status_new, uint64_t status_err, int level1,
+                                             uint64_t init_err) {
+  const uint32_t o = threadIdx.x;
   uint64_t v = 0;
   if (world > 1 && o < world && n > 0) {
     const uint64_t end = (o + 1 < world) ? (uint64_t)off[(uint64_t)(o + 1) * n]
                                          : (uint64_t)off[(uint64_t)world * n - 1] + cnt[(uint64_t)world * n - 1];
     v = end - off[(uint64_t)o * n];
   }
-  tot[o] = v;
-  host_tot[o] = v;
-  if (row && o < world) row[o] = v;
+  owner_row(o, v, world, tot, C, host_tot, host_head, row, status_new, status_err, level1, init_err);
 }
 __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint8_t* __restrict__ cnt,
                                uint64_t n, uint32_t world, uint64_t* __restrict__ tot,
@@ -183,6 +185,60 @@ __global__ void k_owner_totals(const uint32_t* __restrict__ off, const uint8_t* 
                                unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row,
                                uint64_t status_new, uint64_t status_err, int level1, uint64_t init_err) {
   owner_totals(off, cnt, n, world, tot, C, host_tot, host_head, row, status_new, status_err, level1, init_err);
+}
+
+// Owner-major exclusive scan of the tiles' per-owner record counts (k_claim
+// with staging: tcnt[o][tile], world x T cells) -> toff, the send-buffer
+// position of each (owner, tile) segment; the owner totals then go to the
+// all-gather row and the host as in owner_totals.  One workgroup (the
+// engine's k_tile_scan body), instead of a device scan over world x n
+// per-parent cells and a totals launch.
+__global__ void __launch_bounds__(TSCAN_THREADS)
+k_owner_tscan(const uint32_t* __restrict__ tcnt, uint32_t T, uint32_t world, uint32_t* __restrict__ toff,
+              uint64_t* __restrict__ tot, const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+              unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row, uint64_t status_new,
+              uint64_t status_err, int level1, uint64_t init_err) {
+  __shared__ unsigned int sh_mark[17];
+  const uint32_t cells = world * T;
+  tile_scan_body(tcnt, cells, toff, 1, ScanMarks{T, world, cells}, sh_mark);
+  if (threadIdx.x < 64) {
+    const uint32_t o = threadIdx.x;
+    const uint64_t v = o < world ? (uint64_t)(sh_mark[o + 1 < world ? o + 1 : world] - sh_mark[o]) : 0ull;
+    owner_row(o, world > 1 ? v : 0ull, world, tot, C, host_tot, host_head, row, status_new, status_err, level1,
+              init_err);
+  }
+}
+// The staged records into the send buffer (pack without re-expansion): one
+// workgroup per tile moves its segment, owner by owner, to toff[o][tile].
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_gather(const Record<M>* __restrict__ stage, const unsigned long long* __restrict__ stoff,
+               const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ toff, uint32_t T, uint32_t world,
+               Record<M>* __restrict__ out) {
+  constexpr int U = Record<M>::RW / 2;     // 16-B units per record
+  __shared__ uint32_t sh_n[16], sh_src[16], sh_dst[16];
+  const uint32_t tile = blockIdx.x;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t o = 0; o < world; ++o) {
+      const uint32_t c = tcnt[(uint64_t)o * T + tile];
+      sh_n[o] = c;
+      sh_src[o] = acc;
+      sh_dst[o] = toff[(uint64_t)o * T + tile];
+      acc += c;
+    }
+  }
+  __syncthreads();
+  const unsigned long long b = stoff[tile];
+  if (b == ~0ull) return;
+  const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + b);
+  ulonglong2* dst = reinterpret_cast<ulonglong2*>(out);
+  for (uint32_t o = 0; o < world; ++o) {
+    const uint32_t units = sh_n[o] * U;
+    const ulonglong2* s = src + (uint64_t)sh_src[o] * U;
+    ulonglong2* d = dst + (uint64_t)sh_dst[o] * U;
+    for (uint32_t u = threadIdx.x; u < units; u += blockDim.x) d[u] = s[u];
+  }
 }
 
 // 8-bit per-owner counts widened for the owner-major scan
@@ -219,27 +275,39 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
 // PASS 0: candidates fold their claims (a displaced local claim loses its
 // newmask bit, the displacer is flagged); PASS 1: inserters and displacers
 // win iff the stored claim is still theirs.
+// PASS 1 with rtot: the block's winners (the record half of k_win_scan's input).
 template <class M, int PASS>
 __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __restrict__ in, uint64_t n,
                                            ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
                                            uint32_t rank, const unsigned long long* __restrict__ rfp,
                                            unsigned int* __restrict__ flag, uint32_t* __restrict__ newmask,
-                                           uint64_t nlocal, uint32_t* __restrict__ isnew, Counters* __restrict__ C) {
+                                           uint64_t nlocal, uint32_t* __restrict__ isnew, Counters* __restrict__ C,
+                                           uint32_t* __restrict__ rtot) {
   const uint64_t i = blk * 256 + threadIdx.x;
-  if (i >= n) return;
-  const unsigned int fl = flag[i];
   if (PASS == 0) {
+    if (i >= n) return;
+    const unsigned int fl = flag[i];
     if (fl != RF_CAND) return;
     const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
     const unsigned long long prev = claimset_store_claim(cs, nslots, rfp[i], claim);
     if (prev < ~claim) settle_displace(prev, level, rank, 0, nlocal, newmask, C, &flag[i], RF_DISPLACER);
   } else {
     uint32_t w = 0;
-    if (fl >= RF_INSERTER) {
-      const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
-      w = ~claimset_get(cs, nslots, rfp[i]) == claim ? 1u : 0u;
+    if (i < n) {
+      const unsigned int fl = flag[i];
+      if (fl >= RF_INSERTER) {
+        const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
+        w = ~claimset_get(cs, nslots, rfp[i]) == claim ? 1u : 0u;
+      }
+      isnew[i] = w;
     }
-    isnew[i] = w;
+    if (rtot) {
+      __shared__ unsigned int sh_rw[4];
+      const unsigned long long b = __ballot(w != 0);
+      if ((threadIdx.x & 63) == 0) sh_rw[threadIdx.x >> 6] = (unsigned)__popcll(b);
+      __syncthreads();
+      if (threadIdx.x == 0) rtot[blk] = sh_rw[0] + sh_rw[1] + sh_rw[2] + sh_rw[3];
+    }
   }
 }
 // One settle pass over this rank's own claim tiles (blocks [0, tiles)), the
@@ -248,23 +316,51 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
 // (atomicMax claims; a displaced candidate has no bit; with no per-tile
 // counts here, overflow winners set their bits like tile winners).  Pass A
 // also resets the level's error key for the emits.
-template <class M, int PASS>
+// wtot != nullptr (PASS 1, the tile-count path): the own tiles' new-state
+// counts go to wtot[0, tiles) and the record blocks' winners to
+// wtot[tiles, tiles + rblocks) — k_win_scan's input — and the launch has no
+// overflow-list blocks: their pass B adds to the tile counts afterwards
+// (k_settle_ovf<1>), as the engine's does, so no winner is counted twice.
+// (TP own tiles per workgroup, settle_tiles: the first ceil(tiles / TP) blocks)
+template <class M, int PASS, int TP = 1>
 __global__ void __launch_bounds__(256)
 k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots,
               uint32_t level, uint32_t rank, const unsigned int* __restrict__ rcount,
               const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
               uint32_t* __restrict__ newmask, const Record<M>* __restrict__ in, uint64_t n,
               const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
-              uint32_t* __restrict__ isnew, Counters* __restrict__ C, CandOvf ovf) {
+              uint32_t* __restrict__ isnew, Counters* __restrict__ C, CandOvf ovf, uint32_t* __restrict__ wtot) {
   static_assert(CLAIM_TILE == 256, "one block size for both halves");
   if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0) C->err_key = ~0ull;   // (nothing before the emits sets it)
-  if (blockIdx.x < tiles)
-    settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank, nullptr);
-  else if (blockIdx.x < tiles + rblocks)
-    rec_settle<M, PASS>(blockIdx.x - tiles, in, n, cs, nslots, level, rank, rfp, flag, newmask, n_local, isnew, C);
-  else
-    settle_ovf_blocks<PASS>(blockIdx.x - tiles - rblocks, gridDim.x - tiles - rblocks, ovf, n_local, 0, cs, nslots,
+  const uint32_t tb = (tiles + TP - 1) / TP;
+  if (blockIdx.x < tb) {
+    if (TP == 1)
+      settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank,
+                        PASS == 1 ? wtot : nullptr);
+    else
+      settle_tiles<PASS, TP>(blockIdx.x * TP, tiles, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask,
+                             C, rank, PASS == 1 ? wtot : nullptr);
+  } else if (blockIdx.x < tb + rblocks) {
+    rec_settle<M, PASS>(blockIdx.x - tb, in, n, cs, nslots, level, rank, rfp, flag, newmask, n_local, isnew, C,
+                        PASS == 1 && wtot ? wtot + tiles : nullptr);
+  } else {
+    settle_ovf_blocks<PASS>(blockIdx.x - tb - rblocks, gridDim.x - tb - rblocks, ovf, n_local, 0, cs, nslots,
                             level, newmask, C, rank, nullptr);
+  }
+}
+// Positions of the level's new states (the tile-count path): one scan over
+// [own tiles' counts | record blocks' winners] -> woff; chunk_base = this
+// rank's own new states (the records' emit base), level_new = all.
+__global__ void __launch_bounds__(TSCAN_THREADS)
+k_win_scan(const uint32_t* __restrict__ wtot, uint32_t tiles, uint32_t rblocks, uint32_t* __restrict__ woff,
+           Counters* __restrict__ C) {
+  __shared__ unsigned int sh_mark[4];
+  const uint32_t cells = tiles + rblocks;
+  tile_scan_body(wtot, cells, woff, 1, ScanMarks{cells, 2, tiles}, sh_mark);
+  if (threadIdx.x == 0) {
+    C->chunk_base = sh_mark[2];
+    C->level_new = sh_mark[1];
+  }
 }
 constexpr unsigned SHARD_OVF_BLOCKS = 256;
 
@@ -357,9 +453,30 @@ __global__ void k_shard_base(const uint32_t* __restrict__ offsets, const uint32_
 
 // The winners among the received records, after the local ones (one
 // workgroup's share).
+// (boff != nullptr, the tile-count path: the block's first position, the
+// rest from the block's own isnew flags; else per-record offsets ioff after
+// the own states, chunk_base)
+__device__ __forceinline__ uint64_t rec_block_pos(uint64_t blk, uint64_t i, uint64_t n,
+                                                  const uint32_t* __restrict__ isnew,
+                                                  const uint32_t* __restrict__ ioff,
+                                                  const uint32_t* __restrict__ boff, const Counters* __restrict__ C,
+                                                  bool* won) {
+  const bool w = i < n && isnew[i];
+  *won = w;
+  if (!boff) return w ? C->chunk_base + ioff[i] : 0ull;
+  __shared__ unsigned int sh_rw[4];
+  const unsigned long long b = __ballot(w);
+  const unsigned lane = threadIdx.x & 63;
+  if (lane == 0) sh_rw[threadIdx.x >> 6] = (unsigned)__popcll(b);
+  __syncthreads();
+  unsigned before = 0;
+  for (unsigned k = 0; k < (threadIdx.x >> 6); ++k) before += sh_rw[k];
+  return (uint64_t)boff[blk] + before + (unsigned)__popcll(b & ((1ull << lane) - 1ull));
+}
 template <class M>
 __device__ __forceinline__ void emit_rec_block(uint64_t blk, const Record<M>* __restrict__ in, uint64_t n,
                                                const uint32_t* __restrict__ isnew, const uint32_t* __restrict__ ioff,
+                                               const uint32_t* __restrict__ boff,
                                                Flags f, typename M::State* __restrict__ next,
                                                unsigned long long* __restrict__ pkeys, uint64_t next_gidx,
                                                Counters* __restrict__ C) {
@@ -370,11 +487,12 @@ __device__ __forceinline__ void emit_rec_block(uint64_t blk, const Record<M>* __
   __syncthreads();
   const uint64_t i = blk * blockDim.x + threadIdx.x;
   unsigned long long cand = 0;
-  if (i < n && isnew[i]) {
+  bool won;
+  const uint64_t o = rec_block_pos(blk, i, n, isnew, ioff, boff, C, &won);
+  if (won) {
     typename M::State x;
     uint64_t key;
     load_record<M>(in, i, x, key);
-    const uint64_t o = C->chunk_base + ioff[i];
     store_state<M>(next, o, x);
     pkeys[next_gidx + o] = key;
     if (M::check(x, f.inv_mask) >= 0) atomicMin(&C->err_key, (key & ~0xffull) | E_INVARIANT);
@@ -414,6 +532,8 @@ __global__ void __launch_bounds__(64) k_shard_cand(Counters* __restrict__ C,
 // workgroup to finish runs k_shard_cand's tail; a wide level's grid would
 // queue that many device-scope atomics and fences on one counter
 // (measured: NP=2 sharded 172 -> 680 ms), so it takes the separate launch.
+// woff != nullptr: the tile-count path (k_win_scan's offsets: own tiles,
+// then record blocks); else per-parent offsets and per-record ioff.
 template <class M>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_shard_emit(const typename M::State* __restrict__ cur, uint64_t n_local, uint32_t lblocks, Flags f, uint64_t rank,
@@ -421,13 +541,14 @@ k_shard_emit(const typename M::State* __restrict__ cur, uint64_t n_local, uint32
              const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
              const uint32_t* __restrict__ ioff, typename M::State* __restrict__ next,
              unsigned long long* __restrict__ pkeys, uint64_t next_gidx, Counters* __restrict__ C,
-             unsigned long long* __restrict__ host_head, int tail) {
+             unsigned long long* __restrict__ host_head, int tail, const uint32_t* __restrict__ woff) {
   __shared__ bool sh_last;
   if (blockIdx.x < lblocks)
-    emit_body<M, 0, true>(cur, n_local, 0, f, newmask, offsets, next, 0, 0, next_gidx, pkeys, nullptr, 1, C, nullptr,
+    emit_body<M, 0, true>(cur, n_local, 0, f, newmask, offsets, next, 0, 0, next_gidx, pkeys, nullptr, 1, C, woff,
                           rank);
   else
-    emit_rec_block<M>(blockIdx.x - lblocks, in, n, isnew, ioff, f, next, pkeys, next_gidx, C);
+    emit_rec_block<M>(blockIdx.x - lblocks, in, n, isnew, ioff, woff ? woff + lblocks : nullptr, f, next, pkeys,
+                      next_gidx, C);
   if (!tail) return;
   // every thread's atomics (error key, stripes) before this workgroup counts as done
   __threadfence();
@@ -440,6 +561,114 @@ k_shard_emit(const typename M::State* __restrict__ cur, uint64_t n_local, uint32
   level_tail(C, host_head);
 }
 constexpr unsigned SHARD_TAIL_BLOCKS = 64;    // emit grids up to this size run the level tail themselves
+
+// The deferred frontier's emit (round 5; the engine's k_emit_links on the
+// sharded path): per new state only its link and its parent key (TLC's
+// trace file) — own winners at their tile offsets in (parent, position)
+// order (link parent << 8 | position), then the received records' winners
+// in receive order (link bit 63 | record index: the next level's k_claim
+// reads the state from this level's receive buffer).  No state is built,
+// stored, checked or planned here: the next level's k_claim rebuilds each
+// state as it expands it (shard_rebuild).  Entries at or past `cap` are not
+// written and set DF_CAPACITY; the host grows the buffers and runs the
+// launch again (it writes nothing else).
+template <class M>
+__global__ void __launch_bounds__(256)
+k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint32_t* __restrict__ newmask,
+                   const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
+                   const uint32_t* __restrict__ woff, unsigned long long* __restrict__ link,
+                   unsigned long long* __restrict__ pkeys, uint64_t next_gidx, uint64_t cap,
+                   Counters* __restrict__ C, unsigned long long* __restrict__ host_head, int tail) {
+  __shared__ unsigned int sh_wtot[4];
+  __shared__ bool sh_last;
+  bool over = false;
+  if (blockIdx.x < lblocks) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t mask = i < n_local ? newmask[i] : 0u;
+    const int cnt = __builtin_popcount(mask);
+    const int lane = (int)(threadIdx.x & 63);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    const int wtot = __shfl(incl, 63, 64);
+    const int excl = incl - cnt;
+    if (lane == 0) sh_wtot[threadIdx.x >> 6] = (unsigned int)wtot;
+    __syncthreads();
+    uint64_t obase = woff[blockIdx.x];
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) obase += sh_wtot[w];
+    const uint64_t wave0 = i - (uint64_t)lane;
+    for (int r = 0; r < wtot; r += 64) {
+      const int g = r + lane;
+      int p = 0;                                       // last lane with excl <= g
+#pragma unroll
+      for (int b = 32; b > 0; b >>= 1) {
+        const int e = __shfl(excl, p + b, 64);
+        if (e <= g) p += b;
+      }
+      int k = g - __shfl(excl, p, 64);
+      uint32_t m = (uint32_t)__shfl((int)mask, p, 64);
+      if (g >= wtot) continue;
+      for (; k > 0; --k) m &= m - 1;
+      const uint64_t t = (uint64_t)(__ffs(m) - 1);
+      const uint64_t pidx = wave0 + (uint64_t)p;
+      const uint64_t o = obase + (uint64_t)g;
+      if (o >= cap) {
+        over = true;
+        continue;
+      }
+      link[o] = (pidx << 8) | t;
+      pkeys[next_gidx + o] = (rank << 60) | (pidx << 16) | (t << 8);
+    }
+  } else {
+    const uint64_t blk = blockIdx.x - lblocks;
+    const uint64_t i = blk * blockDim.x + threadIdx.x;
+    bool won;
+    const uint64_t o = rec_block_pos(blk, i, n, isnew, nullptr, woff + lblocks, C, &won);
+    if (won) {
+      if (o >= cap) {
+        over = true;
+      } else {
+        link[o] = (1ull << 63) | i;
+        pkeys[next_gidx + o] = in[i].w[0];
+      }
+    }
+  }
+  if (over) atomicOr(&C->defer_flags, DF_CAPACITY);
+  if (!tail) return;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) sh_last = atomicAdd(&C->emit_done, 1ull) == gridDim.x - 1;
+  __syncthreads();
+  if (!sh_last || threadIdx.x >= 64) return;
+  __threadfence();
+  if (threadIdx.x == 0) C->emit_done = 0;
+  level_tail(C, host_head);
+}
+
+// A deferred frontier materialised outside k_claim (before a narrow batch,
+// at a max_levels stop): the same rebuild, plus the level's successor count.
+template <class M>
+__global__ void __launch_bounds__(256) k_shard_materialize(DeferArgs df, uint64_t n, Flags f, uint64_t rank,
+                                                           Counters* __restrict__ C) {
+  __shared__ unsigned int sh_actd[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh_actd[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cand = 0;
+  if (i < n) {
+    const typename M::State s = shard_rebuild<M, 1>(df, i, f, rank, sh_actd, C);
+    cand = (unsigned long long)M::plan(s, f).total;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cand += __shfl_down(cand, off, 64);
+  if ((threadIdx.x & 63) == 0 && cand) atomicAdd(&stripe(C).next_cand, cand);
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh_actd[threadIdx.x])
+    atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)sh_actd[threadIdx.x]);
+}
 
 // ---- seen-set spill (cfg.seen_hbm_bytes > 0), per rank: the engine's hot
 // ClaimSet + cold runs (coldset.h, engine_spill.h) over this rank's share of
@@ -514,6 +743,18 @@ class ShardT final : public ShardBase {
     spill_ = cfg.seen_hbm_bytes > 0;
     if (cfg.spill_dir) spill_dir_ = cfg.spill_dir;   // (the seen-set's disk tier)
     cfg_.spill_dir = nullptr;      // (the caller's string is not kept)
+    // A/B switches (round 5): KC_STAGE=0 packs every level with k_shard_pack
+    // (re-expansion + per-parent owner scan); KC_SHARD_TSCAN=0 positions the
+    // winners with per-parent / per-record device scans
+    const char* sg = getenv("KC_STAGE");
+    stage_on_ = !(sg && sg[0] == '0');
+    const char* ts = getenv("KC_SHARD_TSCAN");
+    tcount_ = !(ts && ts[0] == '0');
+    const char* tp = getenv("KC_SETTLE_TP");
+    if (tp) {
+      const int v = atoi(tp);
+      settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
+    }
   }
   ~ShardT() override { release(); }
 
@@ -538,6 +779,7 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipHostMalloc(&h_exp_, kCtrHead));
     KC_HIP_TRY(hipMalloc(&d_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipMalloc(&d_ovf_cnt_, 8));     // (zeroed by k_head_reset every level)
+    KC_HIP_TRY(hipMalloc(&d_stage_cur_, 8));   // (likewise)
     KC_HIP_TRY(hipHostMalloc(&h_owner_base_, 16 * sizeof(uint64_t)));
     KC_HIP_TRY(hipEventCreate(&ev_[0]));
     KC_HIP_TRY(hipEventCreate(&ev_[1]));
@@ -594,6 +836,12 @@ class ShardT final : public ShardBase {
     }
     n_ = mine.size();
     init_key_ = init_err_;
+    cur_deferred_ = false;
+    emitted_links_ = false;
+    cand_est_ = next_cand_est_ = false;
+    last_new_ = 0;
+    prev_rec_ = nullptr;
+    defer_err_ = ~0ull;
     level_ = 1;
     level_base_.assign(1, 0);
     gen_init_ = n_;
@@ -625,7 +873,8 @@ class ShardT final : public ShardBase {
   }
   int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
-    hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_, d_ovf_cnt_);
+    rebuilt_ = false;
+    hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_, d_ovf_cnt_, d_stage_cur_);
     send_total_ = 0;
     dev_init_err_ = init_err_;
     init_err_ = ~0ull;
@@ -653,7 +902,9 @@ class ShardT final : public ShardBase {
       const uint64_t need = std::min<uint64_t>(cand_, (uint64_t)((double)cand_ * sp_ratio_ * 1.25) + 4096);
       if (cs_.count > 0 && cs_.count + need > hot_limit_) KC_TRY(spill_flush());
     } else {
-      KC_TRY(cs_.reserve(cand_, st_));
+      // (a deferred frontier's successor count is an estimate: 16 per parent
+      // at least, so even MAXSUCC = 32 cannot fill the table, as the engine)
+      KC_TRY(cs_.reserve(cand_est_ ? std::max<uint64_t>(cand_, 16 * n_) : cand_, st_));
     }
     const uint64_t tiles = (n_ + CLAIM_TILE - 1) / CLAIM_TILE;
     KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
@@ -662,7 +913,9 @@ class ShardT final : public ShardBase {
     // candidates past a tile's segment: one overflow list, bounded by the
     // level's successor count
     {
-      const uint64_t bound = std::max<uint64_t>(cand_, 1);
+      // (estimated: at least two per parent; the list holds only the
+      // candidates past a tile's first 256, a few percent of the successors)
+      const uint64_t bound = cand_est_ ? std::max<uint64_t>(cand_, 2 * n_) : std::max<uint64_t>(cand_, 1);
       KC_TRY(grow_buffer_tight(ovf_fp_, ovf_fp_cap_, bound, st_));
       KC_TRY(grow_buffer_tight(ovf_lk_, ovf_lk_cap_, bound, st_));
       KC_TRY(grow_buffer_tight(ovf_tile_, ovf_tile_cap_, bound, st_));
@@ -670,7 +923,6 @@ class ShardT final : public ShardBase {
     }
     KC_TRY(grow_buffer(newmask_, mask_cap_, n_, false, st_));
     KC_TRY(grow_buffer(cnt_, cnt_cap_, n_ * world_, false, st_));
-    KC_TRY(grow_buffer(off_, off_cap_, n_ * world_, false, st_));
     KC_TRY(grow_buffer(repmask_, rm_cap_, n_, false, st_));
     ShardArgs sh;
     sh.world = (uint32_t)world_;
@@ -678,7 +930,44 @@ class ShardT final : public ShardBase {
     sh.repmask = repmask_;
     sh.cnt = cnt_;
     sh.ovf = ovf_;
+    // record staging (world > 1): an estimate from the last level's records
+    // per parent, at most the level's successors; a level past it packs the
+    // old way (DF_STAGE, pack())
+    stage_level_ = world_ > 1 && stage_on_;
+    if (stage_level_) {
+      const uint64_t est = std::min<uint64_t>(std::max<uint64_t>(cand_, 1),
+                                              (uint64_t)((double)n_ * rec_ratio_ * 1.5) + 65536);
+      KC_TRY(grow_buffer_tight(stage_, stage_cap_, est, st_));
+      const uint64_t cells = tiles * (uint64_t)world_;
+      KC_TRY(grow_buffer(tcnt_, tcnt_cap_, cells + 8, false, st_));
+      KC_TRY(grow_buffer(toff_, toff_cap_, cells + 8, false, st_));
+      KC_TRY(grow_buffer(stoff_, stoff_cap_, tiles, false, st_));
+      sh.stage = stage_;
+      sh.stage_cur = d_stage_cur_;
+      sh.stage_cap = stage_cap_;
+      sh.tcnt = tcnt_;
+      sh.stoff = stoff_;
+    }
     const size_t dyn = (size_t)(CLAIM_TILE + ((world_ + 3) / 4) * CLAIM_TILE) * sizeof(unsigned int);
+    // the deferred frontier: this level's plans kept for the next level's
+    // rebuild; a deferred frontier rebuilt into cur_ (the free buffer) from
+    // the previous frontier (next_) and the last receive buffer
+    DeferArgs df;
+    if (defer_on_) {
+      KC_TRY(grow_buffer(pc_cur_, pc_cur_cap_, n_, false, st_));
+      df.counts_out = pc_cur_;
+    }
+    rebuilt_ = cur_deferred_;
+    if (cur_deferred_) {
+      KC_TRY(grow_buffer(cur_, cur_cap_, n_, false, st_));
+      df.prev = next_;
+      df.link = link_cur_;
+      df.prev_rec = prev_rec_;
+      df.out = cur_;
+      df.prev_counts = pc_prev_;
+      cur_deferred_ = false;
+      ++deferred_levels_;
+    }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[0], st_));
     if (world_ == 1) {
       // one rank owns everything: the single-GPU engine's claim kernel (no
@@ -686,17 +975,31 @@ class ShardT final : public ShardBase {
       hipLaunchKernelGGL((k_claim<M, 0, false, 1>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
-                         d_ctr_, sh);
+                         d_ctr_, sh, df);
     } else {
       hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
-                         d_ctr_, sh);
+                         d_ctr_, sh, df);
     }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[1], st_));
+    if (stage_level_) {
+      // positions of the tiles' segments in the owner-grouped send buffer and
+      // the owner totals (the all-gather row)
+      if (tiles * (uint64_t)world_ >= (1ull << 31)) {
+        set_error("kc_shard_expand: %llu tile x owner cells exceed one scan", (unsigned long long)(tiles * world_));
+        return -ENOMEM;
+      }
+      hipLaunchKernelGGL(k_owner_tscan, dim3(1), dim3(TSCAN_THREADS), 0, st_, tcnt_, (uint32_t)tiles, (uint32_t)world_,
+                         toff_, d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
+                         d_row, status_new, status_err, (int)level1, dev_init_err_);
+      KC_HIP_TRY(hipGetLastError());
+      return 0;
+    }
     // one exclusive scan over the owner-major matrix = every record's position
     // in the owner-grouped send buffer (nothing to send at world 1)
     const uint64_t cells = n_ * (uint64_t)world_;
+    KC_TRY(grow_buffer(off_, off_cap_, cells, false, st_));
     if (cells >= (1ull << 31)) {
       set_error("kc_shard_expand: frontier x world = %llu cells exceeds one scan (2^31)",
                 (unsigned long long)cells);
@@ -725,7 +1028,9 @@ class ShardT final : public ShardBase {
   int expand_done(uint64_t* counts, uint64_t* err_key) override {
     for (int o = 0; o < world_; ++o) counts[o] = 0;
     *err_key = dev_init_err_;
+    defer_err_ = ~0ull;
     if (dev_zero_) return 0;
+    defer_err_ = h_exp_->defer_err;
     const bool init_violated = dev_init_err_ != ~0ull;   // then it is THE error (see k_owner_totals)
     if (cfg_.timing) {
       float ms = 0;
@@ -740,10 +1045,13 @@ class ShardT final : public ShardBase {
       set_error("kc_shard_expand: successor overflow or full table");
       return -ENOMEM;
     }
+    staged_ = stage_level_ && !(h_exp_->defer_flags & DF_STAGE);
+    if (stage_level_ && !staged_) ++stage_fallbacks_;
     for (int o = 0; o < world_; ++o) {
       counts[o] = h_owner_base_[o];
       send_total_ += counts[o];
     }
+    if (n_) rec_ratio_ = std::max(0.01, (double)(send_total_ - counts[rank_]) / (double)n_);
     if (h_exp_->err_key != ~0ull && !init_violated)
       *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_exp_->err_key);
     return 0;
@@ -810,7 +1118,24 @@ class ShardT final : public ShardBase {
 
   int pack(void* send) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
-    if (n_ && send_total_) {
+    if (n_ && send_total_ && staged_) {
+      // the tiles' staged segments, in tile order per owner
+      const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
+      hipLaunchKernelGGL(k_shard_gather<M>, dim3(tiles), dim3(256), 0, st_, stage_, stoff_, tcnt_, toff_, tiles,
+                         (uint32_t)world_, (Rec*)send);
+      KC_HIP_TRY(hipGetLastError());
+    } else if (n_ && send_total_) {
+      if (stage_level_) {
+        // (staging overflowed this level: the per-parent owner-major scan
+        // that k_shard_pack positions its records with)
+        const uint64_t cells = n_ * (uint64_t)world_;
+        KC_TRY(grow_buffer(off_, off_cap_, cells, false, st_));
+        size_t tmp_bytes = 0;
+        const hipcub::TransformInputIterator<uint32_t, Widen8, const uint8_t*> cnt32(cnt_, Widen8());
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt32, off_, (int)cells, st_));
+        KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+        KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, cnt32, off_, (int)cells, st_));
+      }
       hipLaunchKernelGGL(k_shard_pack<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
                          cur_, n_, flags_, (uint32_t)world_, (uint64_t)rank_, off_, repmask_,
                          (Rec*)send);
@@ -830,6 +1155,12 @@ class ShardT final : public ShardBase {
     *n_new = 0;
     *err_key = ~0ull;
     next_n_ = 0;
+    next_cand_ = 0;
+    next_cand_est_ = false;
+    last_new_ = 0;
+    // (an empty level emits nothing: advance must not take the last level's
+    // links or plans for this one's)
+    emitted_links_ = false;
     if (n_ == 0 && n == 0) return 0;
     if (n >= (1ull << 31) || n_ >= (1ull << 31)) {
       set_error("kc_shard_insert: more than 2^31 records or parents in one level");
@@ -850,42 +1181,116 @@ class ShardT final : public ShardBase {
     // settle pass A (own tiles, records and the tiles' overflow list in one
     // launch), then pass B; n_ = 0 with n > 0 still runs pass A's first
     // workgroup, which resets the error key
-    const unsigned lt = n_ ? tiles : 0u, ob = n_ ? SHARD_OVF_BLOCKS : 0u;
-    const unsigned sgrid = std::max(lt + (n ? rgrid : 0u) + ob, 1u);
-    hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(sgrid), dim3(256), 0, st_, lt, n ? rgrid : 0u, n_, cs_.t,
-                       cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
-                       flag_, isnew_, d_ctr_, ovf_);
-    hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, n ? rgrid : 0u, n_, cs_.t,
-                       cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
-                       flag_, isnew_, d_ctr_, ovf_);
-    // positions: this rank's own winners first, then the records'
-    KC_TRY(scan_winners(n));
-    if (spill_) {
-      bool changed = false;
-      KC_TRY(spill_check(n, tiles, rgrid, &changed));
-      if (changed) KC_TRY(scan_winners(n));
+    const unsigned lt = n_ ? tiles : 0u, ob = n_ ? SHARD_OVF_BLOCKS : 0u, rb = n ? rgrid : 0u;
+    const unsigned sgrid = std::max(lt + rb + ob, 1u);
+    // the tile-count path (not with the seen-set spill, whose cold check
+    // works on per-parent / per-record offsets): pass B counts each own
+    // tile's and each record block's new states, the overflow list's pass B
+    // adds its winners to their tiles, one scan positions them all
+    const bool tc = tcount_ && !spill_;
+    // (KC_SETTLE_TP own tiles per settle workgroup on the tile-count path)
+    const int tp = tc ? settle_tp_ : 1;
+    auto settle = [&](int pass, unsigned ob_blocks, uint32_t* wt) {
+      const unsigned tb = (lt + tp - 1) / tp, g = std::max(tb + rb + ob_blocks, 1u);
+#define KC_SB(P, T)                                                                                         \
+  hipLaunchKernelGGL((k_settle_both<M, P, T>), dim3(g), dim3(256), 0, st_, lt, rb, n_, cs_.t, cs_.nslots,   \
+                     succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, \
+                     isnew_, d_ctr_, ovf_, wt)
+      if (pass == 0) {
+        if (tp == 2) KC_SB(0, 2); else if (tp == 4) KC_SB(0, 4); else if (tp == 8) KC_SB(0, 8); else KC_SB(0, 1);
+      } else {
+        if (tp == 2) KC_SB(1, 2); else if (tp == 4) KC_SB(1, 4); else if (tp == 8) KC_SB(1, 8); else KC_SB(1, 1);
+      }
+#undef KC_SB
+    };
+    settle(0, ob, (uint32_t*)nullptr);
+    if (tc) {
+      KC_TRY(grow_buffer(wtot_, wtot_cap_, (uint64_t)lt + rb + 8, false, st_));
+      KC_TRY(grow_buffer(woff_, woff_cap_, (uint64_t)lt + rb + 8, false, st_));
+      if (lt + rb) settle(1, 0, wtot_);
+      if (n_)
+        hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SHARD_OVF_BLOCKS), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
+                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, wtot_);
+      hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
+    } else {
+      hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, rb, n_, cs_.t,
+                         cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
+                         flag_, isnew_, d_ctr_, ovf_, (uint32_t*)nullptr);
+      // positions: this rank's own winners first, then the records'
+      KC_TRY(scan_winners(n));
+      if (spill_) {
+        bool changed = false;
+        KC_TRY(spill_check(n, tiles, rgrid, &changed));
+        if (changed) KC_TRY(scan_winners(n));
+      }
     }
     // capacity: at most one new state per own successor and per record
+    // (the deferred frontier: links and parent keys only, sized by the
+    // estimate when the level's successor count is one; past it the emit
+    // runs again with the exact count)
+    const bool links = defer_on_ && tc;
+    emitted_links_ = links;
+    last_in_ = in;
     const uint64_t bound = cand_ + n;
-    KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
+    if (!links) KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const uint64_t next_gidx = level_base_.back() + n_;
     KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + bound + 1, true, st_));
+    if (links) KC_TRY(grow_buffer(link_next_, link_next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const unsigned lb = (unsigned)((n_ + 255) / 256), eg = std::max(lb + (n ? rgrid : 0u), 1u);
     const int tail = eg <= SHARD_TAIL_BLOCKS;
-    hipLaunchKernelGGL(k_shard_emit<M>, dim3(eg), dim3(256), 0, st_, cur_, n_, lb, flags_, (uint64_t)rank_, newmask_,
-                       offsets_, in, n, isnew_, ioff_, next_, pkeys_, next_gidx, d_ctr_,
-                       reinterpret_cast<unsigned long long*>(h_ctr_), tail);
-    if (!tail)
-      hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_, reinterpret_cast<unsigned long long*>(h_ctr_));
+    auto emit = [&]() {
+      if (links)
+        hipLaunchKernelGGL(k_shard_emit_links<M>, dim3(eg), dim3(256), 0, st_, n_, lb, (uint64_t)rank_, newmask_, in, n,
+                           isnew_, woff_, link_next_, pkeys_, next_gidx,
+                           std::min<uint64_t>(link_next_cap_, pk_cap_ - next_gidx), d_ctr_,
+                           reinterpret_cast<unsigned long long*>(h_ctr_), tail);
+      else
+        hipLaunchKernelGGL(k_shard_emit<M>, dim3(eg), dim3(256), 0, st_, cur_, n_, lb, flags_, (uint64_t)rank_,
+                           newmask_, offsets_, in, n, isnew_, ioff_, next_, pkeys_, next_gidx, d_ctr_,
+                           reinterpret_cast<unsigned long long*>(h_ctr_), tail,
+                           tc ? woff_ : (const uint32_t*)nullptr);
+      if (!tail)
+        hipLaunchKernelGGL(k_shard_cand, dim3(1), dim3(64), 0, st_, d_ctr_,
+                           reinterpret_cast<unsigned long long*>(h_ctr_));
+    };
+    emit();
     KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipStreamSynchronize(st_));
+    if (links && (h_ctr_->defer_flags & DF_CAPACITY)) {
+      const uint64_t need = h_ctr_->level_new;
+      KC_TRY(grow_buffer(link_next_, link_next_cap_, need, false, st_));
+      KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + need + 1, true, st_));
+      KC_HIP_TRY(hipMemsetAsync(&d_ctr_->defer_flags, 0, 8, st_));
+      ++emit_retries_;
+      emit();
+      KC_HIP_TRY(hipGetLastError());
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      if (h_ctr_->defer_flags & DF_CAPACITY) {
+        set_error("kc_shard_insert: %llu links do not fit %llu", (unsigned long long)need,
+                  (unsigned long long)link_next_cap_);
+        return -ENOMEM;
+      }
+    }
     if (h_ctr_->overflow || h_ctr_->batch_used) {
       set_error("kc_shard_insert: table full or claim protocol violation");
       return -ENOMEM;
     }
     next_n_ = h_ctr_->level_new;
-    next_cand_ = h_ctr_->cand_total - cand_total_;
+    const uint64_t dc = h_ctr_->cand_total - cand_total_;
     cand_total_ = h_ctr_->cand_total;
+    if (links) {
+      // successors counted this level: those of this level's rebuilt states
+      // (or none: a level k_claim did not rebuild has an exact count already);
+      // the next level's, for its buffers, estimated from them
+      const uint64_t cur_cand = rebuilt_ ? dc : cand_;
+      if (n_ && (rebuilt_ || !cand_est_)) succ_ratio_ = std::max(1.0, (double)cur_cand / (double)n_);
+      next_cand_ = next_n_ ? (uint64_t)((double)next_n_ * succ_ratio_ * 1.25) + 4096 : 0;
+      next_cand_est_ = true;
+    } else {
+      next_cand_ = dc;
+      next_cand_est_ = false;
+    }
+    last_new_ = next_n_;
     if (!spill_) cs_.count += next_n_;   // (spill: spill_check counted the hot slots)
     distinct_ += next_n_;
     if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
@@ -1098,7 +1503,13 @@ class ShardT final : public ShardBase {
     if (!rc) rc = grow_buffer(cur_, cur_cap_, bufs, true, st_);
     if (!rc) rc = grow_buffer(next_, next_cap_, bufs, false, st_);
     if (!rc) rc = grow_buffer(pkeys_, pk_cap_, base + n_ + (uint64_t)batch * per + 1, true, st_);
-    if (!rc) rc = cs_.reserve((uint64_t)batch * per, st_);
+    // ClaimSet room for the batch: a few times the first level's bound, not
+    // the batch's worst case (that forced ~2M entries on every model; ADVICE
+    // r4).  The device stops a level whose claims might not fit (room below,
+    // sn_local_stop: SN_STOP, the counted path takes it), so a reserve that
+    // finds no memory is not a failure either (the table is unchanged then).
+    if (!rc && cs_.reserve(std::min<uint64_t>((uint64_t)batch * per, 4 * (cand_ + in + 1) + (1u << 16)), st_) < 0)
+      (void)hipGetLastError();
     SNCtl& h = *h_snc_;
     memset(&h, 0, offsetof(SNCtl, lwidths));
     h.active = 1;
@@ -1153,10 +1564,9 @@ class ShardT final : public ShardBase {
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
     const SNCtl& h = *h_snc_;
-    if (h_ctr_->overflow) {
-      set_error("kc_shard narrow: a full level table or ClaimSet, or a header of another level");
-      return -ENOMEM;
-    }
+    // (the outcome is filled in before a failure is reported: the caller
+    // keeps in step with its peers on it, shard_driver.hip)
+    out->filled = true;
     out->levels = (int)h.levels;
     out->reason = h.active ? SN_RUN : h.reason;
     out->widths.assign(h.gwidths, h.gwidths + std::min<uint32_t>(h.levels, KC_MAX_LEVELS));
@@ -1177,6 +1587,10 @@ class ShardT final : public ShardBase {
     out->status_new = n_;
     out->status_err = h.err[(h.level - 1) & 1];
     out->sent = h.sent_total;
+    if (h_ctr_->overflow) {
+      set_error("kc_shard narrow: a full level table or ClaimSet, or a header of another level");
+      return -ENOMEM;
+    }
     return 0;
   }
 
@@ -1184,10 +1598,60 @@ class ShardT final : public ShardBase {
     level_base_.push_back(level_base_.back() + n_);
     std::swap(cur_, next_);
     std::swap(cur_cap_, next_cap_);
+    if (emitted_links_) {
+      // the new frontier is links into the old one (now next_) and into the
+      // receive buffer; this level's plans become the previous level's
+      std::swap(link_cur_, link_next_);
+      std::swap(link_cur_cap_, link_next_cap_);
+      std::swap(pc_cur_, pc_prev_);
+      std::swap(pc_cur_cap_, pc_prev_cap_);
+      prev_rec_ = last_in_;
+      cur_deferred_ = next_n_ > 0;
+      emitted_links_ = false;
+    }
     n_ = next_n_;
     cand_ = next_cand_;
+    cand_est_ = next_cand_est_;
     next_cand_ = 0;
+    next_cand_est_ = false;
     ++level_;
+    return 0;
+  }
+
+  void set_deferred(bool on) override { defer_on_ = on && !spill_ && tcount_; }
+  uint64_t defer_error() const override { return defer_err_; }
+  void drop_last_insert() override {
+    distinct_ -= last_new_;
+    last_new_ = 0;
+  }
+  int materialize(uint64_t* derr) override {
+    *derr = ~0ull;
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    if (!cur_deferred_ || n_ == 0) {
+      cur_deferred_ = false;
+      return 0;
+    }
+    KC_TRY(grow_buffer(cur_, cur_cap_, n_, false, st_));
+    DeferArgs df;
+    df.prev = next_;
+    df.link = link_cur_;
+    df.prev_rec = prev_rec_;
+    df.out = cur_;
+    df.prev_counts = pc_prev_;
+    KC_HIP_TRY(hipMemsetAsync(&d_ctr_->defer_err, 0xff, 8, st_));
+    hipLaunchKernelGGL(k_shard_materialize<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_, df, n_, flags_,
+                       (uint64_t)rank_, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    cur_deferred_ = false;
+    ++deferred_levels_;
+    const uint64_t tot = h_ctr_->next_cand();      // (the stripes: materialize added this level's successors)
+    cand_ = tot - cand_total_;
+    cand_total_ = tot;
+    cand_est_ = false;
+    if (n_) succ_ratio_ = std::max(1.0, (double)cand_ / (double)n_);
+    *derr = h_ctr_->defer_err;
     return 0;
   }
 
@@ -1249,7 +1713,9 @@ class ShardT final : public ShardBase {
                     (void*)ovf_fp_, (void*)ovf_lk_, (void*)ovf_tile_, (void*)d_ovf_cnt_,
                     (void*)repmask_, (void*)newmask_, (void*)offsets_, (void*)rcount_, (void*)rec_fp_,
                     (void*)rec_lk_, (void*)rfp_, (void*)flag_, (void*)isnew_, (void*)ioff_,
-                    (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_})
+                    (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_, (void*)stage_, (void*)d_stage_cur_,
+                    (void*)tcnt_, (void*)toff_, (void*)stoff_, (void*)wtot_, (void*)woff_, (void*)link_cur_,
+                    (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_exp_) (void)hipHostFree(h_exp_);
@@ -1294,6 +1760,38 @@ class ShardT final : public ShardBase {
   uint64_t rfp_cap_ = 0, flag_cap_ = 0, isnew_cap_ = 0, ioff_cap_ = 0;
   uint8_t* scan_tmp_ = nullptr;
   uint64_t scan_cap_ = 0;
+  // record staging (ShardArgs::stage; world > 1)
+  Rec* stage_ = nullptr;
+  uint64_t stage_cap_ = 0;
+  unsigned long long* d_stage_cur_ = nullptr;
+  uint32_t *tcnt_ = nullptr, *toff_ = nullptr;
+  uint64_t tcnt_cap_ = 0, toff_cap_ = 0;
+  unsigned long long* stoff_ = nullptr;
+  uint64_t stoff_cap_ = 0;
+  bool stage_on_ = true, stage_level_ = false, staged_ = false;
+  uint64_t stage_fallbacks_ = 0;       // levels packed the old way (staging estimate exceeded)
+  double rec_ratio_ = 1.0;             // records sent per parent, last level (the staging estimate)
+  // the tile-count insert path: own tiles' and record blocks' new-state counts, their scan
+  bool tcount_ = true;
+  int settle_tp_ = SETTLE_TP_DEFAULT;
+  uint32_t *wtot_ = nullptr, *woff_ = nullptr;
+  uint64_t wtot_cap_ = 0, woff_cap_ = 0;
+  // the deferred frontier (set_deferred; the native loop's counted levels)
+  bool defer_on_ = false;
+  bool cur_deferred_ = false;        // cur_ not built: link_cur_ into next_ (the previous frontier) / prev_rec_
+  bool emitted_links_ = false;       // the last insert emitted links (advance swaps them in)
+  bool rebuilt_ = false;             // this level's k_claim rebuilt its parents
+  bool cand_est_ = false, next_cand_est_ = false;   // cand_ / next_cand_ estimated, not counted
+  unsigned long long *link_cur_ = nullptr, *link_next_ = nullptr;
+  uint64_t link_cur_cap_ = 0, link_next_cap_ = 0;
+  unsigned long long *pc_cur_ = nullptr, *pc_prev_ = nullptr;   // plans of this / the previous level's parents
+  uint64_t pc_cur_cap_ = 0, pc_prev_cap_ = 0;
+  const Rec* prev_rec_ = nullptr;    // the receive buffer the links point into
+  const Rec* last_in_ = nullptr;     // the last insert's receive buffer
+  uint64_t defer_err_ = ~0ull;       // expand_done: the rebuild's invariant key
+  double succ_ratio_ = 5.0;          // successors per state, last counted (the estimates)
+  uint64_t last_new_ = 0;            // the last insert's new states (drop_last_insert)
+  uint64_t deferred_levels_ = 0, emit_retries_ = 0;
   uint64_t* d_owner_base_ = nullptr;   // per-owner record totals (device / pinned host)
   uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;

@@ -194,12 +194,45 @@ class Comm {
   virtual bool trivial() const { return false; }
 };
 
+// The emulated exchange's copies in one launch (LocalComm): a transfer list
+// of (src, dst, 16-B units) — src == nullptr writes zeroes — cut into 64 KiB
+// chunks; block b finds its transfer in the chunk prefix (at most a few
+// hundred transfers: R^2 pieces).  One launch per exchange instead of one
+// copy per piece (R = 8: 64+ copy launches per level, 47 ms of an emulated
+// NP=2 check spent in ~13K copies, profiles/r05a_attr_R8.json).
+struct CopyXfer {
+  const ulonglong2* src;
+  ulonglong2* dst;
+  uint64_t units;        // 16-B units
+  uint64_t chunk0;       // first chunk of this transfer (prefix over transfers)
+};
+constexpr uint64_t COPY_CHUNK = 4096;   // 16-B units per chunk (64 KiB)
+__global__ void __launch_bounds__(256) k_multi_copy(const CopyXfer* __restrict__ x, int nx) {
+  __shared__ int sh_x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = nx - 1;        // last transfer with chunk0 <= blockIdx.x
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (x[mid].chunk0 <= blockIdx.x) lo = mid; else hi = mid - 1;
+    }
+    sh_x = lo;
+  }
+  __syncthreads();
+  const CopyXfer t = x[sh_x];
+  const uint64_t u0 = (blockIdx.x - t.chunk0) * COPY_CHUNK;
+  const uint64_t u1 = u0 + COPY_CHUNK < t.units ? u0 + COPY_CHUNK : t.units;
+  for (uint64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x)
+    t.dst[u] = t.src ? t.src[u] : make_ulonglong2(0ull, 0ull);
+}
+
 class LocalComm final : public Comm {
  public:
   explicit LocalComm(std::vector<ShardBase*> shards) : s_(std::move(shards)) {}
   ~LocalComm() override {
     if (rows_) (void)hipFree(rows_);
     if (hrows_) (void)hipHostFree(hrows_);
+    if (xd_) (void)hipFree(xd_);
+    if (xh_) (void)hipHostFree(xh_);
   }
   int all_gather(const std::vector<std::vector<uint64_t>>& rows, std::vector<uint64_t>& out) override {
     out.clear();
@@ -237,6 +270,7 @@ class LocalComm final : public Comm {
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every pack is done
     std::vector<std::vector<Xfer>> plan(R);
     for (int r = 0; r < R; ++r) plan[r] = exchange_plan(Mx, r, piece);
+    xfers_.clear();
     for (int dst = 0; dst < R; ++dst) {
       for (int src = 0; src < R; ++src) {
         std::vector<const Xfer*> sends, recvs;
@@ -257,28 +291,23 @@ class LocalComm final : public Comm {
           }
           if (sunk[dst]) continue;                  // (the failed rank's sink takes it)
           char* to = (char*)recv[dst] + recvs[k]->off * rb;
-          if (sunk[src])                             // a failed sender's records are zeroes
-            KC_HIP_TRY(hipMemsetAsync(to, 0, sends[k]->n * rb, s_[dst]->stream()));
-          else
-            KC_HIP_TRY(hipMemcpyAsync(to, (const char*)send[src] + sends[k]->off * rb, sends[k]->n * rb,
-                                      hipMemcpyDeviceToDevice, s_[dst]->stream()));
+          // a failed sender's records are zeroes
+          const char* from = sunk[src] ? nullptr : (const char*)send[src] + sends[k]->off * rb;
+          add_xfer(from, to, sends[k]->n * rb);
         }
       }
     }
-    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
-    return 0;
+    return run_xfers();
   }
   int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot) override {
     const int R = (int)s_.size();
     if (R == 1) return 0;
     for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // every rank's slots are written
+    xfers_.clear();
     for (int d = 0; d < R; ++d)
       for (int src = 0; src < R; ++src)
-        if (src != d)
-          KC_HIP_TRY(hipMemcpyAsync((char*)recv[d] + src * slot, (const char*)send[src] + d * slot, slot,
-                                    hipMemcpyDeviceToDevice, s_[d]->stream()));
-    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));   // (before any rank's next pack)
-    return 0;
+        if (src != d) add_xfer((const char*)send[src] + d * slot, (char*)recv[d] + src * slot, slot);
+    return run_xfers();    // (synchronised: before any rank's next pack)
   }
   int broadcast(int, uint64_t*) override { return 0; }   // the driver read it from the local root
   bool trivial() const override { return s_.size() == 1; }
@@ -290,10 +319,48 @@ class LocalComm final : public Comm {
   }
 
  private:
+  void add_xfer(const void* src, void* dst, uint64_t bytes) {
+    if (!bytes) return;
+    xfers_.push_back(CopyXfer{(const ulonglong2*)src, (ulonglong2*)dst, bytes / 16, 0});
+  }
+  // the list in one launch on rank 0's stream (every stream is idle: the
+  // callers synchronised them), then that stream's sync
+  int run_xfers() {
+    if (xfers_.empty()) return 0;
+    uint64_t chunks = 0;
+    for (auto& x : xfers_) {
+      x.chunk0 = chunks;
+      chunks += (x.units + COPY_CHUNK - 1) / COPY_CHUNK;
+    }
+    if (chunks >= (1ull << 31)) {
+      set_error("emulated exchange: %llu chunks in one launch", (unsigned long long)chunks);
+      return -EIO;
+    }
+    if (xfers_.size() > xcap_) {
+      if (xd_) KC_HIP_TRY(hipFree(xd_));
+      if (xh_) KC_HIP_TRY(hipHostFree(xh_));
+      xd_ = nullptr;
+      xh_ = nullptr;
+      xcap_ = std::max<size_t>(2 * xfers_.size(), 256);
+      KC_HIP_TRY(hipMalloc(&xd_, xcap_ * sizeof(CopyXfer)));
+      KC_HIP_TRY(hipHostMalloc(&xh_, xcap_ * sizeof(CopyXfer)));
+    }
+    memcpy(xh_, xfers_.data(), xfers_.size() * sizeof(CopyXfer));
+    hipStream_t st = s_[0]->stream();
+    KC_HIP_TRY(hipMemcpyAsync(xd_, xh_, xfers_.size() * sizeof(CopyXfer), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_multi_copy, dim3((unsigned)chunks), dim3(256), 0, st, xd_, (int)xfers_.size());
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
   std::vector<ShardBase*> s_;
   uint64_t* rows_ = nullptr;
   uint64_t* hrows_ = nullptr;
   size_t rows_cap_ = 0;
+  std::vector<CopyXfer> xfers_;
+  CopyXfer* xd_ = nullptr;
+  CopyXfer* xh_ = nullptr;
+  size_t xcap_ = 0;
 };
 
 class RcclComm final : public Comm {
@@ -609,6 +676,15 @@ class Group {
     // KC_SOLO=0: a world-1 group runs the gather path too (A/B)
     const char* so = getenv("KC_SOLO");
     solo_off_ = so && so[0] == '0';
+    // KC_SERIAL=1 (diagnostic): each local shard's stage is synchronised
+    // before the next shard's launches, so emulated ranks' kernels never
+    // overlap and a kernel trace attributes time per rank (Stream_Id)
+    const char* se = getenv("KC_SERIAL");
+    serial_ = se && se[0] == '1';
+    // the deferred frontier on the counted levels (round 5); KC_SDEFER=0:
+    // every insert materialises its new states (A/B)
+    const char* sd = getenv("KC_SDEFER");
+    defer_on_ = !(sd && sd[0] == '0');
   }
   // The narrow levels' buffers, allocated with the group (a failure here is
   // the caller's before any collective of a run).
@@ -617,6 +693,7 @@ class Group {
     // cold check runs between the settle passes and the emit.  Every rank
     // runs with the same configuration, so they all decide alike.)
     if (cfg_.seen_hbm_bytes) sn_on_ = false;
+    for (auto* s : local_) s->set_deferred(defer_on_ && !cfg_.seen_hbm_bytes);
     if (!sn_on_) return 0;
     for (auto* s : local_) KC_TRY(s->sn_setup(sn_cap_));
     return 0;
@@ -688,7 +765,13 @@ class Group {
   int fault_rank_ = -1, fault_level_ = 0, fault_stage_ = 0;
   bool sn_on_ = true;
   bool solo_off_ = false;
+  bool serial_ = false;
+  bool defer_on_ = true;
   uint32_t sn_cap_ = SN_SLOT_DEFAULT;
+  // KC_SERIAL: wait for local shard i's stream (errors surface at its next call)
+  void ser(size_t i) {
+    if (serial_) (void)hipStreamSynchronize(local_[i]->stream());
+  }
 };
 
 // Failure handling: no rank may leave the loop alone, or its peers would
@@ -756,6 +839,13 @@ int Group::run(kc_result* res) {
     const bool last = cfg_.max_levels && level >= cfg_.max_levels;
     if (sn_on_ && !last && !sn_blocked) {
       const uint64_t slot = local_[0]->sn_slot_bytes();
+      // a deferred frontier is built first (the narrow kernels read states);
+      // an invariant violation among its states is the level before's error
+      for (size_t i = 0; i < nl; ++i) {
+        uint64_t d = NONE;
+        if (!fail[i]) note(i, local_[i]->materialize(&d));
+        status_err[i] = std::min(status_err[i], d);
+      }
       for (size_t i = 0; i < nl; ++i) {
         so[i] = ShardBase::SNOut{};
         if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
@@ -769,8 +859,9 @@ int Group::run(kc_result* res) {
       }
       for (int k = 0; k < sn_batch; ++k) {
         for (size_t i = 0; i < nl; ++i) {
-          // a failed rank marks its control block: the level stops every rank
-          bool f = k == 0 && fail[i];
+          // a failed rank marks its control block (at every level: a failure
+          // noted during the batch too): the level stops every rank
+          bool f = fail[i] != 0;
           if (!fail[i] && local_[i]->rank() == fault_rank_ && level + k == fault_level_) {
             set_error("kc_group_run: injected fault (KC_FAULT) on rank %d at level %d, narrow", fault_rank_,
                       level + k);
@@ -778,14 +869,28 @@ int Group::run(kc_result* res) {
             f = true;
           }
           note(i, local_[i]->sn_pre((uint32_t)k, f));
+          ser(i);
         }
         KC_TRY(comm_->sn_exchange(ss, rr, slot));
-        for (size_t i = 0; i < nl; ++i) note(i, local_[i]->sn_post((uint32_t)k));
+        for (size_t i = 0; i < nl; ++i) {
+          note(i, local_[i]->sn_post((uint32_t)k));
+          ser(i);
+        }
       }
       const ShardBase::SNOut* g = nullptr;
+      const ShardBase::SNOut* gf = nullptr;    // a shard's that failed in sn_end after filling it
       for (size_t i = 0; i < nl; ++i) {
         const bool pre = fail[i] != 0;
         note(i, local_[i]->sn_end(&so[i]));
+        // fault injection: a failure found at the end of a batch that ran
+        // level fault_level (KC_FAULT=rank:level:4)
+        if (!pre && !fail[i] && local_[i]->rank() == fault_rank_ && fault_stage_ == 4 && so[i].levels > 0 &&
+            fault_level_ >= level && fault_level_ < level + so[i].levels) {
+          set_error("kc_group_run: injected fault (KC_FAULT) on rank %d at level %d, narrow batch end", fault_rank_,
+                    fault_level_);
+          note(i, -EIO);
+        }
+        if (!pre && fail[i] && so[i].filled && !gf) gf = &so[i];
         if (!pre && !fail[i]) {
           if (g && (g->levels != so[i].levels || g->reason != so[i].reason)) {
             set_error("kc_group_run: narrow levels disagree between ranks (%d vs %d)", g->levels, so[i].levels);
@@ -797,8 +902,14 @@ int Group::run(kc_result* res) {
           status_err[i] = so[i].status_err;
         }
       }
-      bool any_fail = false;
-      for (size_t i = 0; i < nl; ++i) any_fail |= fail[i] != 0;
+      // A process whose only shard failed at the end of the batch still
+      // follows the batch its peers saw (sn_end filled the outcome before it
+      // failed): if it ran to the end, every rank starts the next batch, whose
+      // first level this rank's control block stops for all of them, and they
+      // reach the counted path's gather (and its failure word) together.
+      // Leaving for the gather alone would hang every peer in its next
+      // narrow exchange.
+      if (!g) g = gf;
       if (g) {
         for (uint64_t w : g->widths) {
           if ((int)widths.size() >= KC_MAX_LEVELS) {
@@ -809,9 +920,9 @@ int Group::run(kc_result* res) {
         }
         level += g->levels;
         sn_levels_ += (uint64_t)g->levels;
-        if (g->reason == SN_RUN && !any_fail) {
+        if (g->reason == SN_RUN) {
           sn_batch = std::min(2 * sn_batch, SN_BATCH);
-          continue;                   // the next batch
+          continue;                   // the next batch (which a failed rank's control block stops)
         }
         if (g->reason == SN_STOP) sn_blocked = true;
       }
@@ -836,7 +947,18 @@ int Group::run(kc_result* res) {
       widths.push_back(total);
       if (sn_blocked && total * 4 <= (uint64_t)SN_MAX && total < prev_total) sn_blocked = false;
       prev_total = total;
-      if (last) break;
+      if (last) {
+        // a deferred frontier's invariants (its states are built here)
+        uint64_t d = NONE;
+        note(0, local_[0]->materialize(&d));
+        if (fail[0]) return group_failed(local_[0]->rank(), fail_word(0), fail, fail_msg);
+        if (d != NONE) {
+          widths.pop_back();
+          err = d;
+          --level;
+        }
+        break;
+      }
       uint64_t n_new = 0, e2 = NONE, c0 = 0;
       e1[0] = NONE;
       inject(0, level, 0);
@@ -844,6 +966,17 @@ int Group::run(kc_result* res) {
       inject(0, level, 2);
       if (!fail[0]) note(0, local_[0]->insert(nullptr, 0, &n_new, &e2));
       if (!fail[0]) note(0, local_[0]->expand_done(&c0, &e1[0]));
+      const uint64_t d = fail[0] ? NONE : local_[0]->defer_error();
+      if (d != NONE) {
+        // an invariant violation among this level's states, found as expand
+        // rebuilt them: the level before's error (its emit would have found
+        // it), so this level's width and the level insert just added go
+        local_[0]->drop_last_insert();
+        widths.pop_back();
+        err = d;
+        --level;
+        break;
+      }
       if (!fail[0]) note(0, local_[0]->advance());
       status_new[0] = fail[0] ? 0 : n_new;
       status_err[0] = fail[0] ? NONE : std::min(e1[0], e2);
@@ -869,6 +1002,7 @@ int Group::run(kc_result* res) {
         if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
         inject(i, level, 0);
         if (!fail[i]) note(i, local_[i]->expand_dev(status_new[i], status_err[i], level == 1, d_rows[i]));
+        ser(i);
         if (fail[i]) {          // the row says so, whatever else it holds
           h_fail_[i % 16] = fail_word(i);
           KC_HIP_TRY(hipMemcpyAsync(d_rows[i] + R + 2, &h_fail_[i % 16], 8, hipMemcpyHostToDevice,
@@ -899,9 +1033,16 @@ int Group::run(kc_result* res) {
             e1[i] = NONE;
           }
         }
+        // a deferred frontier's invariant key (expand rebuilt it; at the
+        // max_levels stop it is built here)
+        uint64_t d = NONE;
+        if (last && !fail[i])
+          note(i, local_[i]->materialize(&d));
+        else if (!fail[i])
+          d = local_[i]->defer_error();
         rows[i] = counts[i];
         rows[i].push_back(status_new[i]);
-        rows[i].push_back(status_err[i]);
+        rows[i].push_back(std::min(status_err[i], d));
         rows[i].push_back(fail_word(i));
       }
       KC_TRY(comm_->all_gather(rows, all));
@@ -954,6 +1095,7 @@ int Group::run(kc_result* res) {
         packed = !fail[i];
       }
       if (!packed && !sunk[i] && ns) note(i, hipMemsetAsync(send_[i], 0, ns * rb, local_[i]->stream()) == hipSuccess ? 0 : -EIO);
+      ser(i);
       inject(i, level, 1);      // (a failure found after a complete pack)
     }
     std::vector<void*> sv(send_.begin(), send_.end()), rv(recv_.begin(), recv_.end());
