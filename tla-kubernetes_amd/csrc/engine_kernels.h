@@ -374,6 +374,11 @@ struct DeferArgs {
   // where k_claim writes its own parents' plans for the next level (any k_claim
   // of the engine's wide path; nullptr: not kept)
   unsigned long long* counts_out = nullptr;
+  // diagnostic (sharded, KC_DEFER_CHECK=1): out already holds the states the
+  // materialising emit built; each rebuilt state is compared with its slot:
+  // check[0] += mismatches, check[1] = min mismatching index, check[2] = min
+  // mismatching index whose link is a received record
+  unsigned long long* check = nullptr;
 };
 
 // Rebuild frontier state i (index within the level) from its link; stores it
@@ -433,6 +438,17 @@ __device__ __forceinline__ typename M::State shard_rebuild(const DeferArgs& df, 
     M::apply(gp, slot, j, f, s);
     act = M::slot_action(gp, slot);
     key = (rank << 60) | (pp << 16) | ((uint64_t)t << 8);
+  }
+  if (df.check) {
+    const typename M::State e = load_state<M>(reinterpret_cast<const typename M::State*>(df.out), i);
+    bool same = true;
+#pragma unroll
+    for (int k = 0; k < M::W; ++k) same &= e.w[k] == s.w[k];
+    if (!same) {
+      atomicAdd(&df.check[0], 1ull);
+      atomicMin(&df.check[1], (unsigned long long)i);
+      if (lk >> 63) atomicMin(&df.check[2], (unsigned long long)i);
+    }
   }
   store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
   if (M::check(s, f.inv_mask) >= 0) atomicMin(&C->defer_err, (key & ~0xffull) | E_INVARIANT);
@@ -687,8 +703,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   typename M::State s;
   uint64_t fold = 0, counts = 0;
   int tot = 0;
+  // a deferred frontier: the engine passes its previous frontier; the
+  // sharded path (OWN) its links (a rank whose previous frontier was empty
+  // has no previous-frontier buffer, only record links)
+  const bool dfr = OWN ? df.link != nullptr : df.prev != nullptr;
   if (live) {
-    if (df.prev)
+    if (dfr)
       s = OWN ? shard_rebuild<M, AS>(df, base + i, f, sh.rank, sh_actd, C)     // (the sharded path, any world)
               : defer_rebuild<M, AS>(df, base + i, f, sh_actd, C);
     else
@@ -697,7 +717,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     if (df.counts_out) df.counts_out[base + i] = pl.counts;
     // (an LDS total, not a register live through the kernel: k_claim sits at
     // its 80-VGPR budget for 6 waves per SIMD)
-    if (df.prev && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
+    if (dfr && pl.total) atomicAdd(&sh_dcand, (unsigned long long)pl.total);
     fold = M::fp_fold(s);
     if (OWN) sh_proj[threadIdx.x] = M::owner_proj(s);
     if (ABL == 0) {
@@ -992,7 +1012,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     const unsigned int v = act_sum<AS>(sh_act, threadIdx.x);
     if (v) atomicAdd(&stripe(C).act_gen[threadIdx.x], (unsigned long long)v);
   }
-  if (df.prev) {
+  if (dfr) {
     if (threadIdx.x < A_COUNT) {
       const unsigned int v = act_sum<AS>(sh_actd, threadIdx.x);
       if (v) atomicAdd(&stripe(C).act_dist[threadIdx.x], (unsigned long long)v);

@@ -63,6 +63,8 @@ class ShardBase {
   virtual uint64_t defer_error() const = 0;
   virtual int materialize(uint64_t* defer_err) = 0;
   virtual void drop_last_insert() = 0;
+  // (the solo path) the last deferred expand's act_gen counts go too
+  virtual int drop_last_expand() = 0;
   virtual int replay(int init_idx, const std::vector<int>& ords, int kind, int pos,
                      std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
                      int* err_inv) = 0;

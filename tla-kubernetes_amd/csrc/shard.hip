@@ -755,6 +755,8 @@ class ShardT final : public ShardBase {
       const int v = atoi(tp);
       settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
     }
+    const char* dc = getenv("KC_DEFER_CHECK");     // diagnostic: rebuilt states against materialised ones
+    defer_check_ = dc && dc[0] == '1';
   }
   ~ShardT() override { release(); }
 
@@ -874,6 +876,7 @@ class ShardT final : public ShardBase {
   int expand_dev(uint64_t status_new, uint64_t status_err, bool level1, uint64_t* d_row) override {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     rebuilt_ = false;
+    gen_snap_ok_ = false;
     hipLaunchKernelGGL(k_head_reset, dim3(1), dim3(64), 0, st_, d_ctr_, d_ovf_cnt_, d_stage_cur_);
     send_total_ = 0;
     dev_init_err_ = init_err_;
@@ -967,6 +970,23 @@ class ShardT final : public ShardBase {
       df.prev_counts = pc_prev_;
       cur_deferred_ = false;
       ++deferred_levels_;
+      if (!d_row) {
+        // the solo path stops on this level's deferred invariant after the
+        // expand has counted its successors, where the exact path stops
+        // before it: keep act_gen to undo them (drop_last_expand)
+        if (!d_gen_snap_) KC_HIP_TRY(hipMalloc(&d_gen_snap_, sizeof(d_ctr_->s[0].act_gen) * CTR_STRIPES));
+        KC_HIP_TRY(hipMemcpy2DAsync(d_gen_snap_, sizeof(d_ctr_->s[0].act_gen), d_ctr_->s[0].act_gen,
+                                    sizeof(CtrStripe), sizeof(d_ctr_->s[0].act_gen), CTR_STRIPES,
+                                    hipMemcpyDeviceToDevice, st_));
+        gen_snap_ok_ = true;
+      }
+      if (defer_check_) {
+        if (!d_dchk_) KC_HIP_TRY(hipMalloc(&d_dchk_, 32));
+        const unsigned long long init[4] = {0ull, ~0ull, ~0ull, 0ull};
+        KC_HIP_TRY(hipMemcpyAsync(d_dchk_, init, 32, hipMemcpyHostToDevice, st_));
+        KC_HIP_TRY(hipStreamSynchronize(st_));
+        df.check = d_dchk_;
+      }
     }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[0], st_));
     if (world_ == 1) {
@@ -1046,6 +1066,13 @@ class ShardT final : public ShardBase {
       return -ENOMEM;
     }
     staged_ = stage_level_ && !(h_exp_->defer_flags & DF_STAGE);
+    if (defer_check_ && rebuilt_) {
+      unsigned long long c[4];
+      KC_HIP_TRY(hipMemcpy(c, d_dchk_, 32, hipMemcpyDeviceToHost));
+      if (c[0])
+        fprintf(stderr, "kc_shard rank %d level %d: %llu of %llu rebuilt states differ (first %lld, first record link %lld)\n",
+                rank_, level_, c[0], (unsigned long long)n_, (long long)c[1], (long long)c[2]);
+    }
     if (stage_level_ && !staged_) ++stage_fallbacks_;
     for (int o = 0; o < world_; ++o) {
       counts[o] = h_owner_base_[o];
@@ -1054,6 +1081,10 @@ class ShardT final : public ShardBase {
     if (n_) rec_ratio_ = std::max(0.01, (double)(send_total_ - counts[rank_]) / (double)n_);
     if (h_exp_->err_key != ~0ull && !init_violated)
       *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_exp_->err_key);
+    if (cfg_.verbose > 1)
+      fprintf(stderr, "kc_shard rank %d level %d: expand n %llu rebuilt %d e1 %llx deferred-invariant %llx\n", rank_,
+              level_, (unsigned long long)n_, (int)rebuilt_, (unsigned long long)*err_key,
+              (unsigned long long)defer_err_);
     return 0;
   }
 
@@ -1232,12 +1263,21 @@ class ShardT final : public ShardBase {
     emitted_links_ = links;
     last_in_ = in;
     const uint64_t bound = cand_ + n;
-    if (!links) KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
+    if (!links || defer_check_) KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const uint64_t next_gidx = level_base_.back() + n_;
     KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + bound + 1, true, st_));
     if (links) KC_TRY(grow_buffer(link_next_, link_next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const unsigned lb = (unsigned)((n_ + 255) / 256), eg = std::max(lb + (n ? rgrid : 0u), 1u);
     const int tail = eg <= SHARD_TAIL_BLOCKS;
+    if (links && defer_check_) {
+      // (diagnostic) the materialising emit too, into next_ — which the next
+      // level's rebuild then compares with — on scratch counters and keys
+      if (!d_ctr_dbg_) KC_HIP_TRY(hipMalloc(&d_ctr_dbg_, sizeof(Counters)));
+      KC_TRY(grow_buffer(pk_dbg_, pk_dbg_cap_, bound + 1, false, st_));
+      hipLaunchKernelGGL(k_shard_emit<M>, dim3(eg), dim3(256), 0, st_, cur_, n_, lb, flags_, (uint64_t)rank_, newmask_,
+                         offsets_, in, n, isnew_, ioff_, next_, pk_dbg_, (uint64_t)0, d_ctr_dbg_,
+                         (unsigned long long*)nullptr, 0, woff_);
+    }
     auto emit = [&]() {
       if (links)
         hipLaunchKernelGGL(k_shard_emit_links<M>, dim3(eg), dim3(256), 0, st_, n_, lb, (uint64_t)rank_, newmask_, in, n,
@@ -1295,6 +1335,9 @@ class ShardT final : public ShardBase {
     distinct_ += next_n_;
     if (h_ctr_->err_key != ~0ull) *err_key = h_ctr_->err_key;
     *n_new = next_n_;
+    if (cfg_.verbose > 1)
+      fprintf(stderr, "kc_shard rank %d level %d: insert records %llu new %llu links %d e2 %llx\n", rank_, level_,
+              (unsigned long long)n, (unsigned long long)next_n_, (int)links, (unsigned long long)*err_key);
     return 0;
   }
 
@@ -1624,6 +1667,15 @@ class ShardT final : public ShardBase {
     distinct_ -= last_new_;
     last_new_ = 0;
   }
+  int drop_last_expand() override {
+    if (!gen_snap_ok_) return 0;
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    KC_HIP_TRY(hipMemcpy2DAsync(d_ctr_->s[0].act_gen, sizeof(CtrStripe), d_gen_snap_, sizeof(d_ctr_->s[0].act_gen),
+                                sizeof(d_ctr_->s[0].act_gen), CTR_STRIPES, hipMemcpyDeviceToDevice, st_));
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    gen_snap_ok_ = false;
+    return 0;
+  }
   int materialize(uint64_t* derr) override {
     *derr = ~0ull;
     KC_HIP_TRY(hipSetDevice(cfg_.device));
@@ -1715,7 +1767,8 @@ class ShardT final : public ShardBase {
                     (void*)rec_lk_, (void*)rfp_, (void*)flag_, (void*)isnew_, (void*)ioff_,
                     (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_, (void*)stage_, (void*)d_stage_cur_,
                     (void*)tcnt_, (void*)toff_, (void*)stoff_, (void*)wtot_, (void*)woff_, (void*)link_cur_,
-                    (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_})
+                    (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_, (void*)d_dchk_, (void*)d_ctr_dbg_,
+                    (void*)pk_dbg_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_exp_) (void)hipHostFree(h_exp_);
@@ -1725,6 +1778,7 @@ class ShardT final : public ShardBase {
     if (h_snc_) (void)hipHostFree(h_snc_);
     if (sp_arena_) (void)hipFree(sp_arena_);
     if (d_spctr_) (void)hipFree(d_spctr_);
+    if (d_gen_snap_) (void)hipFree(d_gen_snap_);
     if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
@@ -1790,8 +1844,15 @@ class ShardT final : public ShardBase {
   const Rec* last_in_ = nullptr;     // the last insert's receive buffer
   uint64_t defer_err_ = ~0ull;       // expand_done: the rebuild's invariant key
   double succ_ratio_ = 5.0;          // successors per state, last counted (the estimates)
+  unsigned long long* d_gen_snap_ = nullptr;   // act_gen before a solo deferred expand (drop_last_expand)
+  bool gen_snap_ok_ = false;
   uint64_t last_new_ = 0;            // the last insert's new states (drop_last_insert)
   uint64_t deferred_levels_ = 0, emit_retries_ = 0;
+  bool defer_check_ = false;         // KC_DEFER_CHECK (diagnostic)
+  unsigned long long* d_dchk_ = nullptr;
+  Counters* d_ctr_dbg_ = nullptr;
+  unsigned long long* pk_dbg_ = nullptr;
+  uint64_t pk_dbg_cap_ = 0;
   uint64_t* d_owner_base_ = nullptr;   // per-owner record totals (device / pinned host)
   uint64_t* h_owner_base_ = nullptr;
   Counters *d_ctr_ = nullptr, *h_ctr_ = nullptr;

@@ -972,6 +972,8 @@ int Group::run(kc_result* res) {
         // rebuilt them: the level before's error (its emit would have found
         // it), so this level's width and the level insert just added go
         local_[0]->drop_last_insert();
+        note(0, local_[0]->drop_last_expand());
+        if (fail[0]) return group_failed(local_[0]->rank(), fail_word(0), fail, fail_msg);
         widths.pop_back();
         err = d;
         --level;
