@@ -223,6 +223,14 @@ typedef struct {
    * unbounded seen-set's. */
   uint64_t seen_hbm_bytes;
   uint64_t seen_host_bytes;
+  /* Sharded loop at world > 1 (kc_group_*, kc_shard_*): 1 = claims ordered
+   * by each parent's position in sequential-BFS order instead of (rank, local
+   * index), so the first discoverer of every state, the error reported and
+   * its trace are TLC -workers 1's (KubeAPI___Model_1.launch:4-7); costs a
+   * per-level all-reduce of per-parent masks and a sort of each rank's new
+   * frontier.  Counted levels only, with the deferred frontier; not with the
+   * seen-set spill.  Ignored at world 1, where the order is TLC's anyway. */
+  int tlc_order;
 } kc_model_config;
 
 typedef struct {

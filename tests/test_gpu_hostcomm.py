@@ -47,6 +47,13 @@ CASES = [
     {"name": "model1_counted", "kw": {}, "env": {"KC_SNARROW": "0"}},
     {"name": "lost_update_counted", "kw": {"variant": 1, "invariants": 7}, "env": {"KC_SNARROW": "0"}},
     {"name": "np2_lost_update", "kw": {"np": 2, "variant": 1, "invariants": 7}},
+    # round 5: TLC-ordered claims (ModelConfig.tlc_order): traces equal the oracle's
+    {"name": "model1_tlc", "kw": {"tlc_order": True}},
+    {"name": "nc2_tlc", "kw": {"nc": 2, "tlc_order": True}},
+    {"name": "variant2_tlc", "kw": {"variant": 2, "tlc_order": True}},
+    {"name": "variant3_tlc", "kw": {"variant": 3, "tlc_order": True}},
+    {"name": "ns0_tlc", "kw": {"ns": 0, "tlc_order": True}},
+    {"name": "lost_update_tlc", "kw": {"variant": 1, "invariants": 7, "tlc_order": True}},
 ]
 
 
@@ -136,6 +143,23 @@ def test_errors_and_traces(results, fixtures, oracle, key, name, kind):
     for a, b in zip(r["trace"], r["trace"][1:]):
         succ, _ = oracle.successors(cfg, a)
         assert any(list(map(int, x)) == b for _, x in succ)
+
+
+def test_tlc_order_traces(results, fixtures):
+    _, res = results
+    fx = fixtures["model1"]
+    r = res["model1_tlc"][0]
+    assert "exception" not in r, r.get("exception")
+    assert r["complete"] and r["level_width"] == fx["level_width"]
+    assert r["act_gen"] == fx["act_gen"] and r["act_dist"] == fx["act_dist"]
+    for key, name, kind in (("nc2", "nc2_tlc", "assertion"), ("variant2", "variant2_tlc", "invariant"),
+                            ("variant3", "variant3_tlc", "assertion"), ("ns0", "ns0_tlc", "deadlock"),
+                            ("variant1_lost_update", "lost_update_tlc", "invariant")):
+        r = res[name][0]
+        assert "exception" not in r, (name, r.get("exception"))
+        assert r["error"] == kind, name
+        assert (r["error_level"], r["trace_len"]) == (fixtures[key]["err_level"], fixtures[key]["trace_len"]), name
+        assert r["trace"] == fixtures[key]["trace"], name
 
 
 def test_deferred_counted_levels(results, fixtures):

@@ -386,6 +386,46 @@ def test_native_np2_lost_update_deferred(fixtures, R):
         assert r["trace"] == fk["trace"]
 
 
+# --- round 5: TLC-ordered claims at R > 1 (ModelConfig.tlc_order)
+TLC_CASES = (("nc2", dict(nc=2), "assertion"), ("variant2", dict(variant=2), "invariant"),
+             ("variant3", dict(variant=3), "assertion"), ("ns0", dict(ns=0), "deadlock"),
+             ("variant4", dict(variant=4), "invariant"),
+             ("variant1_lost_update", dict(variant=1, invariants=7), "invariant"))
+
+
+@pytest.mark.parametrize("R", [2, 3, 9])
+def test_native_tlc_order(fixtures, R):
+    # claims ordered by the parents' sequential-BFS positions: every state's
+    # first discoverer is TLC -workers 1's, so the per-action distinct counts
+    # and every counterexample trace equal the oracle's state for state
+    fx = fixtures["model1"]
+    r = native(R, tlc_order=True)
+    assert r["complete"] and r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["act_gen"] == fx["act_gen"] and r["act_dist"] == fx["act_dist"]
+    for key, kw, kind in TLC_CASES:
+        fk = fixtures[key]
+        r = native(R, tlc_order=True, **kw)
+        assert r["error"] == kind, key
+        assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), key
+        assert r["trace"] == fk["trace"], key
+        if kind == "assertion":
+            assert r["error_action"] == fk["err_action"], key
+
+
+def test_native_tlc_order_np2(fixtures):
+    # NP=2's NoLostUpdate violation at depth 25 (wide levels) and the 40-level
+    # prefix, TLC-ordered at 3 and 4 ranks
+    fk = fixtures["np2_variant1_lost_update"]
+    r = native(3, np=2, variant=1, invariants=7, tlc_order=True)
+    assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate"
+    assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"])
+    assert r["trace"] == fk["trace"]
+    fx = fixtures["np2_40levels"]
+    r = native(4, np=2, max_levels=40, tlc_order=True)
+    assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"]
+
+
 def test_native_np2_prefix_switches(fixtures, monkeypatch):
     # the NP=2 40-level prefix at 4 emulated ranks with each round-5 path
     # switched off in turn (materialising emit, k_shard_pack, per-parent

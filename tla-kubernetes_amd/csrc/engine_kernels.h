@@ -289,6 +289,46 @@ __device__ __forceinline__ int lds_claim(unsigned long long* sh_fp, unsigned int
 // representative is marked in repmask and counted per owner for the record
 // exchange.  Claim keys carry the rank above the parent index.
 constexpr int CLAIM_RANK_SHIFT = 40;
+// Claim keys (the ClaimSet keeps the smallest claim of a level).  Default:
+// rank << 40 | parent index << 8 | position, i.e. (rank, parent, position)
+// order.  TLC order (the sharded loop's tlc_order mode at world > 1): G << 12
+// | position << 4 | rank, G = the parent's position in the level in
+// sequential-BFS order (gpos[parent]), so the smallest claim is the first
+// discovery of TLC -workers 1; a rank maps its own claims back to local
+// parents with the level's rank-select map of its G values (gbits: one bit
+// per G of the level; grank: the set bits before each word).
+struct ClaimKeys {
+  uint32_t rank = 0;
+  const uint32_t* gpos = nullptr;
+  const uint32_t* gbits = nullptr;
+  const uint32_t* grank = nullptr;
+  __host__ __device__ ClaimKeys(uint32_t r = 0) : rank(r) {}
+  __device__ __forceinline__ uint64_t own(uint64_t pidx, uint32_t t) const {
+    if (gpos) return ((uint64_t)gpos[pidx] << 12) | ((uint64_t)t << 4) | rank;
+    return ((uint64_t)rank << CLAIM_RANK_SHIFT) | (pidx << 8) | t;
+  }
+  // a claim key of this rank: its parent's local index and position
+  __device__ __forceinline__ bool mine(uint64_t key, uint64_t& pp, uint32_t& t) const {
+    if (!gpos) {
+      if ((uint32_t)(key >> CLAIM_RANK_SHIFT) != rank) return false;
+      pp = (key >> 8) & 0xffffffffull;
+      t = (uint32_t)(key & 31);
+      return true;
+    }
+    if ((uint32_t)(key & 15) != rank) return false;
+    const uint64_t g = key >> 12;
+    const uint32_t w = gbits[g >> 5], b = 1u << (g & 31);
+    pp = (w & b) ? (uint64_t)grank[g >> 5] + (uint64_t)__builtin_popcount(w & (b - 1u)) : ~0ull;
+    t = (uint32_t)((key >> 4) & 31);
+    return true;
+  }
+};
+// claim key of a record key (rank << 60 | parent << 16 | position << 8 |
+// action; in TLC order the parent field holds G)
+__host__ __device__ __forceinline__ uint64_t record_ckey(uint64_t key, bool tlc) {
+  if (tlc) return (((key >> 16) & 0xffffffffull) << 12) | (((key >> 8) & 0xff) << 4) | (key >> 60);
+  return ((key >> 60) << CLAIM_RANK_SHIFT) | (((key >> 16) & 0xffffffffull) << 8) | ((key >> 8) & 0xff);
+}
 constexpr uint32_t CLAIM_SPREAD = 768;   // k_claim tile-order columns (spread_tile)
 // (k_claim's per-launch arguments beyond the engine's: owner sharding, the
 // tile order, and the candidate overflow list)
@@ -312,6 +352,9 @@ struct ShardArgs {
   uint64_t stage_cap = 0;
   uint32_t* tcnt = nullptr;                   // [world][tiles]: records per owner and tile
   unsigned long long* stoff = nullptr;        // [tiles]: the tile's first staging record (~0: none staged)
+  // TLC order (ClaimKeys): G of each parent of the level; records and claims
+  // then carry G instead of the local parent index
+  const uint32_t* gpos = nullptr;
 };
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
 // workgroups resident together (~1,536: 6 per CU) work on tiles spread over
@@ -379,6 +422,8 @@ struct DeferArgs {
   // check[0] += mismatches, check[1] = min mismatching index, check[2] = min
   // mismatching index whose link is a received record
   unsigned long long* check = nullptr;
+  // TLC order: G of each state of the previous frontier (error keys by G)
+  const uint32_t* prev_gpos = nullptr;
 };
 
 // Rebuild frontier state i (index within the level) from its link; stores it
@@ -417,7 +462,7 @@ __device__ __forceinline__ typename M::State defer_rebuild(const DeferArgs& df, 
 // store it, check the invariants (the key the materialising emit would have
 // made, into C->defer_err: an error of the previous level) and count its
 // action into sh_actd.
-template <class M, int AS = ACT_STRIPES>
+template <class M, int AS = ACT_STRIPES, bool TLC = false>
 __device__ __forceinline__ typename M::State shard_rebuild(const DeferArgs& df, uint64_t i, const Flags& f,
                                                            uint64_t rank, unsigned int* sh_actd,
                                                            Counters* __restrict__ C) {
@@ -437,7 +482,7 @@ __device__ __forceinline__ typename M::State shard_rebuild(const DeferArgs& df, 
     M::locate(pl, t, slot, j);
     M::apply(gp, slot, j, f, s);
     act = M::slot_action(gp, slot);
-    key = (rank << 60) | (pp << 16) | ((uint64_t)t << 8);
+    key = (rank << 60) | ((TLC ? (uint64_t)df.prev_gpos[pp] : pp) << 16) | ((uint64_t)t << 8);
   }
   if (df.check) {
     const typename M::State e = load_state<M>(reinterpret_cast<const typename M::State*>(df.out), i);
@@ -451,7 +496,9 @@ __device__ __forceinline__ typename M::State shard_rebuild(const DeferArgs& df, 
     }
   }
   store_state<M>(reinterpret_cast<typename M::State*>(df.out), i, s);
-  if (M::check(s, f.inv_mask) >= 0) atomicMin(&C->defer_err, (key & ~0xffull) | E_INVARIANT);
+  // (TLC order: errors order by G alone, no rank above it)
+  if (M::check(s, f.inv_mask) >= 0)
+    atomicMin(&C->defer_err, (key & (TLC ? 0x0fffffffffffff00ull : ~0xffull)) | E_INVARIANT);
   // (a record's action byte indexes LDS: anything out of range would be a
   // corrupt record, counted nowhere)
   if ((unsigned)act < (unsigned)A_COUNT) atomicAdd(&sh_actd[act * AS + (threadIdx.x & (AS - 1))], 1u);
@@ -518,7 +565,7 @@ static __global__ void k_parent_chain(const unsigned long long* __restrict__ par
 //      prefix + its rank among the parent's records of that owner.
 // The fingerprint is recomputed for the owner (the claim loop had it in LDS
 // only); no parent is reloaded and nothing is planned again.
-template <class M, int NT>
+template <class M, int NT, bool TLC = false>
 __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, const typename M::State& s,
                                               uint64_t fold, uint64_t counts, uint32_t lp, Flags f,
                                               const unsigned int* sh_rep, const unsigned int* sh_cnt,
@@ -606,7 +653,8 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
     }
     const uint64_t pos = sb + tt[16 + o] + ((pre[(o >> 1) * CLAIM_TILE + lp] >> (16 * (o & 1))) & 0xffffu) + r;
     store_record<M>(out, pos, x,
-                    ((uint64_t)sh.rank << 60) | (pbase << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot));
+                    ((uint64_t)sh.rank << 60) | ((TLC ? (uint64_t)sh.gpos[pbase] : pbase) << 16) |
+                        ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot));
   }
 }
 
@@ -620,7 +668,10 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
 // pinned to match (one wave less measured +15 ms per NP=2 check).
 // OWN: the fingerprints' owner projection (kubeapi_spec.h; 1 on the sharded
 // path, also at world 1 where it runs the SH = false variant)
-template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0>
+// TLC (SH only): claims, records and keys by the parents' G (ClaimKeys; the
+// sharded loop's tlc_order mode), a variant of its own so the default one's
+// registers are untouched
+template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false>
 __global__ void __launch_bounds__(CLAIM_TILE) __attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
@@ -673,6 +724,11 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     for (uint32_t k = threadIdx.x; k < ((sh.world + 3) / 4) * CLAIM_TILE; k += CLAIM_TILE) sh_cnt[k] = 0;
   }
   const uint64_t kbase = SH ? ((uint64_t)sh.rank << CLAIM_RANK_SHIFT) : 0ull;
+  // (TLC order, SH only: claims by G; ClaimKeys)
+  auto okey = [&](uint64_t pidx, uint64_t t) -> uint64_t {
+    if (SH && TLC) return ((uint64_t)sh.gpos[pidx] << 12) | (t << 4) | sh.rank;
+    return kbase | (pidx << 8) | t;
+  };
   sh_cur[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT * AS) sh_act[threadIdx.x] = sh_actd[threadIdx.x] = 0;
   __syncthreads();
@@ -709,7 +765,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   const bool dfr = OWN ? df.link != nullptr : df.prev != nullptr;
   if (live) {
     if (dfr)
-      s = OWN ? shard_rebuild<M, AS>(df, base + i, f, sh.rank, sh_actd, C)     // (the sharded path, any world)
+      s = OWN ? shard_rebuild<M, AS, TLC>(df, base + i, f, sh.rank, sh_actd, C)     // (the sharded path, any world)
               : defer_rebuild<M, AS>(df, base + i, f, sh_actd, C);
     else
       s = load_state<M>(cur, i);
@@ -878,7 +934,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         }
         ++probes;
         const uint64_t pidx = base + tile0 + KC_LP;
-        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | (uint64_t)t), level);
+        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, okey(pidx, (uint64_t)t)), level);
         KC_DIAG_OUT(r);
         if (r == CL_NEW)
           atomicOr(&sh_cur[KC_LP], 1u << t);
@@ -970,7 +1026,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       ++probes;
 #if KC_CLAIM_PIPE
       int r;
-      const uint64_t claim = make_claim(level, kbase | (pidx << 8) | t);
+      const uint64_t claim = make_claim(level, okey(pidx, t));
       if (cq[q] == 0ull) {                        // this lane's CAS inserted fp (fingerprints are never ~0)
         __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         r = CL_NEW;
@@ -980,7 +1036,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         r = claimset_claim_store_from(cs, nbuckets, fp, claim, level, iq[q], e);
       }
 #else
-      const int r = claimset_claim_store_from(cs, nbuckets, fp, make_claim(level, kbase | (pidx << 8) | t), level,
+      const int r = claimset_claim_store_from(cs, nbuckets, fp, make_claim(level, okey(pidx, t)), level,
                                               iq[q], eq[q]);
 #endif
       KC_DIAG_OUT(r);
@@ -994,7 +1050,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   }
   __syncthreads();
   if (SH && sh.stage)
-    stage_records<M, NT>(sh, live, s, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
+    stage_records<M, NT, TLC>(sh, live, s, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
                          sh_rep, sh_cnt, sh_proj, sh_fp, sh_key, tile,
                          base + tile0 + (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x), C);
   if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
@@ -1037,7 +1093,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 // A claim displaced the stored ~prev in settle pass A: clear the displaced
 // claim's newmask bit when it is this rank's (parent index - base, position),
 // and flag the displacer (*flag_at = flag_val).
-__device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_t level, uint32_t rank,
+__device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_t level, const ClaimKeys& rank,
                                                 uint64_t base, uint64_t n, uint32_t* __restrict__ newmask,
                                                 Counters* __restrict__ C, unsigned int* flag_at,
                                                 unsigned int flag_val) {
@@ -1046,13 +1102,15 @@ __device__ __forceinline__ void settle_displace(unsigned long long prev, uint32_
     atomicAdd(&C->overflow, 1ull);               // protocol violation: fail loudly
     return;
   }
-  if ((uint32_t)(pkey >> CLAIM_RANK_SHIFT) == rank) {
-    const uint64_t pp = ((pkey >> 8) & 0xffffffffull) - base;
+  uint64_t pp;
+  uint32_t t;
+  if (rank.mine(pkey, pp, t)) {
+    pp -= base;
     if (pp >= n) {
       atomicAdd(&C->overflow, 1ull);
       return;
     }
-    atomicAnd(&newmask[pp], ~(1u << (pkey & 31)));
+    atomicAnd(&newmask[pp], ~(1u << t));
   }
   *flag_at = flag_val;
 }
@@ -1079,12 +1137,12 @@ template <int PASS>
 __device__ __forceinline__ int settle_record(uint32_t tile, unsigned long long fp, unsigned int* lkp, uint64_t n,
                                              uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
                                              uint32_t level, uint32_t* __restrict__ newmask, Counters* __restrict__ C,
-                                             uint32_t rank) {
+                                             const ClaimKeys& rank) {
   const unsigned int lk = *lkp;
   if (PASS == 1 && !(lk & CAND_DISPLACER)) return 0;
   const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
   const unsigned int lp = (lk >> 5) & (CLAIM_TILE - 1), t = lk & 31;
-  const uint64_t claim = make_claim(level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | ((base + tile0 + lp) << 8) | t);
+  const uint64_t claim = make_claim(level, rank.own(base + tile0 + lp, t));
   if (PASS == 0) {
     const unsigned long long prev = claimset_store_claim(cs, nbuckets, fp, claim);
     if (prev < ~claim)                           // displaced ~prev (or found no claim)
@@ -1103,7 +1161,7 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
                                             uint64_t nbuckets, uint32_t level, const unsigned int* __restrict__ rcount,
                                             const unsigned long long* __restrict__ rec_fp,
                                             unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask,
-                                            Counters* __restrict__ C, uint32_t rank, uint32_t* __restrict__ tile_total) {
+                                            Counters* __restrict__ C, ClaimKeys rank, uint32_t* __restrict__ tile_total) {
   __shared__ unsigned int sh_tot[CLAIM_TILE / 64];
   const unsigned int cnt = rcount[tile];
   const uint64_t tile0 = (uint64_t)tile * CLAIM_TILE;
@@ -1148,7 +1206,7 @@ __device__ __forceinline__ void settle_tiles(uint32_t t0, uint32_t ntiles, uint6
                                              const unsigned int* __restrict__ rcount,
                                              const unsigned long long* __restrict__ rec_fp,
                                              unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask,
-                                             Counters* __restrict__ C, uint32_t rank,
+                                             Counters* __restrict__ C, ClaimKeys rank,
                                              uint32_t* __restrict__ tile_total) {
   __shared__ unsigned int sh_cnt[TP + 1];
   __shared__ unsigned int sh_tot[CLAIM_TILE / 64][TP];
@@ -1217,7 +1275,7 @@ template <int PASS>
 __device__ __forceinline__ void settle_ovf_blocks(uint32_t blk, uint32_t nblk, const CandOvf& ovf, uint64_t n,
                                                   uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
                                                   uint32_t level, uint32_t* __restrict__ newmask,
-                                                  Counters* __restrict__ C, uint32_t rank,
+                                                  Counters* __restrict__ C, ClaimKeys rank,
                                                   uint32_t* __restrict__ tile_total) {
   const unsigned long long c = *ovf.count;
   const uint64_t cnt = c < ovf.cap ? c : ovf.cap;
@@ -1236,7 +1294,7 @@ __device__ __forceinline__ void settle_ovf_blocks(uint32_t blk, uint32_t nblk, c
 template <int PASS>
 static __global__ void __launch_bounds__(256)
 k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, ClaimKeys rank,
              uint32_t* __restrict__ tile_total) {
   settle_ovf_blocks<PASS>(blockIdx.x, gridDim.x, ovf, n, base, cs, nbuckets, level, newmask, C, rank, tile_total);
 }
@@ -1252,7 +1310,7 @@ static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
              uint32_t level, const unsigned int* __restrict__ rcount,
              const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
-             uint32_t* __restrict__ newmask, Counters* __restrict__ C, uint32_t rank,
+             uint32_t* __restrict__ newmask, Counters* __restrict__ C, ClaimKeys rank,
              uint32_t* __restrict__ tile_total = nullptr, uint32_t tiles = 0, CandOvf ovf = CandOvf{}) {
   // PASS 0 launched with tiles + SETTLE_OVF_BLOCKS blocks: the blocks past
   // the tiles settle the overflow list
@@ -1276,7 +1334,7 @@ static __global__ void __launch_bounds__(CLAIM_TILE)
 k_settle_mt(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
             const unsigned int* __restrict__ rcount, const unsigned long long* __restrict__ rec_fp,
             unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask, Counters* __restrict__ C,
-            uint32_t rank, uint32_t* __restrict__ tile_total, uint32_t tiles, CandOvf ovf) {
+            ClaimKeys rank, uint32_t* __restrict__ tile_total, uint32_t tiles, CandOvf ovf) {
   const uint32_t tb = (tiles + TP - 1) / TP;
   if (PASS == 0 && blockIdx.x >= tb) {
     settle_ovf_blocks<0>(blockIdx.x - tb, gridDim.x - tb, ovf, n, base, cs, nbuckets, level, newmask, C, rank,

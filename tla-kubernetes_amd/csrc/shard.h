@@ -69,6 +69,23 @@ class ShardBase {
                      std::vector<std::vector<uint64_t>>& tuples, int* err_action, int* err_self,
                      int* err_inv) = 0;
 
+  // ---- TLC order (cfg.tlc_order at world > 1; counted levels with the
+  // deferred frontier): every state carries G, its position in its level in
+  // sequential-BFS order, and claims, records, parent keys and error keys
+  // carry the parent's G instead of (rank, local index), so the first
+  // discoverer of every state, the error reported and its trace are those of
+  // TLC -workers 1.  After every rank's insert of a level of global width W:
+  // tlc_masks() sets, per parent G, the positions of its successors this
+  // rank won (*mask: W words on the device); the caller sums the masks over
+  // the ranks in place; tlc_order() then gives each new state its G (the
+  // winners before it in (parent G, position) order) and sorts this rank's
+  // new frontier by G.  tlc_locate() finds the local index of G at a level
+  // (the trace walk).
+  virtual bool tlc() const = 0;
+  virtual int tlc_masks(uint64_t W, uint32_t** mask) = 0;
+  virtual int tlc_order(uint64_t W) = 0;
+  virtual int tlc_locate(int level, uint64_t G, uint64_t* idx, bool* found) = 0;
+
   // ---- device-driven narrow levels (shard_narrow.h), driven by the native
   // loop: sn_setup once (the control block, scratch and the fixed exchange
   // slots: world x (slot_cap + 1) records each way), then per batch

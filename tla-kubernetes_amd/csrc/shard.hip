@@ -54,17 +54,13 @@ __device__ __forceinline__ uint64_t record_key(const Record<M>* __restrict__ in,
   return in[i].w[0];
 }
 
-// claim order key of a record key: (rank, parent index, successor position)
-__device__ __forceinline__ uint64_t record_ckey(uint64_t key) {
-  return ((key >> 60) << CLAIM_RANK_SHIFT) | (((key >> 16) & 0xffffffffull) << 8) | ((key >> 8) & 0xff);
-}
 
 template <class M>
 __global__ void __launch_bounds__(256)
 k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uint32_t world,
              uint64_t rank, const uint32_t* __restrict__ off /* [world][n], one exclusive scan */,
              const uint32_t* __restrict__ repmask,
-             Record<M>* __restrict__ out) {
+             Record<M>* __restrict__ out, const uint32_t* __restrict__ gpos /* TLC order: G per parent */) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t mask = repmask[i];
@@ -88,7 +84,8 @@ k_shard_pack(const typename M::State* __restrict__ cur, uint64_t n, Flags f, uin
       if (k == o) { r = c[k]; c[k] = r + 1; }
     const uint64_t pos = (uint64_t)off[(uint64_t)o * n + i] + r;   // owner-major scan
     uint64_t w[Record<M>::RW];
-    record_pack<M>(x, (rank << 60) | (i << 16) | ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot), w);
+    record_pack<M>(x, (rank << 60) | ((gpos ? (uint64_t)gpos[i] : i) << 16) | ((uint64_t)t << 8) |
+                          (uint64_t)M::slot_action(s, slot), w);
     ulonglong2* v = reinterpret_cast<ulonglong2*>(out + pos);
 #pragma unroll
     for (int k = 0; k < Record<M>::RW / 2; ++k) v[k] = make_ulonglong2(w[2 * k], w[2 * k + 1]);
@@ -253,7 +250,7 @@ template <class M>
 __global__ void __launch_bounds__(256)
 k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs,
             uint64_t nslots, uint32_t level, unsigned long long* __restrict__ rfp,
-            unsigned int* __restrict__ flag, Counters* __restrict__ C) {
+            unsigned int* __restrict__ flag, Counters* __restrict__ C, int tlc) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long probes = 0;
   if (i < n) {
@@ -262,7 +259,7 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
     load_record<M>(in, i, x, key);
     const uint64_t fp = M::template fingerprint<1>(x);
     rfp[i] = fp;
-    const int r = claimset_claim_store(cs, nslots, fp, make_claim(level, record_ckey(key)), level);
+    const int r = claimset_claim_store(cs, nslots, fp, make_claim(level, record_ckey(key, tlc)), level);
     if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
     flag[i] = r == CL_NEW ? RF_INSERTER : (r == CL_CUR ? RF_CAND : RF_OUT);
     probes = 1;
@@ -279,7 +276,7 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
 template <class M, int PASS>
 __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __restrict__ in, uint64_t n,
                                            ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
-                                           uint32_t rank, const unsigned long long* __restrict__ rfp,
+                                           const ClaimKeys& rank, const unsigned long long* __restrict__ rfp,
                                            unsigned int* __restrict__ flag, uint32_t* __restrict__ newmask,
                                            uint64_t nlocal, uint32_t* __restrict__ isnew, Counters* __restrict__ C,
                                            uint32_t* __restrict__ rtot) {
@@ -288,7 +285,7 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
     if (i >= n) return;
     const unsigned int fl = flag[i];
     if (fl != RF_CAND) return;
-    const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
+    const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i), rank.gpos != nullptr));
     const unsigned long long prev = claimset_store_claim(cs, nslots, rfp[i], claim);
     if (prev < ~claim) settle_displace(prev, level, rank, 0, nlocal, newmask, C, &flag[i], RF_DISPLACER);
   } else {
@@ -296,7 +293,7 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
     if (i < n) {
       const unsigned int fl = flag[i];
       if (fl >= RF_INSERTER) {
-        const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i)));
+        const uint64_t claim = make_claim(level, record_ckey(record_key<M>(in, i), rank.gpos != nullptr));
         w = ~claimset_get(cs, nslots, rfp[i]) == claim ? 1u : 0u;
       }
       isnew[i] = w;
@@ -325,7 +322,7 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
 template <class M, int PASS, int TP = 1>
 __global__ void __launch_bounds__(256)
 k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots,
-              uint32_t level, uint32_t rank, const unsigned int* __restrict__ rcount,
+              uint32_t level, ClaimKeys rank, const unsigned int* __restrict__ rcount,
               const unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
               uint32_t* __restrict__ newmask, const Record<M>* __restrict__ in, uint64_t n,
               const unsigned long long* __restrict__ rfp, unsigned int* __restrict__ flag,
@@ -574,7 +571,8 @@ constexpr unsigned SHARD_TAIL_BLOCKS = 64;    // emit grids up to this size run 
 // launch again (it writes nothing else).
 template <class M>
 __global__ void __launch_bounds__(256)
-k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint32_t* __restrict__ newmask,
+k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint32_t* __restrict__ gpos,
+                   const uint32_t* __restrict__ newmask,
                    const Record<M>* __restrict__ in, uint64_t n, const uint32_t* __restrict__ isnew,
                    const uint32_t* __restrict__ woff, unsigned long long* __restrict__ link,
                    unsigned long long* __restrict__ pkeys, uint64_t next_gidx, uint64_t cap,
@@ -620,7 +618,7 @@ k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint
         continue;
       }
       link[o] = (pidx << 8) | t;
-      pkeys[next_gidx + o] = (rank << 60) | (pidx << 16) | (t << 8);
+      pkeys[next_gidx + o] = (rank << 60) | ((gpos ? (uint64_t)gpos[pidx] : pidx) << 16) | (t << 8);
     }
   } else {
     const uint64_t blk = blockIdx.x - lblocks;
@@ -650,7 +648,7 @@ k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint
 
 // A deferred frontier materialised outside k_claim (before a narrow batch,
 // at a max_levels stop): the same rebuild, plus the level's successor count.
-template <class M>
+template <class M, bool TLC>
 __global__ void __launch_bounds__(256) k_shard_materialize(DeferArgs df, uint64_t n, Flags f, uint64_t rank,
                                                            Counters* __restrict__ C) {
   __shared__ unsigned int sh_actd[A_COUNT];
@@ -659,7 +657,7 @@ __global__ void __launch_bounds__(256) k_shard_materialize(DeferArgs df, uint64_
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long cand = 0;
   if (i < n) {
-    const typename M::State s = shard_rebuild<M, 1>(df, i, f, rank, sh_actd, C);
+    const typename M::State s = shard_rebuild<M, 1, TLC>(df, i, f, rank, sh_actd, C);
     cand = (unsigned long long)M::plan(s, f).total;
   }
 #pragma unroll
@@ -731,6 +729,60 @@ __global__ void k_shard_spill_apply(const uint64_t* __restrict__ qkey, const uin
   if (!claimset_retire(cs, nslots, cold_unkey(qkey[i]))) atomicAdd(&C->overflow, 1ull);
 }
 
+// ---- TLC order (ShardBase::tlc_*; cfg.tlc_order, world > 1).  Per level of
+// global width W, after every rank's insert: k_tlc_mask sets, for each new
+// state this rank won, its position bit in its parent's word (parent keys
+// carry the parent's G); the words are summed over the ranks (bits of one
+// parent are disjoint: every successor has one owner); then G of a new state
+// = the winners of the parents before its parent (one scan over the W
+// popcounts) + its parent's winners before it (k_tlc_pos), and its local
+// index = the rank's G values before it (a bitmap over the next level's G
+// and one scan of its word popcounts: k_tlc_perm).  The bitmap and its scan
+// stay as the next level's G -> local index map (ClaimKeys::mine).
+__global__ void __launch_bounds__(256) k_tlc_mask(const unsigned long long* __restrict__ pk, uint64_t nn,
+                                                  uint32_t* __restrict__ wmask, uint64_t W,
+                                                  Counters* __restrict__ C) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  const uint64_t key = pk[i];
+  const uint64_t g = (key >> 16) & 0xffffffffull;
+  const uint32_t t = (uint32_t)((key >> 8) & 0xff);
+  if (g >= W || t >= 32) {
+    atomicAdd(&C->overflow, 1ull);                // a parent key outside the level: fail loudly
+    return;
+  }
+  atomicOr(&wmask[g], 1u << t);
+}
+__global__ void __launch_bounds__(256) k_tlc_pos(const unsigned long long* __restrict__ pk, uint64_t nn,
+                                                 const uint32_t* __restrict__ wmask,
+                                                 const uint32_t* __restrict__ wbase, uint32_t* __restrict__ gnew,
+                                                 uint32_t* __restrict__ bits) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  const uint64_t key = pk[i];
+  const uint64_t g = (key >> 16) & 0xffffffffull;
+  const uint32_t t = (uint32_t)((key >> 8) & 31);
+  const uint32_t gn = wbase[g] + (uint32_t)__builtin_popcount(wmask[g] & ((1u << t) - 1u));
+  gnew[i] = gn;
+  atomicOr(&bits[gn >> 5], 1u << (gn & 31));
+}
+__global__ void __launch_bounds__(256) k_tlc_perm(uint64_t nn, const uint32_t* __restrict__ gnew,
+                                                  const uint32_t* __restrict__ bits,
+                                                  const uint32_t* __restrict__ brank,
+                                                  const unsigned long long* __restrict__ link_in,
+                                                  const unsigned long long* __restrict__ pk_in,
+                                                  unsigned long long* __restrict__ link_out,
+                                                  unsigned long long* __restrict__ pk_out,
+                                                  uint32_t* __restrict__ gpos_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  const uint32_t gn = gnew[i];
+  const uint64_t j = (uint64_t)brank[gn >> 5] + (uint64_t)__builtin_popcount(bits[gn >> 5] & ((1u << (gn & 31)) - 1u));
+  link_out[j] = link_in[i];
+  pk_out[j] = pk_in[i];
+  gpos_out[j] = gn;
+}
+
 template <class M>
 class ShardT final : public ShardBase {
   using State = typename M::State;
@@ -757,6 +809,7 @@ class ShardT final : public ShardBase {
     }
     const char* dc = getenv("KC_DEFER_CHECK");     // diagnostic: rebuilt states against materialised ones
     defer_check_ = dc && dc[0] == '1';
+    tlc_ = cfg.tlc_order && world > 1;
   }
   ~ShardT() override { release(); }
 
@@ -772,6 +825,10 @@ class ShardT final : public ShardBase {
     }
     if (cfg_.device < 0 || cfg_.device >= ndev) {
       set_error("kc_shard: bad device %d", cfg_.device);
+      return -EINVAL;
+    }
+    if (tlc_ && (spill_ || !tcount_)) {
+      set_error("kc_shard: tlc_order needs the deferred frontier (no seen-set spill, KC_SHARD_TSCAN on)");
       return -EINVAL;
     }
     KC_HIP_TRY(hipSetDevice(cfg_.device));
@@ -850,6 +907,25 @@ class ShardT final : public ShardBase {
     cand_total_ = 0;
     KC_TRY(grow_buffer(cur_, cur_cap_, std::max<uint64_t>(n_, 1), false, st_));
     KC_TRY(grow_buffer(pkeys_, pk_cap_, std::max<uint64_t>(n_, 1), false, st_));
+    if (tlc_) {
+      // level 1 in TLC order: Init states are distinct, each at its index
+      // (G = k); this rank's in increasing k
+      const uint64_t W = (uint64_t)M::num_init(), words = W / 32 + 1;
+      std::vector<uint32_t> g, bits(words, 0), brank(words, 0);
+      for (auto k : keys) {
+        const uint32_t gk = (uint32_t)(k & 0xffffffffull);
+        g.push_back(gk);
+        bits[gk >> 5] |= 1u << (gk & 31);
+      }
+      for (uint64_t w = 1; w < words; ++w) brank[w] = brank[w - 1] + (uint32_t)__builtin_popcount(bits[w - 1]);
+      KC_TRY(grow_buffer(gpos_all_, gp_cap_, pk_cap_, false, st_));
+      KC_TRY(grow_buffer(gbits_cur_, gbits_cur_cap_, words, false, st_));
+      KC_TRY(grow_buffer(grank_cur_, grank_cur_cap_, words, false, st_));
+      if (n_) KC_HIP_TRY(hipMemcpyAsync(gpos_all_, g.data(), n_ * 4, hipMemcpyHostToDevice, st_));
+      KC_HIP_TRY(hipMemcpyAsync(gbits_cur_, bits.data(), words * 4, hipMemcpyHostToDevice, st_));
+      KC_HIP_TRY(hipMemcpyAsync(grank_cur_, brank.data(), words * 4, hipMemcpyHostToDevice, st_));
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+    }
     if (n_) {
       KC_HIP_TRY(hipMemcpyAsync(cur_, mine.data(), n_ * sizeof(State), hipMemcpyHostToDevice, st_));
       KC_HIP_TRY(hipMemcpyAsync(pkeys_, keys.data(), n_ * 8, hipMemcpyHostToDevice, st_));
@@ -933,6 +1009,7 @@ class ShardT final : public ShardBase {
     sh.repmask = repmask_;
     sh.cnt = cnt_;
     sh.ovf = ovf_;
+    if (tlc_) sh.gpos = gpos_cur();
     // record staging (world > 1): an estimate from the last level's records
     // per parent, at most the level's successors; a level past it packs the
     // old way (DF_STAGE, pack())
@@ -968,6 +1045,7 @@ class ShardT final : public ShardBase {
       df.prev_rec = prev_rec_;
       df.out = cur_;
       df.prev_counts = pc_prev_;
+      if (tlc_) df.prev_gpos = gpos_prev();
       cur_deferred_ = false;
       ++deferred_levels_;
       if (!d_row) {
@@ -997,10 +1075,16 @@ class ShardT final : public ShardBase {
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                          d_ctr_, sh, df);
     } else {
-      hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
-                         cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
-                         (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
-                         d_ctr_, sh, df);
+      if (tlc_)
+        hipLaunchKernelGGL((k_claim<M, 0, true, 1, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
+                           cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                           (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                           d_ctr_, sh, df);
+      else
+        hipLaunchKernelGGL((k_claim<M, 0, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
+                           cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                           (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                           d_ctr_, sh, df);
     }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[1], st_));
     if (stage_level_) {
@@ -1079,8 +1163,17 @@ class ShardT final : public ShardBase {
       send_total_ += counts[o];
     }
     if (n_) rec_ratio_ = std::max(0.01, (double)(send_total_ - counts[rank_]) / (double)n_);
-    if (h_exp_->err_key != ~0ull && !init_violated)
-      *err_key = std::min<uint64_t>(*err_key, ((uint64_t)rank_ << 60) | (uint64_t)h_exp_->err_key);
+    if (h_exp_->err_key != ~0ull && !init_violated) {
+      uint64_t e = ((uint64_t)rank_ << 60) | (uint64_t)h_exp_->err_key;
+      if (tlc_) {
+        // TLC order: the parent's G, no rank (the trace walk locates it)
+        const uint64_t pidx = (h_exp_->err_key >> 16) & ((1ull << 44) - 1);
+        uint32_t g = 0;
+        KC_HIP_TRY(hipMemcpy(&g, gpos_cur() + pidx, 4, hipMemcpyDeviceToHost));
+        e = ((uint64_t)g << 16) | (h_exp_->err_key & 0xffffull);
+      }
+      *err_key = std::min<uint64_t>(*err_key, e);
+    }
     if (cfg_.verbose > 1)
       fprintf(stderr, "kc_shard rank %d level %d: expand n %llu rebuilt %d e1 %llx deferred-invariant %llx\n", rank_,
               level_, (unsigned long long)n_, (int)rebuilt_, (unsigned long long)*err_key,
@@ -1169,7 +1262,7 @@ class ShardT final : public ShardBase {
       }
       hipLaunchKernelGGL(k_shard_pack<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_,
                          cur_, n_, flags_, (uint32_t)world_, (uint64_t)rank_, off_, repmask_,
-                         (Rec*)send);
+                         (Rec*)send, tlc_ ? gpos_cur() : (const uint32_t*)nullptr);
       KC_HIP_TRY(hipGetLastError());
     }
     // else stream-ordered with the caller (set_stream, or the native level
@@ -1207,7 +1300,7 @@ class ShardT final : public ShardBase {
       KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
       KC_TRY(grow_buffer(ioff_, ioff_cap_, n, false, st_));
       hipLaunchKernelGGL(k_rec_claim<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots,
-                         succ_level, rfp_, flag_, d_ctr_);
+                         succ_level, rfp_, flag_, d_ctr_, (int)tlc_);
     }
     // settle pass A (own tiles, records and the tiles' overflow list in one
     // launch), then pass B; n_ = 0 with n > 0 still runs pass A's first
@@ -1221,11 +1314,21 @@ class ShardT final : public ShardBase {
     const bool tc = tcount_ && !spill_;
     // (KC_SETTLE_TP own tiles per settle workgroup on the tile-count path)
     const int tp = tc ? settle_tp_ : 1;
+    ClaimKeys ck((uint32_t)rank_);
+    if (tlc_) {
+      if (!(defer_on_ && tc)) {
+        set_error("kc_shard_insert: tlc_order needs the deferred frontier");
+        return -EINVAL;
+      }
+      ck.gpos = gpos_cur();
+      ck.gbits = gbits_cur_;
+      ck.grank = grank_cur_;
+    }
     auto settle = [&](int pass, unsigned ob_blocks, uint32_t* wt) {
       const unsigned tb = (lt + tp - 1) / tp, g = std::max(tb + rb + ob_blocks, 1u);
 #define KC_SB(P, T)                                                                                         \
   hipLaunchKernelGGL((k_settle_both<M, P, T>), dim3(g), dim3(256), 0, st_, lt, rb, n_, cs_.t, cs_.nslots,   \
-                     succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, \
+                     succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, \
                      isnew_, d_ctr_, ovf_, wt)
       if (pass == 0) {
         if (tp == 2) KC_SB(0, 2); else if (tp == 4) KC_SB(0, 4); else if (tp == 8) KC_SB(0, 8); else KC_SB(0, 1);
@@ -1241,11 +1344,11 @@ class ShardT final : public ShardBase {
       if (lt + rb) settle(1, 0, wtot_);
       if (n_)
         hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SHARD_OVF_BLOCKS), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
-                           cs_.nslots, succ_level, newmask_, d_ctr_, (uint32_t)rank_, wtot_);
+                           cs_.nslots, succ_level, newmask_, d_ctr_, ck, wtot_);
       hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
     } else {
       hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, rb, n_, cs_.t,
-                         cs_.nslots, succ_level, (uint32_t)rank_, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
+                         cs_.nslots, succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
                          flag_, isnew_, d_ctr_, ovf_, (uint32_t*)nullptr);
       // positions: this rank's own winners first, then the records'
       KC_TRY(scan_winners(n));
@@ -1266,6 +1369,7 @@ class ShardT final : public ShardBase {
     if (!links || defer_check_) KC_TRY(grow_buffer(next_, next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const uint64_t next_gidx = level_base_.back() + n_;
     KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + bound + 1, true, st_));
+    if (tlc_) KC_TRY(grow_buffer(gpos_all_, gp_cap_, pk_cap_, true, st_));
     if (links) KC_TRY(grow_buffer(link_next_, link_next_cap_, std::max<uint64_t>(bound, 1), false, st_));
     const unsigned lb = (unsigned)((n_ + 255) / 256), eg = std::max(lb + (n ? rgrid : 0u), 1u);
     const int tail = eg <= SHARD_TAIL_BLOCKS;
@@ -1280,7 +1384,8 @@ class ShardT final : public ShardBase {
     }
     auto emit = [&]() {
       if (links)
-        hipLaunchKernelGGL(k_shard_emit_links<M>, dim3(eg), dim3(256), 0, st_, n_, lb, (uint64_t)rank_, newmask_, in, n,
+        hipLaunchKernelGGL(k_shard_emit_links<M>, dim3(eg), dim3(256), 0, st_, n_, lb, (uint64_t)rank_,
+                           tlc_ ? gpos_cur() : (const uint32_t*)nullptr, newmask_, in, n,
                            isnew_, woff_, link_next_, pkeys_, next_gidx,
                            std::min<uint64_t>(link_next_cap_, pk_cap_ - next_gidx), d_ctr_,
                            reinterpret_cast<unsigned long long*>(h_ctr_), tail);
@@ -1300,6 +1405,7 @@ class ShardT final : public ShardBase {
       const uint64_t need = h_ctr_->level_new;
       KC_TRY(grow_buffer(link_next_, link_next_cap_, need, false, st_));
       KC_TRY(grow_buffer(pkeys_, pk_cap_, next_gidx + need + 1, true, st_));
+      if (tlc_) KC_TRY(grow_buffer(gpos_all_, gp_cap_, pk_cap_, true, st_));
       KC_HIP_TRY(hipMemsetAsync(&d_ctr_->defer_flags, 0, 8, st_));
       ++emit_retries_;
       emit();
@@ -1652,6 +1758,12 @@ class ShardT final : public ShardBase {
       cur_deferred_ = next_n_ > 0;
       emitted_links_ = false;
     }
+    if (tlc_) {
+      std::swap(gbits_cur_, gbits_next_);
+      std::swap(gbits_cur_cap_, gbits_next_cap_);
+      std::swap(grank_cur_, grank_next_);
+      std::swap(grank_cur_cap_, grank_next_cap_);
+    }
     n_ = next_n_;
     cand_ = next_cand_;
     cand_est_ = next_cand_est_;
@@ -1690,9 +1802,14 @@ class ShardT final : public ShardBase {
     df.prev_rec = prev_rec_;
     df.out = cur_;
     df.prev_counts = pc_prev_;
+    if (tlc_) df.prev_gpos = gpos_prev();
     KC_HIP_TRY(hipMemsetAsync(&d_ctr_->defer_err, 0xff, 8, st_));
-    hipLaunchKernelGGL(k_shard_materialize<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_, df, n_, flags_,
-                       (uint64_t)rank_, d_ctr_);
+    if (tlc_)
+      hipLaunchKernelGGL((k_shard_materialize<M, true>), dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_, df, n_,
+                         flags_, (uint64_t)rank_, d_ctr_);
+    else
+      hipLaunchKernelGGL((k_shard_materialize<M, false>), dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_, df,
+                         n_, flags_, (uint64_t)rank_, d_ctr_);
     KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipMemcpyAsync(h_ctr_, d_ctr_, sizeof(Counters), hipMemcpyDeviceToHost, st_));
     KC_HIP_TRY(hipStreamSynchronize(st_));
@@ -1704,6 +1821,98 @@ class ShardT final : public ShardBase {
     cand_est_ = false;
     if (n_) succ_ratio_ = std::max(1.0, (double)cand_ / (double)n_);
     *derr = h_ctr_->defer_err;
+    return 0;
+  }
+
+  bool tlc() const override { return tlc_; }
+  const uint32_t* gpos_cur() const { return gpos_all_ + level_base_.back(); }
+  const uint32_t* gpos_prev() const {
+    return gpos_all_ + (level_base_.size() >= 2 ? level_base_[level_base_.size() - 2] : 0);
+  }
+  int tlc_masks(uint64_t W, uint32_t** mask) override {
+    *mask = nullptr;
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    if (!tlc_ || W >= (1ull << 31)) {
+      set_error("kc_shard tlc_masks: %s", tlc_ ? "a level of 2^31 states or more" : "not in TLC order");
+      return -EINVAL;
+    }
+    KC_TRY(grow_buffer(wmask_, wmask_cap_, W, false, st_));
+    KC_HIP_TRY(hipMemsetAsync(wmask_, 0, W * 4, st_));
+    const uint64_t next_gidx = level_base_.back() + n_;
+    if (next_n_)
+      hipLaunchKernelGGL(k_tlc_mask, dim3((unsigned)((next_n_ + 255) / 256)), dim3(256), 0, st_, pkeys_ + next_gidx,
+                         next_n_, wmask_, W, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
+    *mask = wmask_;
+    return 0;
+  }
+  int tlc_order(uint64_t W) override {
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    // (the next level has at most 32 W states: W + 1 bitmap words)
+    const uint64_t words = W + 1;
+    KC_TRY(grow_buffer(gbits_next_, gbits_next_cap_, words, false, st_));
+    KC_TRY(grow_buffer(grank_next_, grank_next_cap_, words, false, st_));
+    KC_TRY(grow_buffer(wbase_, wbase_cap_, W, false, st_));
+    KC_HIP_TRY(hipMemsetAsync(gbits_next_, 0, words * 4, st_));
+    size_t tmp_bytes = 0;
+    const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> wc(wmask_, NewCount());
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, wc, wbase_, (int)W, st_));
+    KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, wc, wbase_, (int)W, st_));
+    const uint64_t nn = next_n_, next_gidx = level_base_.back() + n_;
+    const unsigned g = (unsigned)((nn + 255) / 256);
+    if (nn) {
+      KC_TRY(grow_buffer(gnew_, gnew_cap_, nn, false, st_));
+      hipLaunchKernelGGL(k_tlc_pos, dim3(g), dim3(256), 0, st_, pkeys_ + next_gidx, nn, wmask_, wbase_, gnew_,
+                         gbits_next_);
+    }
+    const hipcub::TransformInputIterator<uint32_t, NewCount, const uint32_t*> bc(gbits_next_, NewCount());
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, bc, grank_next_, (int)words, st_));
+    KC_TRY(grow_buffer(scan_tmp_, scan_cap_, tmp_bytes + 16, false, st_));
+    KC_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, tmp_bytes, bc, grank_next_, (int)words, st_));
+    if (nn) {
+      KC_TRY(grow_buffer(link_tmp_, link_tmp_cap_, std::max(nn, link_next_cap_), false, st_));
+      KC_TRY(grow_buffer(pk_tmp_, pk_tmp_cap_, nn, false, st_));
+      hipLaunchKernelGGL(k_tlc_perm, dim3(g), dim3(256), 0, st_, nn, gnew_, gbits_next_, grank_next_, link_next_,
+                         pkeys_ + next_gidx, link_tmp_, pk_tmp_, gpos_all_ + next_gidx);
+      KC_HIP_TRY(hipMemcpyAsync(pkeys_ + next_gidx, pk_tmp_, nn * 8, hipMemcpyDeviceToDevice, st_));
+      std::swap(link_next_, link_tmp_);
+      std::swap(link_next_cap_, link_tmp_cap_);
+    }
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipStreamSynchronize(st_));
+    KC_HIP_TRY(hipMemcpy(h_ctr_, d_ctr_, kCtrHead, hipMemcpyDeviceToHost));
+    if (h_ctr_->overflow) {
+      set_error("kc_shard tlc_order: a parent key outside its level");
+      return -EIO;
+    }
+    return 0;
+  }
+  int tlc_locate(int level, uint64_t G, uint64_t* idx, bool* found) override {
+    *found = false;
+    if (!tlc_ || level < 1 || level > (int)level_base_.size()) {
+      set_error("kc_shard tlc_locate: bad level %d", level);
+      return -EINVAL;
+    }
+    KC_HIP_TRY(hipSetDevice(cfg_.device));
+    const uint64_t b = level_base_[level - 1];
+    const uint64_t cnt = level < (int)level_base_.size() ? level_base_[level] - b : n_;
+    // (a level's G values are sorted: tlc_order)
+    uint64_t lo = 0, hi = cnt;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      uint32_t v = 0;
+      KC_HIP_TRY(hipMemcpy(&v, gpos_all_ + b + mid, 4, hipMemcpyDeviceToHost));
+      if ((uint64_t)v < G) lo = mid + 1; else hi = mid;
+    }
+    if (lo < cnt) {
+      uint32_t v = 0;
+      KC_HIP_TRY(hipMemcpy(&v, gpos_all_ + b + lo, 4, hipMemcpyDeviceToHost));
+      if ((uint64_t)v == G) {
+        *idx = lo;
+        *found = true;
+      }
+    }
     return 0;
   }
 
@@ -1768,7 +1977,9 @@ class ShardT final : public ShardBase {
                     (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_, (void*)stage_, (void*)d_stage_cur_,
                     (void*)tcnt_, (void*)toff_, (void*)stoff_, (void*)wtot_, (void*)woff_, (void*)link_cur_,
                     (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_, (void*)d_dchk_, (void*)d_ctr_dbg_,
-                    (void*)pk_dbg_})
+                    (void*)pk_dbg_, (void*)gpos_all_, (void*)gbits_cur_, (void*)grank_cur_, (void*)gbits_next_,
+                    (void*)grank_next_, (void*)wmask_, (void*)wbase_, (void*)gnew_, (void*)link_tmp_,
+                    (void*)pk_tmp_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_exp_) (void)hipHostFree(h_exp_);
@@ -1849,6 +2060,17 @@ class ShardT final : public ShardBase {
   uint64_t last_new_ = 0;            // the last insert's new states (drop_last_insert)
   uint64_t deferred_levels_ = 0, emit_retries_ = 0;
   bool defer_check_ = false;         // KC_DEFER_CHECK (diagnostic)
+  // TLC order (tlc_*): G of every state (parallel to pkeys_), the current /
+  // next level's G -> local index map, the per-parent masks and scratch
+  bool tlc_ = false;
+  uint32_t* gpos_all_ = nullptr;
+  uint64_t gp_cap_ = 0;
+  uint32_t *gbits_cur_ = nullptr, *grank_cur_ = nullptr, *gbits_next_ = nullptr, *grank_next_ = nullptr;
+  uint64_t gbits_cur_cap_ = 0, grank_cur_cap_ = 0, gbits_next_cap_ = 0, grank_next_cap_ = 0;
+  uint32_t *wmask_ = nullptr, *wbase_ = nullptr, *gnew_ = nullptr;
+  uint64_t wmask_cap_ = 0, wbase_cap_ = 0, gnew_cap_ = 0;
+  unsigned long long *link_tmp_ = nullptr, *pk_tmp_ = nullptr;
+  uint64_t link_tmp_cap_ = 0, pk_tmp_cap_ = 0;
   unsigned long long* d_dchk_ = nullptr;
   Counters* d_ctr_dbg_ = nullptr;
   unsigned long long* pk_dbg_ = nullptr;

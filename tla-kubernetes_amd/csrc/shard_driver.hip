@@ -189,6 +189,10 @@ class Comm {
   // of i); every slot is slot_bytes.  The same transfers every level,
   // whatever the ranks' device state, so they always match.
   virtual int sn_exchange(const std::vector<void*>& send, const std::vector<void*>& recv, uint64_t slot_bytes) = 0;
+  // TLC order (ShardBase::tlc_masks): buf[i] = local shard i's n device words
+  // (nullptr: a failed shard, which adds zeroes); every buffer becomes the
+  // element-wise sum over the ranks, stream-ordered on its shard's stream
+  virtual int all_reduce_dev_u32(const std::vector<uint32_t*>& buf, uint64_t n) = 0;
   // one rank in one process and every collective the identity: the level
   // loop needs no gather (Group::run's solo levels)
   virtual bool trivial() const { return false; }
@@ -223,6 +227,22 @@ __global__ void __launch_bounds__(256) k_multi_copy(const CopyXfer* __restrict__
   const uint64_t u1 = u0 + COPY_CHUNK < t.units ? u0 + COPY_CHUNK : t.units;
   for (uint64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x)
     t.dst[u] = t.src ? t.src[u] : make_ulonglong2(0ull, 0ull);
+}
+
+// LocalComm's all_reduce_dev_u32: every emulated rank's words summed into all
+// of them (nullptr: a failed rank, zeroes)
+struct SumBufs {
+  uint32_t* p[16];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_sum_u32(SumBufs b, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v = 0;
+    for (int r = 0; r < b.n; ++r)
+      if (b.p[r]) v += b.p[r][i];
+    for (int r = 0; r < b.n; ++r)
+      if (b.p[r]) b.p[r][i] = v;
+  }
 }
 
 class LocalComm final : public Comm {
@@ -308,6 +328,18 @@ class LocalComm final : public Comm {
       for (int src = 0; src < R; ++src)
         if (src != d) add_xfer((const char*)send[src] + d * slot, (char*)recv[d] + src * slot, slot);
     return run_xfers();    // (synchronised: before any rank's next pack)
+  }
+  int all_reduce_dev_u32(const std::vector<uint32_t*>& buf, uint64_t n) override {
+    if (s_.size() == 1 || n == 0) return 0;
+    for (auto* s : s_) KC_HIP_TRY(hipStreamSynchronize(s->stream()));
+    SumBufs b{};
+    b.n = (int)s_.size();
+    for (size_t i = 0; i < s_.size(); ++i) b.p[i] = buf[i];
+    hipStream_t st = s_[0]->stream();
+    hipLaunchKernelGGL(k_sum_u32, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 65536)), dim3(256), 0, st, b, n);
+    KC_HIP_TRY(hipGetLastError());
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
   }
   int broadcast(int, uint64_t*) override { return 0; }   // the driver read it from the local root
   bool trivial() const override { return s_.size() == 1; }
@@ -454,6 +486,18 @@ class RcclComm final : public Comm {
     return 0;
   }
   bool trivial() const override { return trivial_; }
+  int all_reduce_dev_u32(const std::vector<uint32_t*>& buf, uint64_t n) override {
+    if (trivial_ || n == 0) return 0;
+    hipStream_t st = s_->stream();
+    uint32_t* p = buf[0];
+    if (!p) {                      // a failed rank: zeroes, through the scratch
+      KC_TRY(scratch((n + 1) / 2));
+      p = reinterpret_cast<uint32_t*>(buf_);
+      KC_HIP_TRY(hipMemsetAsync(p, 0, n * 4, st));
+    }
+    KC_NCCL_TRY(rccl()->all_reduce(p, p, n, ncclUint32, ncclSum, comm_, st));
+    return 0;
+  }
   int broadcast(int root, uint64_t* v) override {
     if (trivial_) return 0;
     KC_TRY(scratch(1));
@@ -596,6 +640,23 @@ class HostComm final : public Comm {
     return 0;
   }
   int broadcast(int root, uint64_t* v) override { return call(ops_.broadcast(ops_.ctx, root, v), "broadcast"); }
+  // (the caller's all_reduce_sum works on 64-bit host words)
+  int all_reduce_dev_u32(const std::vector<uint32_t*>& buf, uint64_t n) override {
+    if (n == 0) return 0;
+    hipStream_t st = s_->stream();
+    std::vector<uint32_t> h(n, 0);
+    if (buf[0]) {
+      KC_HIP_TRY(hipMemcpyAsync(h.data(), buf[0], n * 4, hipMemcpyDeviceToHost, st));
+      KC_HIP_TRY(hipStreamSynchronize(st));
+    }
+    std::vector<uint64_t> w(h.begin(), h.end());
+    KC_TRY(call(ops_.all_reduce_sum(ops_.ctx, w.data(), w.size()), "all_reduce_sum"));
+    if (!buf[0]) return 0;
+    for (uint64_t k = 0; k < n; ++k) h[k] = (uint32_t)w[k];
+    KC_HIP_TRY(hipMemcpyAsync(buf[0], h.data(), n * 4, hipMemcpyHostToDevice, st));
+    KC_HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
   int all_reduce_sum(const std::vector<std::vector<uint64_t>>& v, std::vector<uint64_t>& out) override {
     out = v[0];
     return call(ops_.all_reduce_sum(ops_.ctx, out.data(), out.size()), "all_reduce_sum");
@@ -693,6 +754,12 @@ class Group {
     // cold check runs between the settle passes and the emit.  Every rank
     // runs with the same configuration, so they all decide alike.)
     if (cfg_.seen_hbm_bytes) sn_on_ = false;
+    // TLC order: counted levels only, on the deferred frontier (ShardBase::tlc)
+    tlc_ = local_[0]->tlc();
+    if (tlc_) {
+      sn_on_ = false;
+      defer_on_ = true;
+    }
     for (auto* s : local_) s->set_deferred(defer_on_ && !cfg_.seen_hbm_bytes);
     if (!sn_on_) return 0;
     for (auto* s : local_) KC_TRY(s->sn_setup(sn_cap_));
@@ -747,6 +814,30 @@ class Group {
     caps[i] = nb;
     return 0;
   }
+  // TLC order: the rank and local index of the state at position G of
+  // `level` (every rank searches its sorted G values; one all-reduce)
+  int tlc_locate(int level, uint64_t G, int* rank, uint64_t* idx) {
+    std::vector<std::vector<uint64_t>> mine(local_.size(), std::vector<uint64_t>(1, 0));
+    std::string why;
+    for (size_t i = 0; i < local_.size(); ++i) {
+      uint64_t k = 0;
+      bool found = false;
+      if (local_[i]->tlc_locate(level, G, &k, &found) < 0)
+        why = last_error();
+      else if (found)
+        mine[i][0] = ((uint64_t)(local_[i]->rank() + 1) << 48) | k;
+    }
+    std::vector<uint64_t> tot;
+    KC_TRY(comm_->all_reduce_sum(mine, tot));
+    if (tot[0] == 0 || (tot[0] >> 48) > (uint64_t)world_) {
+      set_error("kc_group_run: trace walk: no state at position %llu of level %d%s%s", (unsigned long long)G, level,
+                why.empty() ? "" : ": ", why.c_str());
+      return -EIO;
+    }
+    *rank = (int)(tot[0] >> 48) - 1;
+    *idx = tot[0] & ((1ull << 48) - 1);
+    return 0;
+  }
   int error_trace(uint64_t err, int level, kc_result* res);
   int group_failed(int rank, uint64_t word, const std::vector<int>& fail, const std::string& msg);
 
@@ -767,6 +858,7 @@ class Group {
   bool solo_off_ = false;
   bool serial_ = false;
   bool defer_on_ = true;
+  bool tlc_ = false;                   // TLC order (cfg.tlc_order at world > 1)
   uint32_t sn_cap_ = SN_SLOT_DEFAULT;
   // KC_SERIAL: wait for local shard i's stream (errors surface at its next call)
   void ser(size_t i) {
@@ -1110,10 +1202,27 @@ int Group::run(kc_result* res) {
       if (!fail[i]) note(i, hipSetDevice(local_[i]->device()) == hipSuccess ? 0 : -EIO);
       inject(i, level, 2);
       if (!fail[i]) note(i, local_[i]->insert(recv_[i], nr, &n_new, &e2));
-      if (!fail[i]) note(i, local_[i]->advance());
       status_new[i] = fail[i] ? 0 : n_new;
       status_err[i] = fail[i] ? NONE : std::min(e1[i], e2);
     }
+    if (tlc_) {
+      // the new states' G: per-parent winner masks summed over the ranks
+      // (a failed rank adds zeroes and fails at the next gather)
+      if (total >= (1ull << 31)) {
+        set_error("kc_group_run: tlc_order: a level of %llu states (2^31 at most)", (unsigned long long)total);
+        return -ENOMEM;
+      }
+      std::vector<uint32_t*> masks(nl, nullptr);
+      for (size_t i = 0; i < nl; ++i)
+        if (!fail[i]) note(i, local_[i]->tlc_masks(total, &masks[i]));
+      KC_TRY(comm_->all_reduce_dev_u32(masks, total));
+      for (size_t i = 0; i < nl; ++i) {
+        if (!fail[i]) note(i, local_[i]->tlc_order(total));
+        if (fail[i]) status_new[i] = 0;
+      }
+    }
+    for (size_t i = 0; i < nl; ++i)
+      if (!fail[i]) note(i, local_[i]->advance());
     ++level;
     if ((int)widths.size() >= KC_MAX_LEVELS) {
       set_error("kc_group_run: more than %d levels", KC_MAX_LEVELS);
@@ -1209,6 +1318,8 @@ int Group::error_trace(uint64_t err, int level, kc_result* res) {
     res->trace_len = (int)trace_.size();
     return 0;
   }
+  // (TLC order: keys carry G, located by a search on every rank)
+  if (tlc_) KC_TRY(tlc_locate(lvl, idx, &r, &idx));
   while (lvl > 1) {
     uint64_t key = 0;
     KC_TRY(query_parent(r, lvl, idx, &key));
@@ -1216,6 +1327,7 @@ int Group::error_trace(uint64_t err, int level, kc_result* res) {
     r = (int)(key >> 60);
     idx = (key >> 16) & KEY44;
     --lvl;
+    if (tlc_) KC_TRY(tlc_locate(lvl, idx, &r, &idx));
   }
   uint64_t init_key = 0;
   KC_TRY(query_parent(r, 1, idx, &init_key));

@@ -66,6 +66,9 @@ class ModelConfig:
     # 0 = unlimited), then to files in spill_dir
     seen_hbm_bytes: int = 0
     seen_host_bytes: int = 0
+    # sharded runs at R > 1: claims in sequential-BFS order, so errors and
+    # traces equal TLC -workers 1's (a per-level all-reduce and sort)
+    tlc_order: bool = False
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()

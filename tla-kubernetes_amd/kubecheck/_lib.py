@@ -36,6 +36,7 @@ class KcModelConfig(C.Structure):
         ("frontier_hbm_bytes", C.c_uint64), ("frontier_host_bytes", C.c_uint64),
         ("frontier_segment_states", C.c_uint64), ("spill_dir", C.c_char_p), ("trace_host", C.c_int),
         ("seen_hbm_bytes", C.c_uint64), ("seen_host_bytes", C.c_uint64),
+        ("tlc_order", C.c_int),
     ]
 
 
