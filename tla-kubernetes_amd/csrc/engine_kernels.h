@@ -671,8 +671,12 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
 // TLC (SH only): claims, records and keys by the parents' G (ClaimKeys; the
 // sharded loop's tlc_order mode), a variant of its own so the default one's
 // registers are untouched
+#ifndef KC_SH_WAVES
+#define KC_SH_WAVES 6
+#endif
 template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false>
-__global__ void __launch_bounds__(CLAIM_TILE) __attribute__((amdgpu_waves_per_eu(6, 6)))
+__global__ void __launch_bounds__(CLAIM_TILE)
+__attribute__((amdgpu_waves_per_eu(SH ? KC_SH_WAVES : 6, SH ? KC_SH_WAVES : 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,

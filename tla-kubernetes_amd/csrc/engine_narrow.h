@@ -381,25 +381,37 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
 #pragma unroll
     for (int k = 0; k < PT; ++k)
       e[k] = sub + k * NARROW_ESUB < tot ? *reinterpret_cast<const ulonglong2*>(&lt[hs[k]]) : make_ulonglong2(0, 0);
+    // the level's first copies go into the ClaimSet (new unless an earlier
+    // level stored them): every first CAS issued back to back, so a lane's
+    // round trips overlap instead of running one after another; linear
+    // probing then goes on for the few whose slot held another fingerprint
+    uint64_t ixs[PT];
+    unsigned long long os[PT];
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const int t = sub + k * NARROW_ESUB;
-      if (t >= tot) continue;
       const unsigned int key = (unsigned int)((i << 5) | (uint64_t)t);
-      if ((unsigned int)~(unsigned int)e[k].y != key) continue;    // an earlier copy of the level holds it
+      // (an earlier copy of the level holds the entry: not this lane's)
+      const bool first = t < tot && (unsigned int)~(unsigned int)e[k].y == key;
+      e[k].x = first ? e[k].x : 0ull;
+      ixs[k] = first ? bucket_of(e[k].x, nslots) : 0ull;
+      os[k] = first ? atomicCAS(&cs[ixs[k]].fp, 0ull, e[k].x) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
       const uint64_t fp = e[k].x;
-      // the level's first copy: into the ClaimSet, new unless an earlier level stored it
+      if (!fp) continue;
+      const int t = sub + k * NARROW_ESUB;
       ++probes;
-      uint64_t ix = bucket_of(fp, nslots);
-      for (uint64_t q = 0; q < nslots; ++q) {
-        const unsigned long long o = atomicCAS(&cs[ix].fp, 0ull, fp);
-        if (o == 0ull) {
-          cs[ix].nclaim = ~make_claim(succ_level, (i << 8) | (uint64_t)t);
-          mine |= 1u << t;
-          break;
-        }
-        if (o == fp) break;
+      uint64_t ix = ixs[k];
+      unsigned long long o = os[k];
+      for (uint64_t q = 1; o != 0ull && o != fp && q < nslots; ++q) {
         ix = (ix + 1 == nslots) ? 0 : ix + 1;
+        o = atomicCAS(&cs[ix].fp, 0ull, fp);
+      }
+      if (o == 0ull) {
+        cs[ix].nclaim = ~make_claim(succ_level, (i << 8) | (uint64_t)t);
+        mine |= 1u << t;
       }
     }
   }

@@ -526,14 +526,46 @@ k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, co
     if (live) {
       const int tot = sc->ptot[i];
       const uint32_t rm = sc->rmask[i];
-      for (int t = sub; t < tot; t += SN_ESUB) {
-        if ((rm >> t) & 1u) continue;
-        const uint32_t hx = sc->hidx[i * 32 + t];
-        if (hx >= SN_LT) continue;                    // (k_sn_expand wrote every own successor's slot)
-        const NarrowLT e = lt[hx];
-        if (~e.nkey != sn_key(rank, i, (uint32_t)t)) continue;    // an earlier copy of the level holds it
+      // the lane's own first copies (an earlier copy of the level holds the
+      // others; k_sn_expand wrote every own successor's slot): their first
+      // ClaimSet CASes issued back to back, then linear probing for the few
+      // that met another fingerprint
+      constexpr int PT = 32 / SN_ESUB;
+      uint64_t fps[PT], ixs[PT];
+      unsigned long long os[PT];
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const int t = sub + k * SN_ESUB;
+        fps[k] = 0;
+        if (t < tot && !((rm >> t) & 1u)) {
+          const uint32_t hx = sc->hidx[i * 32 + t];
+          if (hx < SN_LT) {
+            const NarrowLT e = lt[hx];
+            if (~e.nkey == sn_key(rank, i, (uint32_t)t)) fps[k] = e.fp;
+          }
+        }
+        ixs[k] = fps[k] ? bucket_of(fps[k], nslots) : 0ull;
+        os[k] = fps[k] ? atomicCAS(&cs[ixs[k]].fp, 0ull, (unsigned long long)fps[k]) : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint64_t fp = fps[k];
+        if (!fp) continue;
+        const int t = sub + k * SN_ESUB;
         ++probes;
-        if (insert(e.fp, ((uint64_t)rank << CLAIM_RANK_SHIFT) | (i << 8) | (uint64_t)t)) mine |= 1u << t;
+        uint64_t ix = ixs[k];
+        unsigned long long o = os[k];
+        uint64_t q = 1;
+        for (; o != 0ull && o != fp && q < nslots; ++q) {
+          ix = (ix + 1 == nslots) ? 0 : ix + 1;
+          o = atomicCAS(&cs[ix].fp, 0ull, (unsigned long long)fp);
+        }
+        if (o == 0ull) {
+          cs[ix].nclaim = ~make_claim(succ_level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | (i << 8) | (uint64_t)t);
+          mine |= 1u << t;
+        } else if (o != fp) {
+          atomicAdd(&C->overflow, 1ull);               // a full table
+        }
       }
     }
 #pragma unroll

@@ -1,12 +1,13 @@
 """Per-rank, per-kernel attribution of an emulated sharded NP=2 check
 (VERDICT r4 "next" item 1a).
 
-  run:        python tools/shard_attr.py run R [--checks K]
+  run:        python tools/shard_attr.py run R [--checks K] [--tlc]
               K (default 2) sharded NP=2 checks with R ranks emulated on one
               GPU; with KC_SERIAL=1 in the environment every rank's stage is
               synchronised before the next rank's launches, so no two ranks'
               kernels overlap.  Prints one JSON line per check (wall ms,
-              distinct).  Run it under rocprofv3 --kernel-trace.
+              distinct).  Run it under rocprofv3 --kernel-trace.  --tlc:
+              with ModelConfig.tlc_order (TLC-ordered claims).
   summarize:  python tools/shard_attr.py summarize TRACE_DIR R [--out f.json]
               reads rocprofv3's *_kernel_trace.csv (and *_memory_copy_trace.csv
               if present), keeps the last check (from the last R
@@ -26,19 +27,21 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(R, checks):
+def run(R, checks, tlc=False):
     sys.path.insert(0, os.path.join(ROOT, "tla-kubernetes_amd"))
     import torch  # noqa: F401  (owns the HIP runtime first)
     from kubecheck import ModelConfig
     from kubecheck.distributed import NativeShardedChecker
-    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False), emulate=R)
+    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False, tlc_order=tlc), emulate=R)
     try:
         for k in range(checks):
             t0 = time.perf_counter()
             r = mc.run()
             dt = time.perf_counter() - t0
             print(json.dumps({"R": R, "check": k, "ms": round(dt * 1e3, 2), "distinct": r["distinct"],
-                              "depth": r["depth"], "serial": os.environ.get("KC_SERIAL", "0")}), flush=True)
+                              "depth": r["depth"], "serial": os.environ.get("KC_SERIAL", "0"), "tlc": tlc,
+                              "lib": os.path.basename(os.environ.get("KUBECHECK_LIB", "libkubecheck.so"))}),
+                  flush=True)
     finally:
         mc.close()
 
@@ -76,6 +79,23 @@ def summarize(d, R, out):
         nm = short(name) if kind == "k" else name
         per[rk][nm] += (t1 - t0) / 1e6
         calls[rk][nm] += 1
+    # per counted level (a level starts at its k_head_reset) of every rank:
+    # kernel time and k_claim's share; narrow batches (k_sn_*) apart
+    lv = defaultdict(list)
+    for kind, name, sid, t0, t1 in last:
+        rk = rank_of.get(sid, -1)
+        if rk < 0 or kind != "k":
+            continue
+        nm = short(name)
+        if nm.startswith("k_sn_"):
+            continue
+        if nm == "k_head_reset" or not lv[rk]:
+            lv[rk].append([0.0, 0.0, 0])
+        cur = lv[rk][-1]
+        cur[0] += (t1 - t0) / 1e3
+        cur[2] += 1
+        if nm.startswith("k_claim"):
+            cur[1] += (t1 - t0) / 1e3
     tot = {rk: sum(v.values()) for rk, v in per.items()}
     names = sorted({n for v in per.values() for n in v}, key=lambda n: -sum(per[r][n] for r in per))
     res = {"R": R, "span_ms": round((max(r[4] for r in last) - last[0][3]) / 1e6, 3),
@@ -85,8 +105,10 @@ def summarize(d, R, out):
            "per_rank_ms": {str(k): round(v, 3) for k, v in sorted(tot.items())},
            "per_kernel_ms": {n: {"sum": round(sum(per[r][n] for r in per), 3),
                                  "max_rank": round(max(per[r][n] for r in per if r >= 0) if any(r >= 0 for r in per) else 0, 3),
-                                 "calls": sum(calls[r][n] for r in calls)} for n in names}}
-    print(json.dumps(res, indent=1))
+                                 "calls": sum(calls[r][n] for r in calls)} for n in names},
+           # [kernel us, k_claim us, launches] per counted level, per rank
+           "levels_us": {str(k): [[round(a, 1), round(b, 1), c] for a, b, c in v] for k, v in sorted(lv.items())}}
+    print(json.dumps({k: v for k, v in res.items() if k != "levels_us"}, indent=1))
     if out:
         json.dump(res, open(out, "w"), indent=1)
 
@@ -94,7 +116,7 @@ def summarize(d, R, out):
 if __name__ == "__main__":
     a = sys.argv[1:]
     if a and a[0] == "run":
-        run(int(a[1]), int(a[a.index("--checks") + 1]) if "--checks" in a else 2)
+        run(int(a[1]), int(a[a.index("--checks") + 1]) if "--checks" in a else 2, "--tlc" in a)
     elif a and a[0] == "summarize":
         summarize(a[1], int(a[2]), a[a.index("--out") + 1] if "--out" in a else None)
     else:
