@@ -281,7 +281,7 @@ def cpu_baseline(kw, seconds):
     if (kw["nc"], kw["np"], kw["ns"]) == (1, 2, 1):
         import glob
         # the whole model at 16, 64, 128 and all 256 affinity CPUs of a GPU
-        # box's host (tools/gpu_r04_probe.sh): the box's CPU share makes more
+        # box's host (tools/gpu.sh probe): the box's CPU share makes more
         # threads slower, so 16 is the comparator's best
         sweep = []
         for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r04a_cpu_np2_full_t*.json"))):

@@ -1,6 +1,6 @@
 """The native sharded level loop with ONE SHARD PER PROCESS at world 2 and 3,
 on the one-GPU box: the layout `bench.py --gpus N` runs on N GPUs (RcclComm),
-which RCCL itself refuses on one device ("duplicate GPU", tools/gpu_r03_rccl2.sh).
+which RCCL itself refuses on one device ("duplicate GPU"; round-3 tools/gpu_r03_rccl2.sh, git history).
 Here the collectives go over gloo through kc_group_create_host (HostComm,
 shard_driver.hip): the same Group::run with one local shard and R > 1, the
 device all-gather rows written by k_owner_totals, the exchange plan handed
