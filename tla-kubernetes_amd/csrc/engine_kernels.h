@@ -674,6 +674,20 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
 #ifndef KC_SH_WAVES
 #define KC_SH_WAVES 6
 #endif
+// Diagnostic builds (-DKC_CLAIM_TRACE): thread 0 of every k_claim workgroup
+// stamps the wall clock (100 MHz) at its phase boundaries and adds each
+// phase's duration to g_ctrace[1..7] ([0] workgroups, [8] the longest
+// workgroup, [9] / [10] the earliest start / latest end); the host reads and
+// resets it after each launch (shard.hip).
+#ifdef KC_CLAIM_TRACE
+static __device__ unsigned long long g_ctrace[16];
+#define KC_CT(k)                                 \
+  do {                                           \
+    if (threadIdx.x == 0) ct[k] = wall_clock64(); \
+  } while (0)
+#else
+#define KC_CT(k) ((void)0)
+#endif
 template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false>
 __global__ void __launch_bounds__(CLAIM_TILE)
 __attribute__((amdgpu_waves_per_eu(SH ? KC_SH_WAVES : 6, SH ? KC_SH_WAVES : 6)))
@@ -735,6 +749,10 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   };
   sh_cur[threadIdx.x] = 0;
   if (threadIdx.x < A_COUNT * AS) sh_act[threadIdx.x] = sh_actd[threadIdx.x] = 0;
+#ifdef KC_CLAIM_TRACE
+  unsigned long long ct[8] = {};
+#endif
+  KC_CT(0);
   __syncthreads();
   const uint32_t tile = spread_tile(blockIdx.x, gridDim.x, sh.spread);
 #ifdef KC_DIAG
@@ -837,6 +855,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   // (the parent's index travels in bits 56-63 of its plan, which locate()
   // never reads: one register more across the loop spills k_claim)
   static_assert(!DEAL || (M::NSLOT * 6 <= 56 && CLAIM_TILE <= 256), "deal: lp in the plan word");
+  KC_CT(1);
   if (DEAL) {
     const unsigned int pos = live ? atomicAdd(&deal_cnt[tot], 1u) : 0u;
     __syncthreads();
@@ -885,6 +904,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     __syncthreads();
   }
+  KC_CT(2);
   if (live) {
 #define KC_LP (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x)
     // KC_LOCATE_SWAR: the slot lookup from cumulative counts (its top byte
@@ -952,6 +972,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 #undef KC_LP
   }
   __syncthreads();
+  KC_CT(3);
   if (ABL != 0) {
     if (live) scratch[i] = sh_cur[threadIdx.x] ^ sh_key[threadIdx.x] ^ (unsigned)sh_fp[threadIdx.x];
     return;
@@ -982,6 +1003,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     __syncthreads();
   }
+  KC_CT(4);
   // every tile representative claims its fp in the ClaimSet.  A lane takes
   // representatives k = tid, tid + 256, ... in groups of KC_CLAIM_BATCH:
   // the first probe loads of a group are issued back to back, then each
@@ -1053,10 +1075,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
   }
   __syncthreads();
+  KC_CT(5);
   if (SH && sh.stage)
     stage_records<M, NT, TLC>(sh, live, s, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
                          sh_rep, sh_cnt, sh_proj, sh_fp, sh_key, tile,
                          base + tile0 + (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x), C);
+  KC_CT(6);
   if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
   if (live) newmask[i] = sh_cur[threadIdx.x];
   if (SH && live) {
@@ -1079,6 +1103,16 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     }
     if (threadIdx.x == 0 && sh_dcand) atomicAdd(&stripe(C).next_cand, sh_dcand);
   }
+#ifdef KC_CLAIM_TRACE
+  KC_CT(7);
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_ctrace[0], 1ull);
+    for (int k = 1; k < 8; ++k) atomicAdd(&g_ctrace[k], ct[k] - ct[k - 1]);
+    atomicMax(&g_ctrace[8], ct[7] - ct[0]);
+    atomicMin(&g_ctrace[9], ct[0]);
+    atomicMax(&g_ctrace[10], ct[7]);
+  }
+#endif
 #ifdef KC_DIAG
 #pragma unroll
   for (int r = 0; r < 4; ++r) {

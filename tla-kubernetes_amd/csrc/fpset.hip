@@ -196,10 +196,17 @@ void DevClaimSet::release() {
 // larger clear included).  Past 1/3 load the table grows to
 // land at <= 1/4; when HBM cannot hold that, at <= 1/2.
 int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
+  // KC_CS_LOAD=k (A/B): grow once the reserved fill would pass 1/k of the
+  // slots, to at most 1/(k + 1) (default k = 3)
+  static const uint64_t ld = [] {
+    const char* e = getenv("KC_CS_LOAD");
+    const int v = e ? atoi(e) : 0;
+    return (uint64_t)(v >= 2 && v <= 8 ? v : 3);
+  }();
   const uint64_t need = count + extra;
-  if (need * 3 <= capacity()) return 0;
+  if (need * ld <= capacity()) return 0;
   uint64_t ns = nslots, ns_min = nslots;
-  while (need * 4 > ns) ns *= 2;
+  while (need * (ld + 1) > ns) ns *= 2;
   while (need * 2 > ns_min) ns_min *= 2;
   ClaimEntry* nt = nullptr;
   if (hipMalloc(&nt, ns * sizeof(ClaimEntry)) != hipSuccess) {

@@ -1087,6 +1087,22 @@ class ShardT final : public ShardBase {
                            d_ctr_, sh, df);
     }
     if (cfg_.timing) KC_HIP_TRY(hipEventRecord(ev_[1], st_));
+#ifdef KC_CLAIM_TRACE
+    {
+      unsigned long long t[16];
+      KC_HIP_TRY(hipStreamSynchronize(st_));
+      KC_HIP_TRY(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_ctrace), sizeof t));
+      if (t[0])
+        fprintf(stderr, "ctrace rank %d level %d n %llu tiles %llu | us/block: prep %.2f deal %.2f succ %.2f compact %.2f "
+                "claims %.2f stage %.2f tail %.2f | longest %.2f span %.2f\n", rank_, level_, (unsigned long long)n_,
+                (unsigned long long)tiles, t[1] * 0.01 / t[0], t[2] * 0.01 / t[0], t[3] * 0.01 / t[0],
+                t[4] * 0.01 / t[0], t[5] * 0.01 / t[0], t[6] * 0.01 / t[0], t[7] * 0.01 / t[0], t[8] * 0.01,
+                (t[10] - t[9]) * 0.01);
+      memset(t, 0, sizeof t);
+      t[9] = ~0ull;
+      KC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace), t, sizeof t));
+    }
+#endif
     if (stage_level_) {
       // positions of the tiles' segments in the owner-grouped send buffer and
       // the owner totals (the all-gather row)
