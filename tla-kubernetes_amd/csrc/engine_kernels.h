@@ -630,6 +630,8 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
   Record<M>* out = reinterpret_cast<Record<M>*>(sh.stage);
   const typename M::Plan pl{counts, 0, -1, -1};
   const uint32_t proj = sh_proj[lp];
+  static_assert(M::OWNER_BITS == 4, "owner bits >> (4 - k) at R = 2^k");
+  const int sh_pow2 = R == 1 ? 4 : R == 2 ? 3 : R == 4 ? 2 : R == 8 ? 1 : -1;
   uint64_t c0 = 0, c1 = 0;            // the parent's records so far per owner, 6 bits each (owners 0-9, 10-14)
   for (; mask; mask &= mask - 1) {
     const int t = __ffs(mask) - 1;
@@ -641,8 +643,9 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
     typename M::State x;
     int who;
     M::apply(s, slot, j, f, x, who);
-    const uint64_t fp = M::template fingerprint_succ<1>(s, fold, x, who, proj);
-    const uint32_t o = owner_of(fp, R);
+    // (R = 2^k: the owner from the successor's owner bits alone, no fold)
+    const uint32_t o = sh_pow2 >= 0 ? (M::owner_bits_succ(s, x, who, proj) >> sh_pow2)
+                                    : owner_of(M::template fingerprint_succ<1>(s, fold, x, who, proj), R);
     uint32_t r;
     if (o < 10) {
       r = (uint32_t)(c0 >> (6 * o)) & 63u;

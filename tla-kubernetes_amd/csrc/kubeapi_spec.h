@@ -866,6 +866,26 @@ struct Model {
       return fp_final<0>(h, x);
   }
 
+  // The owner bits of successor x alone (OWN = 1; what fingerprint_succ<1>
+  // puts in its top bits), without the fold's re-mixing: at R = 2^k ranks
+  // the owner floor(fp * R / 2^63) is these bits >> (4 - k), whatever the
+  // fold bits below them (shard.hip's record staging needs only the owner)
+  KC_HD static uint32_t owner_bits_succ(const State& s, const State& x, int who, uint32_t proj_s) {
+    uint32_t wo = proj_s;
+    const int wi = 1 + A + who / OBJ_PER_WORD;
+    uint64_t o = s.w[1 + A], nw = x.w[1 + A];
+#pragma unroll
+    for (int k = 1; k < OBJ_WORDS; ++k) {
+      uint64_t vo = s.w[1 + A + k], vn = x.w[1 + A + k];
+      opaque(vo);
+      opaque(vn);
+      o = (wi == 1 + A + k) ? vo : o;
+      nw = (wi == 1 + A + k) ? vn : nw;
+    }
+    if (o != nw) wo ^= owner_word(o ^ nw, wi - (1 + A));
+    return (uint32_t)owner_hash(x.w[0], wo);
+  }
+
   // ------------------------------------------------ canonical tuple (ABI)
   // Interchange form shared with tests (include/kubecheck.h): word 0 =
   // apiState as a U mask; then 19 words per process: pc, op, obj, kind, sr,

@@ -267,7 +267,15 @@ int kc_spec_fp_selfcheck(const kc_model_config* cfg, const uint64_t* tuple) {
       M::apply(s, slot, j, f, x, who);
       if (M::fingerprint_succ(s, fold, x, who) != M::fingerprint(x)) ++bad;
       // the sharded path's owner projection (incremental from the parent's)
-      if (M::template fingerprint_succ<1>(s, fold, x, who, M::owner_proj(s)) != M::template fingerprint<1>(x)) ++bad;
+      const uint64_t fp1 = M::template fingerprint<1>(x);
+      if (M::template fingerprint_succ<1>(s, fold, x, who, M::owner_proj(s)) != fp1) ++bad;
+      // the record staging's owner at R = 2^k (owner_bits_succ >> (4 - k))
+      // is the fingerprint's owner floor(fp * R / 2^63)
+      const uint32_t ob = M::owner_bits_succ(s, x, who, M::owner_proj(s));
+      for (int k = 0; k <= 3; ++k) {
+        const uint64_t R = 1ull << k;
+        if ((uint64_t)(ob >> (4 - k)) != (uint64_t)(((unsigned __int128)(fp1 << 1) * R) >> 64)) ++bad;
+      }
       // the sharded path's exchange record round-trips the successor exactly
       uint64_t r[Record<M>::RW];
       const uint64_t key = 0x9e3779b97f4a7c15ull * (uint64_t)(t + 1);
