@@ -177,6 +177,8 @@ class EngineT final : public EngineBase {
     if (sp) claim_args_.spread = (uint32_t)atoi(sp);
     const char* ts = getenv("KC_TSCAN");
     tscan_ = spill_ || !(ts && ts[0] == '0');
+    const char* fz = getenv("KC_FUSE_SCAN");
+    fuse_scan_ = !(fz && fz[0] == '0');
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
@@ -504,10 +506,18 @@ class EngineT final : public EngineBase {
                                succ_level, abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_);
           });
         }
-        timed(KK_RESOLVE, [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr); });
+        // (a small chunk: the overflow list's pass B inside the tile scan's launch)
+        const bool fuse = tscan_ && fuse_scan_ && cn <= FUSE_OVF_SCAN_MAX;
+        timed(KK_RESOLVE,
+              [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr, fuse); });
         if (tscan_) {
           timed(KK_SCAN, [&] {
-            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
+            if (fuse)
+              hipLaunchKernelGGL(k_ovf_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, claim_args_.ovf, cn, start,
+                                 cs_.t, cs_.nslots, succ_level, newmask_, d_ctr_, ClaimKeys(0u), ttot_, tiles, toff_,
+                                 tscan_reg_);
+            else
+              hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ttot_, tiles, toff_, tscan_reg_);
           });
         } else {
         size_t tmp_bytes = 0;
@@ -1799,7 +1809,8 @@ class EngineT final : public EngineBase {
   int settle_tp_ = SETTLE_TP_DEFAULT;   // claim tiles per settle workgroup (KC_SETTLE_TP)
   // settle passes A and B of a chunk's tiles (k_settle_rec, or k_settle_mt
   // with settle_tp_ tiles per workgroup), then the overflow list's pass B
-  void launch_settle(uint64_t cn, uint64_t start, unsigned tiles, uint32_t succ_level, uint32_t* ttot) {
+  void launch_settle(uint64_t cn, uint64_t start, unsigned tiles, uint32_t succ_level, uint32_t* ttot,
+                     bool ovf_in_scan = false) {
     if (settle_tp_ == 1) {
       hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
                          cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
@@ -1821,9 +1832,11 @@ class EngineT final : public EngineBase {
       KC_SETTLE_MT(8)
 #undef KC_SETTLE_MT
     }
-    hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
-                       cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
+    if (!ovf_in_scan)   // (else k_ovf_tile_scan settles it)
+      hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
+                         cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
   }
+  bool fuse_scan_ = true;   // KC_FUSE_SCAN=0: small chunks keep the separate overflow pass B launch (A/B)
   int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;
   uint64_t ttot_cap_ = 0, toff_cap_ = 0;

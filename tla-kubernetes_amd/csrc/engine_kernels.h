@@ -1479,6 +1479,22 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
   tile_scan_body(tot, T, off, reg_ok, ScanMarks{}, nullptr);
 }
 
+// A small chunk's settle pass B over its candidate overflow list and the
+// tile scan in one workgroup (round 5): the list of a chunk of <= 2^16
+// parents is short (usually empty), so the 1,024-workgroup k_settle_ovf<1>
+// launch and k_tile_scan's launch become one.  The overflow winners' tile
+// counts are this workgroup's own atomics, visible to its scan after the
+// barrier.  (A long list is still settled correctly, only by one workgroup.)
+constexpr uint64_t FUSE_OVF_SCAN_MAX = 1ull << 16;
+static __global__ void __launch_bounds__(TSCAN_THREADS)
+k_ovf_tile_scan(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets,
+                uint32_t level, uint32_t* __restrict__ newmask, Counters* __restrict__ C, ClaimKeys rank,
+                uint32_t* __restrict__ tile_total, uint32_t T, uint32_t* __restrict__ off, int reg_ok) {
+  settle_ovf_blocks<1>(0, 1, ovf, n, base, cs, nbuckets, level, newmask, C, rank, tile_total);
+  __syncthreads();
+  tile_scan_body(tile_total, T, off, reg_ok, ScanMarks{}, nullptr);
+}
+
 // popcount(newmask): the scan's input (new states per parent)
 struct NewCount {
   __host__ __device__ __forceinline__ uint32_t operator()(uint32_t m) const {

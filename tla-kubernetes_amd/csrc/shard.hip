@@ -360,6 +360,22 @@ k_win_scan(const uint32_t* __restrict__ wtot, uint32_t tiles, uint32_t rblocks, 
   }
 }
 constexpr unsigned SHARD_OVF_BLOCKS = 256;
+// A small level (<= FUSE_OVF_SCAN_MAX own parents): the overflow list's
+// pass B and k_win_scan in one workgroup (engine_kernels.h k_ovf_tile_scan)
+__global__ void __launch_bounds__(TSCAN_THREADS)
+k_ovf_win_scan(CandOvf ovf, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots, uint32_t level,
+               uint32_t* __restrict__ newmask, Counters* __restrict__ C, ClaimKeys rank, uint32_t* __restrict__ wtot,
+               uint32_t tiles, uint32_t rblocks, uint32_t* __restrict__ woff) {
+  settle_ovf_blocks<1>(0, 1, ovf, n_local, 0, cs, nslots, level, newmask, C, rank, wtot);
+  __syncthreads();
+  __shared__ unsigned int sh_mark[4];
+  const uint32_t cells = tiles + rblocks;
+  tile_scan_body(wtot, cells, woff, 1, ScanMarks{cells, 2, tiles}, sh_mark);
+  if (threadIdx.x == 0) {
+    C->chunk_base = sh_mark[2];
+    C->level_new = sh_mark[1];
+  }
+}
 
 // Narrow levels: both exclusive scans (own winners' popcounts, records'
 // isnew flags) and k_shard_base's totals in one workgroup, instead of two
@@ -807,6 +823,8 @@ class ShardT final : public ShardBase {
       const int v = atoi(tp);
       settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
     }
+    const char* fz = getenv("KC_FUSE_SCAN");       // KC_FUSE_SCAN=0: no fused overflow pass B + scan (A/B)
+    fuse_scan_ = !(fz && fz[0] == '0');
     const char* dc = getenv("KC_DEFER_CHECK");     // diagnostic: rebuilt states against materialised ones
     defer_check_ = dc && dc[0] == '1';
     tlc_ = cfg.tlc_order && world > 1;
@@ -1358,10 +1376,15 @@ class ShardT final : public ShardBase {
       KC_TRY(grow_buffer(wtot_, wtot_cap_, (uint64_t)lt + rb + 8, false, st_));
       KC_TRY(grow_buffer(woff_, woff_cap_, (uint64_t)lt + rb + 8, false, st_));
       if (lt + rb) settle(1, 0, wtot_);
-      if (n_)
-        hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SHARD_OVF_BLOCKS), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
-                           cs_.nslots, succ_level, newmask_, d_ctr_, ck, wtot_);
-      hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
+      if (n_ && fuse_scan_ && n_ <= FUSE_OVF_SCAN_MAX) {
+        hipLaunchKernelGGL(k_ovf_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ovf_, n_, cs_.t, cs_.nslots,
+                           succ_level, newmask_, d_ctr_, ck, wtot_, lt, rb, woff_);
+      } else {
+        if (n_)
+          hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SHARD_OVF_BLOCKS), dim3(256), 0, st_, ovf_, n_, (uint64_t)0, cs_.t,
+                             cs_.nslots, succ_level, newmask_, d_ctr_, ck, wtot_);
+        hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
+      }
     } else {
       hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(sgrid), dim3(256), 0, st_, lt, rb, n_, cs_.t,
                          cs_.nslots, succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_,
@@ -2054,6 +2077,7 @@ class ShardT final : public ShardBase {
   double rec_ratio_ = 1.0;             // records sent per parent, last level (the staging estimate)
   // the tile-count insert path: own tiles' and record blocks' new-state counts, their scan
   bool tcount_ = true;
+  bool fuse_scan_ = true;              // small levels: k_ovf_win_scan (KC_FUSE_SCAN)
   int settle_tp_ = SETTLE_TP_DEFAULT;
   uint32_t *wtot_ = nullptr, *woff_ = nullptr;
   uint64_t wtot_cap_ = 0, woff_cap_ = 0;
