@@ -556,29 +556,48 @@ static __global__ void k_parent_chain(const unsigned long long* __restrict__ par
 // (sh_cnt, 4 x 8 bits per word) complete and the LDS table free.
 //   1. per owner, the exclusive prefix of the counts over the tile's parents
 //      (lane = parent; two owners per word in 16-bit halves: a tile has at
-//      most 256 x 32 records) -> pre[owner pair][parent] in the table's LDS;
+//      most 256 x 32 records) -> pre[owner pair][parent]; the prefix of the
+//      parents' remote-representative counts -> rbase[parent]; each dealt
+//      lane leaves its parent's plan word (and fold) in LDS;
 //   2. the tile's totals per owner, its segment reserved with one atomic,
 //      tcnt / stoff for k_shard_gather;
-//   3. each dealt lane (its parent's state, fold and plan still in
-//      registers) re-applies its parent's remote successors in position
-//      order and stores each record at segment base + owner base + parent
-//      prefix + its rank among the parent's records of that owner.
-// The fingerprint is recomputed for the owner (the claim loop had it in LDS
-// only); no parent is reloaded and nothing is planned again.
+//   3. the tile's remote representatives dealt out flat, one per lane per
+//      round (round 5: per parent, one lane ran all of its parent's records,
+//      and a wave waited for its busiest parent): lane r finds its parent
+//      and position (rbase, the remote mask), reloads the parent (the
+//      frontier or the rebuilt states: L2), re-applies the successor and
+//      takes its owner; after a barrier, its rank among the parent's records
+//      of that owner (their owners, as 4-bit codes per position in LDS, are
+//      all known: the parent's lower positions are lower ranks r) places
+//      the record at segment base + owner base + the parent's prefix for
+//      that owner + that rank — the order the per-parent loop produced.
+// At R = 2^k the owner comes from the successor's owner bits alone
+// (kubeapi_spec.h owner_bits_succ), else from its fingerprint (the parent's
+// fold kept in LDS).
 template <class M, int NT, bool TLC = false>
-__device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, const typename M::State& s,
-                                              uint64_t fold, uint64_t counts, uint32_t lp, Flags f,
-                                              const unsigned int* sh_rep, const unsigned int* sh_cnt,
-                                              const uint32_t* sh_proj, unsigned long long* sh_fp,
-                                              unsigned int* sh_key, uint32_t tile, uint64_t pbase,
-                                              Counters* __restrict__ C) {
+__device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, uint64_t fold, uint64_t counts,
+                                              uint32_t lp, Flags f, const unsigned int* sh_rep,
+                                              const unsigned int* sh_cnt, const uint32_t* sh_proj,
+                                              unsigned long long* sh_fp, unsigned int* sh_key, uint32_t tile,
+                                              const typename M::State* __restrict__ psrc, uint64_t pbase0,
+                                              uint64_t pkey0, Counters* __restrict__ C) {
   constexpr bool SWAR = KC_LOCATE_SWAR && M::CUM_OK;
   static_assert(NT * 8 >= 8 * CLAIM_TILE * 4, "pre[] needs (world + 1) / 2 x 256 words (world <= 15)");
+  static_assert(NT >= 1536 && CLAIM_TILE == 256, "stage LDS layout (below)");
   const uint32_t R = sh.world, npair = (R + 1) / 2;
+  // LDS (the claim table's, free now): sh_fp as u32 pre[npair][256], then
+  // u64 pcnt[256] and pfold[256] (<= 8 x 128 + 512 u64 words); sh_key:
+  // wsum [0, 32), tt [32, 64), seg [64, 66), rbase [128, 384), rep wave
+  // totals [384, 388), owner codes onib[256][4] at [512, 1536)
   uint32_t* pre = reinterpret_cast<uint32_t*>(sh_fp);   // [npair][CLAIM_TILE]
+  unsigned long long* pcnt = sh_fp + npair * (CLAIM_TILE / 2);
+  unsigned long long* pfold = pcnt + CLAIM_TILE;
   unsigned int* wsum = sh_key;                          // [4 waves][8 pairs]
   unsigned int* tt = sh_key + 32;                       // [0, 16): per-owner totals; [16, 32): owner bases
   unsigned int* seg = sh_key + 64;                      // segment base, lo / hi (~0: none)
+  unsigned int* rbase = sh_key + 128;
+  unsigned int* rwave = sh_key + 384;
+  unsigned int* onib = sh_key + 512;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (uint32_t w = 0; w < npair; ++w) {
     const uint32_t o0 = 2 * w, o1 = 2 * w + 1;
@@ -593,11 +612,30 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
     if (lane == 63) wsum[wv * 8 + w] = x;
     pre[w * CLAIM_TILE + tid] = x - v;
   }
+  const uint32_t nrep = (uint32_t)__builtin_popcount(sh_rep[tid]);
+  uint32_t rx = nrep;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(rx, d, 64);
+    if (lane >= (uint32_t)d) rx += y;
+  }
+  if (lane == 63) rwave[wv] = rx;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) onib[tid * 4 + q] = 0u;
+  if (live) {
+    pcnt[lp] = counts;
+    pfold[lp] = fold;
+  }
   __syncthreads();
   for (uint32_t w = 0; w < npair; ++w) {
     uint32_t b = 0;
     for (uint32_t k = 0; k < wv; ++k) b += wsum[k * 8 + w];
     pre[w * CLAIM_TILE + tid] += b;
+  }
+  {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < wv; ++k) b += rwave[k];
+    rbase[tid] = b + rx - nrep;
   }
   if (tid < R) {
     uint32_t a = 0;
@@ -624,40 +662,63 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, co
   if (tid < R) sh.tcnt[(uint64_t)tid * gridDim.x + tile] = tt[tid];
   __syncthreads();
   const unsigned long long sb = (unsigned long long)seg[0] | ((unsigned long long)seg[1] << 32);
-  if (!live || sb == ~0ull) return;
-  uint32_t mask = sh_rep[lp];
-  if (!mask) return;
+  const uint32_t total = rwave[0] + rwave[1] + rwave[2] + rwave[3];
+  if (sb == ~0ull || total == 0) return;                 // (uniform over the workgroup)
   Record<M>* out = reinterpret_cast<Record<M>*>(sh.stage);
-  const typename M::Plan pl{counts, 0, -1, -1};
-  const uint32_t proj = sh_proj[lp];
   static_assert(M::OWNER_BITS == 4, "owner bits >> (4 - k) at R = 2^k");
   const int sh_pow2 = R == 1 ? 4 : R == 2 ? 3 : R == 4 ? 2 : R == 8 ? 1 : -1;
-  uint64_t c0 = 0, c1 = 0;            // the parent's records so far per owner, 6 bits each (owners 0-9, 10-14)
-  for (; mask; mask &= mask - 1) {
-    const int t = __ffs(mask) - 1;
-    int slot, j;
-    if (SWAR)
-      M::locate_cum(counts, t, slot, j);
-    else
-      M::locate(pl, t, slot, j);
+  for (uint32_t r0 = 0; r0 < total; r0 += CLAIM_TILE) {
+    const uint32_t r = r0 + tid;
+    const bool act = r < total;
+    uint32_t p = 0, t = 0, o = 0, m = 0;
     typename M::State x;
-    int who;
-    M::apply(s, slot, j, f, x, who);
-    // (R = 2^k: the owner from the successor's owner bits alone, no fold)
-    const uint32_t o = sh_pow2 >= 0 ? (M::owner_bits_succ(s, x, who, proj) >> sh_pow2)
-                                    : owner_of(M::template fingerprint_succ<1>(s, fold, x, who, proj), R);
-    uint32_t r;
-    if (o < 10) {
-      r = (uint32_t)(c0 >> (6 * o)) & 63u;
-      c0 += 1ull << (6 * o);
-    } else {
-      r = (uint32_t)(c1 >> (6 * (o - 10))) & 63u;
-      c1 += 1ull << (6 * (o - 10));
+    uint64_t key = 0;
+    if (act) {
+      uint32_t lo = 0, hi = CLAIM_TILE;                  // the last parent with rbase <= r
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rbase[mid] <= r) lo = mid; else hi = mid;
+      }
+      p = lo;
+      m = sh_rep[p];
+      uint32_t mm = m;
+      for (uint32_t k = r - rbase[p]; k > 0; --k) mm &= mm - 1;
+      t = (uint32_t)(__ffs(mm) - 1);
+      const typename M::State ps = load_state<M>(psrc, pbase0 + p);
+      const uint64_t pc = pcnt[p];
+      int slot, j;
+      if (SWAR) {
+        M::locate_cum(pc, (int)t, slot, j);
+      } else {
+        const typename M::Plan pl{pc, 0, -1, -1};
+        M::locate(pl, (int)t, slot, j);
+      }
+      int who;
+      M::apply(ps, slot, j, f, x, who);
+      const uint32_t proj = sh_proj[p];
+      o = sh_pow2 >= 0 ? (M::owner_bits_succ(ps, x, who, proj) >> sh_pow2)
+                       : owner_of(M::template fingerprint_succ<1>(ps, pfold[p], x, who, proj), R);
+      atomicOr(&onib[p * 4 + (t >> 3)], o << (4 * (t & 7)));
+      const uint64_t pg = pkey0 + p;                     // the parent's index in the frontier
+      key = ((uint64_t)sh.rank << 60) | ((TLC ? (uint64_t)sh.gpos[pg] : pg) << 16) | ((uint64_t)t << 8) |
+            (uint64_t)M::slot_action(ps, slot);
     }
-    const uint64_t pos = sb + tt[16 + o] + ((pre[(o >> 1) * CLAIM_TILE + lp] >> (16 * (o & 1))) & 0xffffu) + r;
-    store_record<M>(out, pos, x,
-                    ((uint64_t)sh.rank << 60) | ((TLC ? (uint64_t)sh.gpos[pbase] : pbase) << 16) |
-                        ((uint64_t)t << 8) | (uint64_t)M::slot_action(s, slot));
+    __syncthreads();
+    if (act) {
+      // the parent's records of owner o at lower positions
+      uint32_t below = 0;
+      const uint32_t lower = m & ((1u << t) - 1u);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t wq = onib[p * 4 + q] ^ (o * 0x11111111u);   // nibble 0 = owner o
+        const uint32_t lm = (lower >> (8 * q)) & 0xffu;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          below += (((lm >> i) & 1u) && ((wq >> (4 * i)) & 0xfu) == 0u) ? 1u : 0u;
+      }
+      const uint64_t pos = sb + tt[16 + o] + ((pre[(o >> 1) * CLAIM_TILE + p] >> (16 * (o & 1))) & 0xffffu) + below;
+      store_record<M>(out, pos, x, key);
+    }
   }
 }
 
@@ -1080,9 +1141,11 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
   __syncthreads();
   KC_CT(5);
   if (SH && sh.stage)
-    stage_records<M, NT, TLC>(sh, live, s, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
-                         sh_rep, sh_cnt, sh_proj, sh_fp, sh_key, tile,
-                         base + tile0 + (DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x), C);
+    // (the parents reloaded from the frontier, or from the states rebuilt above)
+    stage_records<M, NT, TLC>(sh, live, fold, counts, DEAL ? (unsigned)(counts >> 56) : (unsigned)threadIdx.x, f,
+                              sh_rep, sh_cnt, sh_proj, sh_fp, sh_key, tile,
+                              dfr ? reinterpret_cast<const typename M::State*>(df.out) : cur,
+                              dfr ? base + tile0 : tile0, base + tile0, C);
   KC_CT(6);
   if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
   if (live) newmask[i] = sh_cur[threadIdx.x];
