@@ -67,8 +67,10 @@ constexpr int NARROW_LT_BITS = 16;
 constexpr uint64_t NARROW_LT = 1ull << NARROW_LT_BITS;   // level-table entries
 constexpr uint64_t NARROW_CAND_MAX = NARROW_LT / 2;       // successors of a narrow level
 // levels enqueued per host sync (Model_1, same box: 8 -> 3.20 ms, 16 -> 3.00,
-// 32 -> 2.90; KC_NARROW_BATCH overrides it)
-constexpr int NARROW_BATCH = 32;
+// 32 -> 2.90; round 5, same box twice: 32 -> 2.91 / 3.21, 64 -> 2.83 / 2.84,
+// 128 -> 2.85 / 2.80, profiles/r05ab_narrow_batch.txt; KC_NARROW_BATCH
+// overrides it).  The launches enqueued past a run's end return at once.
+constexpr int NARROW_BATCH = 64;
 // k_nexpand lanes per parent: a narrow level has few waves (<= 1 per SIMD),
 // so its time is one lane's serial successor chain; NARROW_SUB lanes share a
 // parent, lane k taking successors k, k + NARROW_SUB, ...
