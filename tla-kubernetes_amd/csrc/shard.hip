@@ -799,6 +799,31 @@ __global__ void __launch_bounds__(256) k_tlc_perm(uint64_t nn, const uint32_t* _
   gpos_out[j] = gn;
 }
 
+// drop_last_expand: take a level's per-action generated counts back out
+// (what k_claim added: each parent's plan slot counts, by action), from the
+// level's states and the plans k_claim kept
+template <class M>
+__global__ void __launch_bounds__(256) k_undo_gen(const typename M::State* __restrict__ st,
+                                                  const unsigned long long* __restrict__ counts, uint64_t n,
+                                                  Counters* __restrict__ C) {
+  __shared__ unsigned int sh[A_COUNT];
+  if (threadIdx.x < A_COUNT) sh[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const typename M::State s = load_state<M>(st, i);
+    const unsigned long long c = counts[i];
+#pragma unroll
+    for (int slot = 0; slot < M::NSLOT; ++slot) {
+      const unsigned v = (unsigned)((c >> (6 * slot)) & 63);
+      if (v) atomicAdd(&sh[M::slot_action(s, slot)], v);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < A_COUNT && sh[threadIdx.x])
+    atomicAdd(&stripe(C).act_gen[threadIdx.x], 0ull - (unsigned long long)sh[threadIdx.x]);   // (mod 2^64)
+}
+
 template <class M>
 class ShardT final : public ShardBase {
   using State = typename M::State;
@@ -1066,16 +1091,11 @@ class ShardT final : public ShardBase {
       if (tlc_) df.prev_gpos = gpos_prev();
       cur_deferred_ = false;
       ++deferred_levels_;
-      if (!d_row) {
-        // the solo path stops on this level's deferred invariant after the
-        // expand has counted its successors, where the exact path stops
-        // before it: keep act_gen to undo them (drop_last_expand)
-        if (!d_gen_snap_) KC_HIP_TRY(hipMalloc(&d_gen_snap_, sizeof(d_ctr_->s[0].act_gen) * CTR_STRIPES));
-        KC_HIP_TRY(hipMemcpy2DAsync(d_gen_snap_, sizeof(d_ctr_->s[0].act_gen), d_ctr_->s[0].act_gen,
-                                    sizeof(CtrStripe), sizeof(d_ctr_->s[0].act_gen), CTR_STRIPES,
-                                    hipMemcpyDeviceToDevice, st_));
-        gen_snap_ok_ = true;
-      }
+      // (the solo path stops on this level's deferred invariant after the
+      // expand has counted its successors, where the exact path stops before
+      // it: drop_last_expand then subtracts them, from the rebuilt states
+      // and the plans this k_claim keeps)
+      gen_snap_ok_ = d_row == nullptr && df.counts_out != nullptr;
       if (defer_check_) {
         if (!d_dchk_) KC_HIP_TRY(hipMalloc(&d_dchk_, 32));
         const unsigned long long init[4] = {0ull, ~0ull, ~0ull, 0ull};
@@ -1821,8 +1841,9 @@ class ShardT final : public ShardBase {
   int drop_last_expand() override {
     if (!gen_snap_ok_) return 0;
     KC_HIP_TRY(hipSetDevice(cfg_.device));
-    KC_HIP_TRY(hipMemcpy2DAsync(d_ctr_->s[0].act_gen, sizeof(CtrStripe), d_gen_snap_, sizeof(d_ctr_->s[0].act_gen),
-                                sizeof(d_ctr_->s[0].act_gen), CTR_STRIPES, hipMemcpyDeviceToDevice, st_));
+    if (n_)
+      hipLaunchKernelGGL(k_undo_gen<M>, dim3((unsigned)((n_ + 255) / 256)), dim3(256), 0, st_, cur_, pc_cur_, n_, d_ctr_);
+    KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipStreamSynchronize(st_));
     gen_snap_ok_ = false;
     return 0;
@@ -2028,7 +2049,6 @@ class ShardT final : public ShardBase {
     if (h_snc_) (void)hipHostFree(h_snc_);
     if (sp_arena_) (void)hipFree(sp_arena_);
     if (d_spctr_) (void)hipFree(d_spctr_);
-    if (d_gen_snap_) (void)hipFree(d_gen_snap_);
     if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
@@ -2095,8 +2115,7 @@ class ShardT final : public ShardBase {
   const Rec* last_in_ = nullptr;     // the last insert's receive buffer
   uint64_t defer_err_ = ~0ull;       // expand_done: the rebuild's invariant key
   double succ_ratio_ = 5.0;          // successors per state, last counted (the estimates)
-  unsigned long long* d_gen_snap_ = nullptr;   // act_gen before a solo deferred expand (drop_last_expand)
-  bool gen_snap_ok_ = false;
+  bool gen_snap_ok_ = false;        // drop_last_expand can undo the last expand's act_gen
   uint64_t last_new_ = 0;            // the last insert's new states (drop_last_insert)
   uint64_t deferred_levels_ = 0, emit_retries_ = 0;
   bool defer_check_ = false;         // KC_DEFER_CHECK (diagnostic)
