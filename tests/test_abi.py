@@ -90,3 +90,11 @@ def test_struct_layouts_match_header(tmp_path):
         assert int(got[cname]) == C.sizeof(py), cname
         for f in py._fields_:
             assert int(got[f"{cname}.{f[0]}"]) == getattr(py, f[0]).offset, (cname, f[0])
+
+
+def test_model_config_carries_tlc_order():
+    # ModelConfig.tlc_order (round 5: TLC-ordered claims at R > 1) reaches
+    # the C struct; the default stays off
+    from kubecheck import ModelConfig
+    assert ModelConfig().to_c().tlc_order == 0
+    assert ModelConfig(tlc_order=True).to_c().tlc_order == 1
