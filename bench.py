@@ -57,6 +57,11 @@ def parse():
                     help="HIP events on every kernel (default: on the roofline kernel k_claim only;"
                          " events on all five per-level launches cost the NP=2 check ~6 ms)")
     ap.add_argument("--chunk", type=int, default=0, help="parents per expansion chunk (0 = default)")
+    ap.add_argument("--first-claim", action="store_true",
+                    help="the whole line in first-claim mode (TLC -workers N semantics: the first inserter owns a "
+                         "state; same counts and trace lengths, no settle passes)")
+    ap.add_argument("--no-first-claim-line", action="store_true",
+                    help="skip the secondary first-claim measurement of the single-GPU line")
     ap.add_argument("--frontier-hbm-mb", type=int, default=0,
                     help="frontier spill mode: keep the frontiers in a StateQueue with this HBM budget")
     ap.add_argument("--fp-count", type=float, default=1e10,
@@ -308,7 +313,7 @@ def bench_single(args, kw, desc):
     cfg = kubecheck.ModelConfig(**kw, keep_trace=True,
                                 timing=0 if args.no_timing else (1 if args.all_kernel_timing else 2),
                                 fpset_slots=1 << 20, chunk_states=args.chunk,
-                                frontier_hbm_bytes=args.frontier_hbm_mb << 20)
+                                frontier_hbm_bytes=args.frontier_hbm_mb << 20, first_claim=args.first_claim)
     mc = kubecheck.ModelChecker(cfg)
     cold_ms = None
     for w in range(args.warmup):
@@ -365,6 +370,9 @@ def bench_single(args, kw, desc):
                    "chunks": r.levels_chunks, "deferred_frontier_states": r.deferred_states,
                    "deferred_frontier_redone": r.defer_fallback, "narrow_levels": r.narrow_levels,
                    "cold_first_check_ms": cold_ms,
+                   "claims": ("first inserter (TLC -workers N semantics: same counts and trace lengths; "
+                              "the winning copy of a same-level duplicate is not deterministic)"
+                              if args.first_claim else "sequential-BFS minimum (TLC -workers 1 order)"),
                    "cold_first_check_note": "the first (warmup) check of a fresh engine, its ClaimSet grown by "
                                             "rehash from 2^20 slots; the timed checks reuse the grown table "
                                             "(cleared each check), like TLC's -fpmem pre-sizing"},
@@ -386,7 +394,35 @@ def bench_single(args, kw, desc):
             out["kernel_ms_per_step"]["narrow"] = round(narrow[0] / args.steps, 3)
             out["config"]["narrow_levels_per_step"] = narrow[2] // args.steps
     mc.close()
+    if not args.first_claim and not args.no_first_claim_line and not args.frontier_hbm_mb:
+        out["first_claim"] = first_claim_line(args, cfg, r)
     return out
+
+
+def first_claim_line(args, cfg, ref):
+    """The same check in first-claim mode (ModelConfig.first_claim),
+    timed the same way, beside the headline: TLC -workers N semantics, whose
+    counts and widths must equal the deterministic run's."""
+    import dataclasses
+    import torch
+    import kubecheck
+
+    mc = kubecheck.ModelChecker(dataclasses.replace(cfg, first_claim=True, timing=0))
+    for _ in range(args.warmup):
+        mc.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = mc.run()
+        if (r.distinct, r.generated, r.depth, r.level_width) != (ref.distinct, ref.generated, ref.depth,
+                                                                  ref.level_width):
+            raise RuntimeError("bench: first-claim mode changed the counts")
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    mc.close()
+    return {"value": round(r.distinct * args.steps / dt, 1), "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "note": "ModelConfig(first_claim=True): the first ClaimSet inserter owns a state, as in a TLC "
+                    "-workers N run; no settle passes; not the headline value"}
 
 
 def bench_fpset(args):

@@ -231,6 +231,14 @@ typedef struct {
    * frontier.  Counted levels only, with the deferred frontier; not with the
    * seen-set spill.  Ignored at world 1, where the order is TLC's anyway. */
   int tlc_order;
+  /* Single-GPU engine: 1 = the first inserter of a fingerprint owns it, as in
+   * a TLC -workers N run (KubeAPI___Model_1.launch:33): no settle passes.
+   * Counts, widths, per-action generated counts, error kinds and levels and
+   * trace lengths are unchanged; which same-level copy wins (its parent, the
+   * per-action distinct split, which of several equal-level errors is
+   * reported) is not deterministic.  In-HBM wide levels only (not with the
+   * seen-set spill); KC_FIRST_CLAIM=1 sets it too. */
+  int first_claim;
 } kc_model_config;
 
 typedef struct {

@@ -98,3 +98,5 @@ def test_model_config_carries_tlc_order():
     from kubecheck import ModelConfig
     assert ModelConfig().to_c().tlc_order == 0
     assert ModelConfig(tlc_order=True).to_c().tlc_order == 1
+    assert ModelConfig().to_c().first_claim == 0
+    assert ModelConfig(first_claim=True).to_c().first_claim == 1

@@ -373,3 +373,45 @@ def test_wide_level_state_set_identical(oracle, monkeypatch, defer):
     want = oracle.level_tuples(oracle.config(np_=2), 30)
     assert got.shape == want.shape == (35224, got.shape[1])
     assert np.array_equal(got, want)
+
+
+# --- first-claim mode (KC_FIRST_CLAIM=1, k_claim FIRST): the first inserter
+# of a fingerprint wins, as in a multi-worker TLC run; no settle passes.
+# Counts, generated per action, widths, error kinds, levels and trace lengths
+# are the exact path's; which copy of a same-level duplicate wins is not
+# deterministic, so per-action distinct counts only sum to the same total and
+# a trace is checked as a real behaviour from an Init state.
+def _valid_trace(oracle, cfg, trace):
+    init = {tuple(map(int, t)) for t in oracle.level_tuples(cfg, 1)}
+    assert tuple(trace[0]) in init
+    for a, b in zip(trace, trace[1:]):
+        succ, _ = oracle.successors(cfg, a)
+        assert any(list(map(int, x)) == b for _, x in succ)
+
+
+@pytest.mark.parametrize("env", [{}, {"KC_DEFER": "0"}, {"KC_DEFER_SLACK": "0.001"}])
+def test_first_claim_counts(model1, fixtures, monkeypatch, env):
+    monkeypatch.setenv("KC_FIRST_CLAIM", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = run(chunk_states=1 << 20)          # every level on the wide path
+    assert (r.distinct, r.generated, r.depth) == (model1.distinct, model1.generated, model1.depth)
+    assert r.level_width == model1.level_width and r.act_gen == model1.act_gen
+    assert sum(r.act_dist.values()) == sum(model1.act_dist.values())
+    assert r.complete and r.error is None
+    fx = fixtures["np2_40levels"]
+    r = run(np=2, max_levels=40)
+    assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+
+
+@pytest.mark.parametrize("key,kw,kind", [("nc2", dict(nc=2), "assertion"), ("variant2", dict(variant=2), "invariant"),
+                                         ("variant3", dict(variant=3), "assertion"),
+                                         ("variant4", dict(variant=4), "invariant")])
+def test_first_claim_errors(fixtures, oracle, monkeypatch, key, kw, kind):
+    monkeypatch.setenv("KC_FIRST_CLAIM", "1")
+    fx = fixtures[key]
+    r = run(chunk_states=1 << 20, **kw)
+    assert r.error == kind
+    assert (r.error_level, r.trace_len) == (fx.get("err_level", fx["trace_len"]), fx["trace_len"])
+    cfg = oracle.config(nc=kw.get("nc", 1), variant=kw.get("variant", 0))
+    _valid_trace(oracle, cfg, [list(map(int, t)) for t in r.trace])

@@ -179,6 +179,10 @@ class EngineT final : public EngineBase {
     tscan_ = spill_ || !(ts && ts[0] == '0');
     const char* fz = getenv("KC_FUSE_SCAN");
     fuse_scan_ = !(fz && fz[0] == '0');
+    // KC_FIRST_CLAIM=1: first-claim mode (k_claim FIRST) on the in-HBM wide
+    // path: the first inserter of a fingerprint wins, no settle passes
+    const char* fc = getenv("KC_FIRST_CLAIM");
+    first_claim_ = (cfg.first_claim || (fc && fc[0] == '1')) && tscan_ && !spill_;
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
@@ -474,9 +478,17 @@ class EngineT final : public EngineBase {
         const unsigned grid = (unsigned)((cn + 255) / 256);
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
         timed(KK_EXPAND, [&] {
-          hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
-                             start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                             abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_, df);
+          if (first_claim_) {
+            ShardArgs fa = claim_args_;
+            fa.ttot = ttot_;
+            hipLaunchKernelGGL((k_claim<M, 0, false, 0, false, true>), dim3(tiles), dim3(CLAIM_TILE), 0, st_,
+                               cur_ + start, cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
+                               abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, fa, df);
+          } else {
+            hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
+                               start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
+                               abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, claim_args_, df);
+          }
         });
         if (ablate_) {
           KC_TRY(grow_buffer(abl_mask_, abl_cap_, cn, false, st_));
@@ -507,9 +519,10 @@ class EngineT final : public EngineBase {
           });
         }
         // (a small chunk: the overflow list's pass B inside the tile scan's launch)
-        const bool fuse = tscan_ && fuse_scan_ && cn <= FUSE_OVF_SCAN_MAX;
-        timed(KK_RESOLVE,
-              [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr, fuse); });
+        const bool fuse = tscan_ && fuse_scan_ && cn <= FUSE_OVF_SCAN_MAX && !first_claim_;
+        if (!first_claim_)
+          timed(KK_RESOLVE,
+                [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr, fuse); });
         if (tscan_) {
           timed(KK_SCAN, [&] {
             if (fuse)
@@ -1836,6 +1849,7 @@ class EngineT final : public EngineBase {
       hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
                          cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
   }
+  bool first_claim_ = false;   // KC_FIRST_CLAIM=1: k_claim FIRST, no settle passes (multi-worker TLC semantics)
   bool fuse_scan_ = true;   // KC_FUSE_SCAN=0: small chunks keep the separate overflow pass B launch (A/B)
   int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;

@@ -355,6 +355,9 @@ struct ShardArgs {
   // TLC order (ClaimKeys): G of each parent of the level; records and claims
   // then carry G instead of the local parent index
   const uint32_t* gpos = nullptr;
+  // first-claim mode (k_claim FIRST; the engine, KC_FIRST_CLAIM): each tile's
+  // new-state count, the input of k_tile_scan (no settle passes run)
+  uint32_t* ttot = nullptr;
 };
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
 // workgroups resident together (~1,536: 6 per CU) work on tiles spread over
@@ -752,7 +755,14 @@ static __device__ unsigned long long g_ctrace[16];
 #else
 #define KC_CT(k) ((void)0)
 #endif
-template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false>
+// FIRST (the engine only): first-claim mode, TLC's -workers N semantics —
+// the copy whose CAS inserts a fingerprint is its new state, every other copy
+// (an earlier level's, or a later claimant's of this level) is not new; no
+// candidates, no settle passes, the tile's new-state count written here.
+// Counts, widths and trace lengths are the exact path's; which copy of a
+// same-level duplicate wins (its parent, its action's distinct count) is
+// not deterministic, as in a multi-worker TLC run.
+template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false, bool FIRST = false>
 __global__ void __launch_bounds__(CLAIM_TILE)
 __attribute__((amdgpu_waves_per_eu(SH ? KC_SH_WAVES : 6, SH ? KC_SH_WAVES : 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
@@ -1026,7 +1036,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         KC_DIAG_OUT(r);
         if (r == CL_NEW)
           atomicOr(&sh_cur[KC_LP], 1u << t);
-        else if (r == CL_CUR)
+        else if (r == CL_CUR && !FIRST)
           push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, (KC_LP << 5) | (unsigned)t, sh.ovf, C);
         else if (r == CL_FULL)
           atomicAdd(&C->overflow, 1ull);
@@ -1132,7 +1142,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       KC_DIAG_OUT(r);
       if (r == CL_NEW)
         atomicOr(&sh_cur[lp], 1u << t);
-      else if (r == CL_CUR)
+      else if (r == CL_CUR && !FIRST)
         push_candidate(&sh_rc, tile, rec_fp, rec_lk, fp, lk, sh.ovf, C);
       else if (r == CL_FULL)
         atomicAdd(&C->overflow, 1ull);
@@ -1147,8 +1157,17 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
                               dfr ? reinterpret_cast<const typename M::State*>(df.out) : cur,
                               dfr ? base + tile0 : tile0, base + tile0, C);
   KC_CT(6);
-  if (threadIdx.x == 0) rcount[tile] = sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
+  if (threadIdx.x == 0) rcount[tile] = FIRST ? 0u : sh_rc < (unsigned)CLAIM_RCAP ? sh_rc : (unsigned)CLAIM_RCAP;
   if (live) newmask[i] = sh_cur[threadIdx.x];
+  if (FIRST) {
+    // the tile's new states (sh_cur is final: the barrier after the claims)
+    unsigned int c = live ? (unsigned)__builtin_popcount(sh_cur[threadIdx.x]) : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += (unsigned)__shfl_xor((int)c, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&sh_rc, c);   // (sh_rc is 0: no candidates)
+    __syncthreads();
+    if (threadIdx.x == 0) sh.ttot[tile] = sh_rc;
+  }
   if (SH && live) {
     sh.repmask[i] = sh_rep[threadIdx.x];
     for (uint32_t o = 0; o < sh.world; ++o)

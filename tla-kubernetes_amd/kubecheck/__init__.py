@@ -69,6 +69,10 @@ class ModelConfig:
     # sharded runs at R > 1: claims in sequential-BFS order, so errors and
     # traces equal TLC -workers 1's (a per-level all-reduce and sort)
     tlc_order: bool = False
+    # single-GPU engine: the first inserter of a state owns it (TLC -workers N
+    # semantics: same counts and trace lengths, no settle passes; the winning
+    # copy of a same-level duplicate is not deterministic)
+    first_claim: bool = False
 
     def to_c(self) -> KcModelConfig:
         c = KcModelConfig()

@@ -37,6 +37,7 @@ class KcModelConfig(C.Structure):
         ("frontier_segment_states", C.c_uint64), ("spill_dir", C.c_char_p), ("trace_host", C.c_int),
         ("seen_hbm_bytes", C.c_uint64), ("seen_host_bytes", C.c_uint64),
         ("tlc_order", C.c_int),
+        ("first_claim", C.c_int),
     ]
 
 
