@@ -206,7 +206,9 @@ class EngineT final : public EngineBase {
     const char* dp = getenv("KC_DEFER_PC");
     pc_pass_ = !(dp && dp[0] == '0');
     const char* dr = getenv("KC_DEFER_REDO");      // KC_DEFER_REDO=0: an anomaly redoes the run from Init
-    redo_on_ = !(dr && dr[0] == '0');
+    // (first-claim mode writes no claim words, so no level's inserts can be
+    // dropped: a deferred-frontier anomaly redoes the run from Init)
+    redo_on_ = !(dr && dr[0] == '0') && !first_claim_;
     const char* dd = getenv("KC_DEFER_DIRECT");    // KC_DEFER_DIRECT=0: invariant anomalies are redone too (A/B)
     defer_direct_ = !(dd && dd[0] == '0');
     const char* ds = getenv("KC_DEFER_SLACK");

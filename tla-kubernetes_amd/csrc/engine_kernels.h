@@ -1032,7 +1032,9 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         }
         ++probes;
         const uint64_t pidx = base + tile0 + KC_LP;
-        const int r = claimset_claim_store(cs, nbuckets, fp, make_claim(level, okey(pidx, (uint64_t)t)), level);
+        const uint64_t b = bucket_of(fp, nbuckets);
+        const int r = FIRST ? claimset_insert_from(cs, nbuckets, fp, b, cs[b].fp)
+                            : claimset_claim_store(cs, nbuckets, fp, make_claim(level, okey(pidx, (uint64_t)t)), level);
         KC_DIAG_OUT(r);
         if (r == CL_NEW)
           atomicOr(&sh_cur[KC_LP], 1u << t);
@@ -1128,8 +1130,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       int r;
       const uint64_t claim = make_claim(level, okey(pidx, t));
       if (cq[q] == 0ull) {                        // this lane's CAS inserted fp (fingerprints are never ~0)
-        __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!FIRST)
+          __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         r = CL_NEW;
+      } else if (FIRST) {
+        r = claimset_insert_from(cs, nbuckets, fp, iq[q], cq[q] != ~0ull ? cq[q] : eq[q].x);
       } else {
         ulonglong2 e = eq[q];
         if (cq[q] != ~0ull) e = make_ulonglong2(cq[q], 0ull);   // another claimant's fp took the slot first

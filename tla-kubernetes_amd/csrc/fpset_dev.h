@@ -223,6 +223,23 @@ __device__ __forceinline__ int claimset_claim_store(ClaimEntry* __restrict__ t, 
   return claimset_claim_store_from(t, nslots, fp, claim, level, i, claimset_first(t, i));
 }
 
+// First-claim mode (k_claim FIRST): the CAS that inserts fp is the claim and
+// no claim word is written.  From slot i, whose fp word the caller loaded as
+// f.  CL_NEW: this call inserted fp; CL_OLD: fp is present; CL_FULL.
+__device__ __forceinline__ int claimset_insert_from(ClaimEntry* __restrict__ t, uint64_t nslots, uint64_t fp,
+                                                    uint64_t i, unsigned long long f) {
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    if (probe) f = t[i].fp;
+    if (f == 0ull) {
+      f = atomicCAS(&t[i].fp, 0ull, (unsigned long long)fp);
+      if (f == 0ull) return CL_NEW;
+    }
+    if (f == fp) return CL_OLD;
+    i = (i + 1 == nslots) ? 0 : i + 1;
+  }
+  return CL_FULL;
+}
+
 // Settle pass A of a CL_CUR candidate: fold its claim into the slot.
 // Returns the ~claim the slot held before (0 if fp is absent, which the
 // protocol never produces).
