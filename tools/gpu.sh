@@ -5,8 +5,9 @@
 # so that the first failure ends the call.
 #
 #   gpurun -- bash tools/gpu.sh tests  <tag> [pytest args...]   GPU tests (default: all of -m gpu)
-#   gpurun -- bash tools/gpu.sh round  <tag>                    part A + part B, then the NP=2 bench
-#                                                               line that reads part A's PMC summary
+#   gpurun -- bash tools/gpu.sh round  <tag>                    part A, the NP=2 bench line that reads
+#                                                               part A's PMC summary, then part B
+#                                                               (round1: without part B)
 #   gpurun -- bash tools/gpu.sh parta  <tag>                    tests, smoke, bench lines (Model_1,
 #                                                               NP=2, FPSet), NP=2 / FPSet kernel traces
 #                                                               + FETCH_SIZE / WRITE_SIZE passes
@@ -61,7 +62,7 @@ tests)
     || { echo TESTS_FAIL; grep -E "FAIL|Error" $O/tests.log | head -20; tail -30 $O/tests.log; exit 1; }
   tail -3 $O/tests.log
   ;;
-round)
+round|round1)
   bash tools/gpu.sh parta $TAG || exit 1
   cp $O/summary.json $R/profiles/${TAG}_np2_rocprof_summary.json
   cp $O/fpset_summary.json $R/profiles/${TAG}_fpset_rocprof_summary.json
@@ -69,7 +70,7 @@ round)
   timeout -k 10 600 python -u bench.py > $O/bench_np2_pmc.json 2> $O/bench_np2_pmc.err \
     || { echo BENCH2_FAIL; tail -20 $O/bench_np2_pmc.err; exit 1; }
   cat $O/bench_np2_pmc.json
-  bash tools/gpu.sh partb $TAG || exit 1
+  [ "$CMD" = round1 ] || bash tools/gpu.sh partb $TAG || exit 1
   ;;
 parta)
   step tests
@@ -86,7 +87,7 @@ parta)
   step bench_np2
   timeout -k 10 600 python -u bench.py > $O/bench_np2.json 2> $O/bench_np2.err || { echo BENCH2_FAIL; tail -20 $O/bench_np2.err; exit 1; }
   cat $O/bench_np2.json
-  pmc "" $O/summary.json python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-timing || exit 1
+  pmc "" $O/summary.json python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-first-claim-line || exit 1
   # FPSet stress (BASELINE config 4): the bench line at 1e10 fps, PMC passes at 2^30
   step bench_fpset
   timeout -k 10 300 python -u bench.py --workload fpset --steps 2 --warmup 1 > $O/bench_fpset.json 2> $O/bench_fpset.err \
@@ -95,7 +96,8 @@ parta)
   pmc f $O/fpset_summary.json python3 $R/bench.py --workload fpset --fp-count 1073741824 --steps 1 --warmup 0 || exit 1
   ;;
 partb)
-  pmc n3 $O/np3_summary.json python3 $R/bench.py --workload np3_52 --steps 1 --warmup 1 --no-cpu-baseline --no-timing || exit 1
+  pmc n3 $O/np3_summary.json python3 $R/bench.py --workload np3_52 --steps 1 --warmup 1 --no-cpu-baseline --no-timing \
+    --no-first-claim-line || exit 1
   # (the box's copy of profiles/: the bench line below finds this build's PMC)
   cp $O/np3_summary.json $R/profiles/${TAG}_np3_52_rocprof_summary.json
   step bench_np3
