@@ -236,8 +236,9 @@ typedef struct {
    * Counts, widths, per-action generated counts, error kinds and levels and
    * trace lengths are unchanged; which same-level copy wins (its parent, the
    * per-action distinct split, which of several equal-level errors is
-   * reported) is not deterministic.  In-HBM wide levels only (not with the
-   * seen-set spill); KC_FIRST_CLAIM=1 sets it too. */
+   * reported) is not deterministic.  In-HBM wide levels only (ignored with
+   * the seen-set spill or a frontier HBM budget); KC_FIRST_CLAIM=1 sets it
+   * too. */
   int first_claim;
 } kc_model_config;
 

@@ -182,7 +182,7 @@ class EngineT final : public EngineBase {
     // KC_FIRST_CLAIM=1: first-claim mode (k_claim FIRST) on the in-HBM wide
     // path: the first inserter of a fingerprint wins, no settle passes
     const char* fc = getenv("KC_FIRST_CLAIM");
-    first_claim_ = (cfg.first_claim || (fc && fc[0] == '1')) && tscan_ && !spill_;
+    first_claim_ = (cfg.first_claim || (fc && fc[0] == '1')) && tscan_ && !spill_ && !queued_;
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
