@@ -70,6 +70,9 @@ def parse():
                     help="fpset workload: table load after the inserts")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded (multi-GPU) stages even at N=1 (started under torch.distributed.run)")
+    ap.add_argument("--deterministic-shards", action="store_true",
+                    help="N>1 / --sharded: (rank, parent)-ordered minimum claims with their settle passes instead of "
+                         "the sharded loop's default first-claim mode")
     ap.add_argument("--launcher-check", action="store_true",
                     help="only start the ranks (gloo, no GPU) and report what each saw: a CPU test of "
                          "the --gpus N self-launch")
@@ -150,36 +153,64 @@ def roofline_bfs(times, res, S):
     }
 
 
-def op_rate_roofline(kclaim_ms: float, probes: int, inserts: int) -> dict:
-    """The roofline that bounds k_claim: its random
-    memory OPERATIONS, each priced at the rate it runs at alone on this GPU
-    (tools/microbench/pmc_calib.hip, profiles/r02b_pmc_calibration.json:
-    random 16-B load, random 64-bit CAS, random agent-scope 8-B store over a
-    32 GiB table).  Per check: every ClaimSet probe is one first-slot load;
-    every inserted state one CAS and one claim store (the STORE-claim
-    protocol).  `serial_ms` is what those operations take one
-    kind after another at the isolated rates; frac = serial_ms / kernel time
-    (> 1: the kernel overlaps the three kinds beyond their isolated sum)."""
-    cal = {"probe": 44.93e9, "cas": 17.11e9, "store": 22.21e9}
-    try:
-        with open(os.path.join(ROOT, "profiles", "r02b_pmc_calibration.json")) as fh:
-            sh = json.load(fh)["shapes"]
-        cal = {"probe": sh["c_rand_load16"]["G_per_s"] * 1e9, "cas": sh["c_rand_cas_new"]["G_per_s"] * 1e9,
-               "store": sh["c_rand_store_agent"]["G_per_s"] * 1e9}
-    except (OSError, ValueError, KeyError):
-        pass
+def claim_ceiling():
+    """The newest committed mixed-operation ceiling of k_claim's claim protocol
+    (tools/microbench/claim_ceiling.hip -> profiles/<round>_claim_ceiling.json)."""
+    import glob
+
+    def run_order(f):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(f))
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_claim_ceiling.json")), key=run_order, reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            d["ceiling_ms"]["deterministic"], d["per_check"]["claims"]
+            return d, os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
+def op_rate_roofline(kclaim_ms: float, probes: int, inserts: int, checks: int, first: bool) -> dict:
+    """The roofline that bounds k_claim: its random memory
+    OPERATIONS — per check every ClaimSet claim is one first-slot 16-B load,
+    every new state one inserting CAS and, in the deterministic protocol, one
+    agent-scope claim store — measured TOGETHER, in k_claim's own ratio and
+    with the product's claimset_* code on a 2^32-slot (64 GiB) table like the
+    NP=2 ClaimSet, by tools/microbench/claim_ceiling.hip with nothing else
+    running (profiles/*_claim_ceiling.json).  ceiling_ms = that time scaled
+    to this run's claims; frac = ceiling_ms / k_claim's time (<= 1: the share
+    of the kernel's time its claims would need at the memory system's mixed
+    random-operation rate; 1 - frac is what overlapping them with the
+    successor computation has not hidden).  The per-kind fractions use the
+    same table's isolated rates."""
+    cal, src = claim_ceiling()
     t = kclaim_ms * 1e-3
-    serial = probes / cal["probe"] + inserts / cal["cas"] + inserts / cal["store"]
-    return {"bound": "random-op rate", "kernel": "k_claim", "kernel_ms": round(kclaim_ms, 3),
-            "probes": int(probes), "probes_per_s": round(probes / t, 1) if t else 0.0,
-            "probe_peak_per_s": cal["probe"], "probe_frac": round(probes / t / cal["probe"], 4) if t else 0.0,
-            "cas": int(inserts), "cas_per_s": round(inserts / t, 1) if t else 0.0, "cas_peak_per_s": cal["cas"],
-            "cas_frac": round(inserts / t / cal["cas"], 4) if t else 0.0,
-            "claim_stores": int(inserts), "stores_per_s": round(inserts / t, 1) if t else 0.0,
-            "store_peak_per_s": cal["store"], "store_frac": round(inserts / t / cal["store"], 4) if t else 0.0,
-            "serial_ms": round(serial * 1e3, 3), "frac": round(serial / t, 4) if t else 0.0,
-            "source": "profiles/r02b_pmc_calibration.json (isolated rates, 32 GiB table); inserts = the "
-                      "check's new states (each one CAS + one claim store), probes = kc_result.fpset_probes"}
+    out = {"bound": "random-op rate (mixed, measured)", "kernel": "k_claim", "kernel_ms": round(kclaim_ms, 3),
+           "claims": "first inserter" if first else "deterministic (claim store)",
+           "probes": int(probes), "probes_per_s": round(probes / t, 1) if t else 0.0,
+           "cas": int(inserts), "cas_per_s": round(inserts / t, 1) if t else 0.0,
+           "claim_stores": 0 if first else int(inserts)}
+    if cal is None or not t:
+        out["frac"] = None
+        out["source"] = "no committed claim-ceiling profile"
+        return out
+    mode = "first" if first else "deterministic"
+    per_check = cal["ceiling_ms"][mode]
+    ceil_ms = per_check * (probes / max(checks, 1)) / cal["per_check"]["claims"] * checks
+    iso = cal["isolated_64GiB_G_per_s"]
+    out.update({
+        "ceiling_ms": round(ceil_ms, 3), "frac": round(ceil_ms / kclaim_ms, 4),
+        "ceiling_claims_per_s": round(cal["per_check"]["claims"] / (per_check * 1e-3), 1),
+        "probe_frac_isolated": round(probes / t / (iso["first_slot_load16"] * 1e9), 4),
+        "cas_frac_isolated": round(inserts / t / (iso["cas_insert"] * 1e9), 4),
+        "store_frac_isolated": 0.0 if first else round(inserts / t / (iso["agent_store8"] * 1e9), 4),
+        "source": f"{src}: {mode} claims at {per_check} ms per NP=2 check ({cal['per_check']['claims']} claims, "
+                  f"{cal['per_check']['units_new_states']} inserts), scaled by this run's claims per check; "
+                  "isolated rates on the same 64 GiB table"})
+    return out
 
 
 def pmc_traffic(workload: str, kernel: str, stream_read_bytes: float = 0.0):
@@ -370,9 +401,12 @@ def bench_single(args, kw, desc):
                    "chunks": r.levels_chunks, "deferred_frontier_states": r.deferred_states,
                    "deferred_frontier_redone": r.defer_fallback, "narrow_levels": r.narrow_levels,
                    "cold_first_check_ms": cold_ms,
+                   # (the mode the engine reports it ran, kc_result.claim_mode: a flag the engine
+                   # cannot honour, e.g. with a frontier HBM budget, does not relabel the line)
                    "claims": ("first inserter (TLC -workers N semantics: same counts and trace lengths; "
                               "the winning copy of a same-level duplicate is not deterministic)"
-                              if args.first_claim else "sequential-BFS minimum (TLC -workers 1 order)"),
+                              if r.claim_mode == "first" else "sequential-BFS minimum (TLC -workers 1 order)"),
+                   "claim_mode": r.claim_mode,
                    "cold_first_check_note": "the first (warmup) check of a fresh engine, its ClaimSet grown by "
                                             "rehash from 2^20 slots; the timed checks reuse the grown table "
                                             "(cleared each check), like TLC's -fpmem pre-sizing"},
@@ -387,7 +421,8 @@ def bench_single(args, kw, desc):
         stream = acc["parents"] * S / max(times["expand"][1], 1) if roof["kernel"] == "k_claim" else 0.0
         set_traffic(roof, *pmc_traffic(args.workload, roof["kernel"], stream))
         if roof["kernel"] == "k_claim":
-            roof["op_rate"] = op_rate_roofline(times["expand"][0], acc["probes"], acc["new"])
+            roof["op_rate"] = op_rate_roofline(times["expand"][0], acc["probes"], acc["new"], args.steps,
+                                               r.claim_mode == "first")
         out["roofline"] = roof
         out["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in times.items() if v[0] > 0}
         if narrow[1]:
@@ -421,6 +456,7 @@ def first_claim_line(args, cfg, ref):
     dt = time.perf_counter() - t0
     mc.close()
     return {"value": round(r.distinct * args.steps / dt, 1), "ms_per_step": round(dt * 1e3 / args.steps, 3),
+            "claim_mode": r.claim_mode, "defer_fallback": r.defer_fallback,
             "note": "ModelConfig(first_claim=True): the first ClaimSet inserter owns a state, as in a TLC "
                     "-workers N run; no settle passes; not the headline value"}
 

@@ -231,14 +231,16 @@ typedef struct {
    * frontier.  Counted levels only, with the deferred frontier; not with the
    * seen-set spill.  Ignored at world 1, where the order is TLC's anyway. */
   int tlc_order;
-  /* Single-GPU engine: 1 = the first inserter of a fingerprint owns it, as in
-   * a TLC -workers N run (KubeAPI___Model_1.launch:33): no settle passes.
-   * Counts, widths, per-action generated counts, error kinds and levels and
-   * trace lengths are unchanged; which same-level copy wins (its parent, the
-   * per-action distinct split, which of several equal-level errors is
-   * reported) is not deterministic.  In-HBM wide levels only (ignored with
-   * the seen-set spill or a frontier HBM budget); KC_FIRST_CLAIM=1 sets it
-   * too. */
+  /* 1 = the first inserter of a fingerprint owns it, as in a TLC -workers N
+   * run (KubeAPI___Model_1.launch:33): no settle passes.  Counts, widths,
+   * per-action generated counts, error kinds and levels and trace lengths are
+   * unchanged; which same-level copy wins (its parent, the per-action
+   * distinct split, which of several equal-level errors is reported) is not
+   * deterministic.  Single-GPU engine: in-HBM wide levels only (ignored with
+   * the seen-set spill or a frontier HBM budget; KC_FIRST_CLAIM=1 sets it
+   * too).  Sharded loop (kc_shard_*, kc_group_*): every counted level, at any
+   * world; kc_shard_create fails with -EINVAL together with tlc_order or the
+   * seen-set spill.  kc_result.claim_mode reports what ran. */
   int first_claim;
 } kc_model_config;
 
@@ -298,6 +300,11 @@ typedef struct {
   /* levels run by a device-driven narrow path (single-GPU engine: k_nfinish;
    * sharded loop: the fixed-slot exchange levels, shard_narrow.h) */
   uint64_t narrow_levels;
+  /* the claim protocol the wide (counted) levels ran with: 0 = the
+   * sequential-BFS minimum key (TLC -workers 1's first discoverer on one GPU;
+   * (rank, parent) order on shards), 1 = first inserter (cfg.first_claim),
+   * 2 = TLC order on shards (cfg.tlc_order at world > 1) */
+  int claim_mode;
 } kc_result;
 
 typedef struct kc_engine kc_engine;

@@ -399,19 +399,31 @@ def test_first_claim_counts(model1, fixtures, monkeypatch, env):
     assert r.level_width == model1.level_width and r.act_gen == model1.act_gen
     assert sum(r.act_dist.values()) == sum(model1.act_dist.values())
     assert r.complete and r.error is None
+    assert r.claim_mode == "first"
     fx = fixtures["np2_40levels"]
     r = run(np=2, max_levels=40)
     assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+    # (the mode is decided after the deferred frontier forces the tile scan
+    # on, so KC_TSCAN=0 does not drop it: ADVICE r5)
+    monkeypatch.setenv("KC_TSCAN", "0")
+    r = run(chunk_states=1 << 20)
+    assert r.claim_mode == ("minimum" if env.get("KC_DEFER") == "0" else "first")
+    assert r.level_width == model1.level_width
 
 
 @pytest.mark.parametrize("key,kw,kind", [("nc2", dict(nc=2), "assertion"), ("variant2", dict(variant=2), "invariant"),
                                          ("variant3", dict(variant=3), "assertion"),
-                                         ("variant4", dict(variant=4), "invariant")])
+                                         ("variant4", dict(variant=4), "invariant"),
+                                         ("ns0", dict(ns=0), "deadlock")])
 def test_first_claim_errors(fixtures, oracle, monkeypatch, key, kw, kind):
     monkeypatch.setenv("KC_FIRST_CLAIM", "1")
     fx = fixtures[key]
     r = run(chunk_states=1 << 20, **kw)
     assert r.error == kind
     assert (r.error_level, r.trace_len) == (fx.get("err_level", fx["trace_len"]), fx["trace_len"])
-    cfg = oracle.config(nc=kw.get("nc", 1), variant=kw.get("variant", 0))
+    cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1), variant=kw.get("variant", 0))
     _valid_trace(oracle, cfg, [list(map(int, t)) for t in r.trace])
+    # found on a deferred level and reported there: an Assert or deadlock key
+    # from the states k_claim rebuilt, an invariant violation among them as
+    # the level before's (no redo of the whole run from Init)
+    assert r.claim_mode == "first" and not r.defer_fallback, (r.defer_fallback, r.defer_redo_level)

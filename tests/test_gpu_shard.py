@@ -453,3 +453,82 @@ def test_native_np2_prefix_switches(fixtures, monkeypatch):
     for name, r in runs.items():
         assert r["act_dist"] == runs["sdefer0"]["act_dist"], name
         assert r["records_sent"] == runs["sdefer0"]["records_sent"], name
+
+
+# --- round 6: first-claim mode on the sharded loop (ModelConfig.first_claim;
+# VERDICT r5 item 1): a state belongs to the copy whose ClaimSet CAS inserts
+# it, as in a TLC -workers N run — no candidates, no settle passes, the
+# records' claims CAS-only.  Counts, widths, depth, per-action generated
+# counts, error kinds, levels and trace lengths are the deterministic mode's;
+# which same-level copy wins is not (so per-action distinct counts and the
+# trace states are checked for consistency, not equality).
+FIRST_CASES = TLC_CASES + (("variant5", dict(variant=5), "invariant"),)
+
+
+def _first_trace_ok(oracle, kw, trace):
+    cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1), variant=kw.get("variant", 0),
+                        invariants=kw.get("invariants", 3))
+    init = {tuple(map(int, t)) for t in oracle.level_tuples(cfg, 1)}
+    assert tuple(trace[0]) in init
+    for a, b in zip(trace, trace[1:]):
+        succ, _ = oracle.successors(cfg, a)
+        assert any(list(map(int, x)) == b for _, x in succ)
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 8])
+@pytest.mark.parametrize("snarrow", ["1", "0"])
+def test_native_first_claim(fixtures, oracle, monkeypatch, R, snarrow):
+    # snarrow 0: every level on the counted path (every claim first-claim)
+    monkeypatch.setenv("KC_SNARROW", snarrow)
+    fx = fixtures["model1"]
+    r = native(R, first_claim=True)
+    assert r["claim_mode"] == "first"
+    assert r["complete"] and r["error"] is None and r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["act_gen"] == fx["act_gen"]
+    assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+    for key, kw, kind in FIRST_CASES:
+        fk = fixtures[key]
+        r = native(R, first_claim=True, **kw)
+        assert r["error"] == kind, key
+        assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), key
+        if kind == "assertion":
+            assert r["error_action"] == fk["err_action"], key
+        _first_trace_ok(oracle, kw, r["trace"])
+
+
+def test_native_first_claim_np2(fixtures):
+    # NP=2: the 40-level prefix at 4 emulated ranks, and the seeded race's
+    # NoLostUpdate violation at depth 25 (wide, deferred levels) at 3
+    fx = fixtures["np2_40levels"]
+    r = native(4, np=2, max_levels=40, first_claim=True)
+    assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"] and not r["complete"]
+    assert r["distinct"] == fx["distinct"]
+    fk = fixtures["np2_variant1_lost_update"]
+    r = native(3, np=2, variant=1, invariants=7, first_claim=True)
+    assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate"
+    assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"])
+
+
+def test_native_enlarged_full_emulated_first_claim(fixtures):
+    # the whole NP=2 model at 8 emulated ranks in first-claim mode (the
+    # deterministic mode's run is test_native_enlarged_full_emulated), exact
+    # against the golden
+    fx = fixtures["np2_full"]
+    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False, first_claim=True), emulate=8)
+    try:
+        r = mc.run()
+    finally:
+        mc.close()
+    assert r["claim_mode"] == "first"
+    assert r["complete"] and r["error"] is None
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"]
+
+
+def test_native_first_claim_rejects_tlc_order():
+    # first-claim and TLC order are two different claim orders
+    from kubecheck import KubecheckError
+    with pytest.raises(KubecheckError) as e:
+        native(2, first_claim=True, tlc_order=True)
+    assert "first_claim" in str(e.value) and e.value.code == -22

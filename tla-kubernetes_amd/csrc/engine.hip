@@ -179,10 +179,6 @@ class EngineT final : public EngineBase {
     tscan_ = spill_ || !(ts && ts[0] == '0');
     const char* fz = getenv("KC_FUSE_SCAN");
     fuse_scan_ = !(fz && fz[0] == '0');
-    // KC_FIRST_CLAIM=1: first-claim mode (k_claim FIRST) on the in-HBM wide
-    // path: the first inserter of a fingerprint wins, no settle passes
-    const char* fc = getenv("KC_FIRST_CLAIM");
-    first_claim_ = (cfg.first_claim || (fc && fc[0] == '1')) && tscan_ && !spill_ && !queued_;
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
@@ -206,14 +202,21 @@ class EngineT final : public EngineBase {
     const char* dp = getenv("KC_DEFER_PC");
     pc_pass_ = !(dp && dp[0] == '0');
     const char* dr = getenv("KC_DEFER_REDO");      // KC_DEFER_REDO=0: an anomaly redoes the run from Init
-    // (first-claim mode writes no claim words, so no level's inserts can be
-    // dropped: a deferred-frontier anomaly redoes the run from Init)
-    redo_on_ = !(dr && dr[0] == '0') && !first_claim_;
+    redo_on_ = !(dr && dr[0] == '0');
     const char* dd = getenv("KC_DEFER_DIRECT");    // KC_DEFER_DIRECT=0: invariant anomalies are redone too (A/B)
     defer_direct_ = !(dd && dd[0] == '0');
     const char* ds = getenv("KC_DEFER_SLACK");
     if (ds && atof(ds) > 0) defer_slack_ = atof(ds);
     if (defer_) tscan_ = true;    // the link emit takes the tile offsets
+    // KC_FIRST_CLAIM=1: first-claim mode (k_claim FIRST) on the in-HBM wide
+    // path: the first inserter of a fingerprint wins, no settle passes (decided
+    // after the tile scan is, which it needs; kc_result.claim_mode reports it)
+    const char* fc = getenv("KC_FIRST_CLAIM");
+    first_claim_ = (cfg.first_claim || (fc && fc[0] == '1')) && tscan_ && !spill_ && !queued_;
+    // (first-claim mode writes no claim words, so no level's inserts can be
+    // dropped: a deferred-frontier capacity anomaly redoes the run from Init;
+    // an Assert or deadlock key is reported directly, as on the exact path)
+    if (first_claim_) redo_on_ = false;
   }
   ~EngineT() override { release(); }
 
@@ -267,6 +270,7 @@ class EngineT final : public EngineBase {
     KC_HIP_TRY(hipSetDevice(cfg_.device));
     memset(res, 0, sizeof *res);
     res->err_action = res->err_self = res->err_invariant = -1;
+    res->claim_mode = first_claim_ ? 1 : 0;
     trace_.clear();
     narrow_probes_ = 0;
     for (auto& t : ktime_ms_) t = 0;
@@ -603,7 +607,11 @@ class EngineT final : public EngineBase {
       const Counters& c = *h_ctr_;
       // a deferred level with anything to report: redo exactly, from the level
       // the anomaly belongs to
-      if (dfr && (c.overflow || c.batch_used || c.err_key != ~0ull || c.defer_flags)) {
+      // (first-claim mode: an Assert or deadlock key alone is reported below,
+      // from the states this k_claim rebuilt into cur_, exactly as the
+      // materialising path's k_claim of this level reports it — no redo)
+      const bool key_only = first_claim_ && !c.overflow && !c.batch_used && !c.defer_flags;
+      if (dfr && !key_only && (c.overflow || c.batch_used || c.err_key != ~0ull || c.defer_flags)) {
         // an invariant violation among the states this level rebuilt is
         // the previous level's error (its emit would have found it); the
         // rest (Assert / deadlock keys of this level's parents, a capacity
@@ -1263,8 +1271,12 @@ class EngineT final : public EngineBase {
     KC_TRY(counter_snap(L));
     hipLaunchKernelGGL(k_counters_restore, dim3(1), dim3(64), 0, st_, d_ctr_, d_snap_[(L - 1) % 3].s,
                        d_snap_[L % 3].s);
-    hipLaunchKernelGGL(k_claimset_drop, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t, cs_.nslots,
-                       (uint32_t)L + 1);
+    // (first-claim mode writes no claim words: there is no level to drop by,
+    // and a drop keyed on the empty word would clear every wide-level entry;
+    // the run ends here and the next one clears the table)
+    if (!first_claim_)
+      hipLaunchKernelGGL(k_claimset_drop, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_, cs_.t, cs_.nslots,
+                         (uint32_t)L + 1);
     KC_HIP_TRY(hipGetLastError());
     KC_HIP_TRY(hipStreamSynchronize(st_));
     std::vector<State> path;

@@ -414,6 +414,8 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
       if (o == 0ull) {
         cs[ix].nclaim = ~make_claim(succ_level, (i << 8) | (uint64_t)t);
         mine |= 1u << t;
+      } else if (o != fp) {
+        atomicAdd(&C->overflow, 1ull);               // a full table: fail loudly (as shard_narrow.h)
       }
     }
   }

@@ -269,6 +269,39 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
   if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&stripe(C).probes, probes);
 }
 
+// First-claim mode (cfg.first_claim; ShardT::first_): a received record is
+// new iff its CAS inserts the fingerprint — no claim word, no candidates, no
+// settle passes (a copy this rank's own k_claim inserted at expand, or an
+// earlier record's, makes it old).  isnew[i] directly, and each block's
+// winners into rtot[blk] (the record half of k_win_scan's input).
+template <class M>
+__global__ void __launch_bounds__(256)
+k_rec_claim_first(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs, uint64_t nslots,
+                  uint32_t* __restrict__ isnew, uint32_t* __restrict__ rtot, Counters* __restrict__ C) {
+  __shared__ unsigned int sh_rw[4];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t w = 0;
+  if (i < n) {
+    typename M::State x;
+    uint64_t key;
+    load_record<M>(in, i, x, key);
+    const uint64_t fp = M::template fingerprint<1>(x);
+    const uint64_t b = bucket_of(fp, nslots);
+    const int r = claimset_insert_from(cs, nslots, fp, b, cs[b].fp);
+    if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
+    w = r == CL_NEW ? 1u : 0u;
+    isnew[i] = w;
+  }
+  const unsigned long long bw = __ballot(w != 0);
+  const unsigned long long bp = __ballot(i < n);
+  if ((threadIdx.x & 63) == 0) {
+    sh_rw[threadIdx.x >> 6] = (unsigned)__popcll(bw);
+    if (bp) atomicAdd(&stripe(C).probes, (unsigned long long)__popcll(bp));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) rtot[blockIdx.x] = sh_rw[0] + sh_rw[1] + sh_rw[2] + sh_rw[3];
+}
+
 // PASS 0: candidates fold their claims (a displaced local claim loses its
 // newmask bit, the displacer is flagged); PASS 1: inserters and displacers
 // win iff the stored claim is still theirs.
@@ -349,6 +382,9 @@ k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __
 // [own tiles' counts | record blocks' winners] -> woff; chunk_base = this
 // rank's own new states (the records' emit base), level_new = all.
 __global__ void __launch_bounds__(TSCAN_THREADS)
+// (it also resets the level's error key for the emits — expand's Assert /
+// deadlock keys were read from its own head copy; in the deterministic mode
+// settle pass A did this already, first-claim mode runs no settle pass)
 k_win_scan(const uint32_t* __restrict__ wtot, uint32_t tiles, uint32_t rblocks, uint32_t* __restrict__ woff,
            Counters* __restrict__ C) {
   __shared__ unsigned int sh_mark[4];
@@ -357,6 +393,7 @@ k_win_scan(const uint32_t* __restrict__ wtot, uint32_t tiles, uint32_t rblocks, 
   if (threadIdx.x == 0) {
     C->chunk_base = sh_mark[2];
     C->level_new = sh_mark[1];
+    C->err_key = ~0ull;
   }
 }
 constexpr unsigned SHARD_OVF_BLOCKS = 256;
@@ -853,6 +890,10 @@ class ShardT final : public ShardBase {
     const char* dc = getenv("KC_DEFER_CHECK");     // diagnostic: rebuilt states against materialised ones
     defer_check_ = dc && dc[0] == '1';
     tlc_ = cfg.tlc_order && world > 1;
+    // first-claim mode on the counted levels (k_claim FIRST, k_rec_claim_first;
+    // no candidates, no settle passes): the first inserter owns a state, as in
+    // a TLC -workers N run
+    first_ = cfg.first_claim != 0;
   }
   ~ShardT() override { release(); }
 
@@ -872,6 +913,12 @@ class ShardT final : public ShardBase {
     }
     if (tlc_ && (spill_ || !tcount_)) {
       set_error("kc_shard: tlc_order needs the deferred frontier (no seen-set spill, KC_SHARD_TSCAN on)");
+      return -EINVAL;
+    }
+    if (first_ && (tlc_ || spill_ || !tcount_)) {
+      set_error("kc_shard: first_claim cannot run with %s", tlc_ ? "tlc_order (a deterministic claim order)"
+                                                         : spill_ ? "the seen-set spill (its cold check settles winners)"
+                                                                  : "KC_SHARD_TSCAN=0 (it needs the tile counts)");
       return -EINVAL;
     }
     KC_HIP_TRY(hipSetDevice(cfg_.device));
@@ -940,6 +987,7 @@ class ShardT final : public ShardBase {
     init_key_ = init_err_;
     cur_deferred_ = false;
     emitted_links_ = false;
+    deferred_states_ = 0;
     cand_est_ = next_cand_est_ = false;
     last_new_ = 0;
     prev_rec_ = nullptr;
@@ -1030,11 +1078,14 @@ class ShardT final : public ShardBase {
     }
     const uint64_t tiles = (n_ + CLAIM_TILE - 1) / CLAIM_TILE;
     KC_TRY(grow_buffer(rcount_, rcount_cap_, tiles, false, st_));
-    KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
-    KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
+    // (first-claim mode has no candidates: no records, no overflow list; its
+    // k_claim writes each tile's new-state count, k_win_scan's input)
+    if (first_) KC_TRY(grow_buffer(wtot_, wtot_cap_, tiles + 8, false, st_));
+    if (!first_) KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
+    if (!first_) KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
     // candidates past a tile's segment: one overflow list, bounded by the
     // level's successor count
-    {
+    if (!first_) {
       // (estimated: at least two per parent; the list holds only the
       // candidates past a tile's first 256, a few percent of the successors)
       const uint64_t bound = cand_est_ ? std::max<uint64_t>(cand_, 2 * n_) : std::max<uint64_t>(cand_, 1);
@@ -1053,6 +1104,7 @@ class ShardT final : public ShardBase {
     sh.cnt = cnt_;
     sh.ovf = ovf_;
     if (tlc_) sh.gpos = gpos_cur();
+    if (first_) sh.ttot = wtot_;
     // record staging (world > 1): an estimate from the last level's records
     // per parent, at most the level's successors; a level past it packs the
     // old way (DF_STAGE, pack())
@@ -1091,6 +1143,7 @@ class ShardT final : public ShardBase {
       if (tlc_) df.prev_gpos = gpos_prev();
       cur_deferred_ = false;
       ++deferred_levels_;
+      deferred_states_ += n_;     // (rebuilt inside this k_claim: its algorithmic bytes, bench.py)
       // (the solo path stops on this level's deferred invariant after the
       // expand has counted its successors, where the exact path stops before
       // it: drop_last_expand then subtracts them, from the rebuilt states
@@ -1108,7 +1161,18 @@ class ShardT final : public ShardBase {
     if (world_ == 1) {
       // one rank owns everything: the single-GPU engine's claim kernel (no
       // owner counting; claim keys then carry rank 0, which they do anyway)
-      hipLaunchKernelGGL((k_claim<M, 0, false, 1>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+      if (first_)
+        hipLaunchKernelGGL((k_claim<M, 0, false, 1, false, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+                           cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                           (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                           d_ctr_, sh, df);
+      else
+        hipLaunchKernelGGL((k_claim<M, 0, false, 1>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+                           cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
+                           (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
+                           d_ctr_, sh, df);
+    } else if (first_) {
+      hipLaunchKernelGGL((k_claim<M, 0, true, 1, false, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                          d_ctr_, sh, df);
@@ -1348,6 +1412,20 @@ class ShardT final : public ShardBase {
     const uint32_t succ_level = (uint32_t)level_ + 1;
     const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
     const unsigned rgrid = (unsigned)((n + 255) / 256);
+    if (first_) {
+      // first-claim mode: the records' CASes (their block counts after this
+      // level's own tile counts, which k_claim wrote), one scan, the emit
+      const unsigned lt = n_ ? tiles : 0u, rb = n ? rgrid : 0u;
+      KC_TRY(grow_buffer(wtot_, wtot_cap_, (uint64_t)lt + rb + 8, true, st_));
+      KC_TRY(grow_buffer(woff_, woff_cap_, (uint64_t)lt + rb + 8, false, st_));
+      if (n) {
+        KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
+        hipLaunchKernelGGL(k_rec_claim_first<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots, isnew_,
+                           wtot_ + lt, d_ctr_);
+      }
+      hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
+      return insert_emit(in, n, true, n_new, err_key);
+    }
     if (n) {
       KC_TRY(grow_buffer(rfp_, rfp_cap_, n, false, st_));
       KC_TRY(grow_buffer(flag_, flag_cap_, n, false, st_));
@@ -1417,6 +1495,13 @@ class ShardT final : public ShardBase {
         if (changed) KC_TRY(scan_winners(n));
       }
     }
+    return insert_emit(in, n, tc, n_new, err_key);
+  }
+
+  // The emit half of insert(): the winners' positions are known (woff_ on
+  // the tile-count path `tc`, else offsets_ / ioff_).
+  int insert_emit(const Rec* in, uint64_t n, bool tc, uint64_t* n_new, uint64_t* err_key) {
+    const unsigned rgrid = (unsigned)((n + 255) / 256);
     // capacity: at most one new state per own successor and per record
     // (the deferred frontier: links and parent keys only, sized by the
     // estimate when the level's successor count is one; past it the emit
@@ -2023,6 +2108,8 @@ class ShardT final : public ShardBase {
     r->fpset_probes = h_ctr_->probes();
     r->batch_inserts = h_ctr_->settles();
     r->nlevels = level_;
+    r->claim_mode = first_ ? 1 : tlc_ ? 2 : 0;
+    r->deferred_states = deferred_states_;
     return 0;
   }
 
@@ -2093,6 +2180,7 @@ class ShardT final : public ShardBase {
   unsigned long long* stoff_ = nullptr;
   uint64_t stoff_cap_ = 0;
   bool stage_on_ = true, stage_level_ = false, staged_ = false;
+  bool first_ = false;    // first-claim mode (cfg.first_claim)
   uint64_t stage_fallbacks_ = 0;       // levels packed the old way (staging estimate exceeded)
   double rec_ratio_ = 1.0;             // records sent per parent, last level (the staging estimate)
   // the tile-count insert path: own tiles' and record blocks' new-state counts, their scan
@@ -2118,6 +2206,7 @@ class ShardT final : public ShardBase {
   bool gen_snap_ok_ = false;        // drop_last_expand can undo the last expand's act_gen
   uint64_t last_new_ = 0;            // the last insert's new states (drop_last_insert)
   uint64_t deferred_levels_ = 0, emit_retries_ = 0;
+  uint64_t deferred_states_ = 0;   // this run's states rebuilt inside k_claim (kc_result.deferred_states)
   bool defer_check_ = false;         // KC_DEFER_CHECK (diagnostic)
   // TLC order (tlc_*): G of every state (parallel to pkeys_), the current /
   // next level's G -> local index map, the per-parent masks and scratch

@@ -880,6 +880,7 @@ class Group {
 int Group::run(kc_result* res) {
   memset(res, 0, sizeof *res);
   res->err_action = res->err_self = res->err_invariant = -1;
+  res->claim_mode = cfg_.first_claim ? 1 : (cfg_.tlc_order && world_ > 1) ? 2 : 0;
   trace_.clear();
   sent_ = 0;
   sn_levels_ = 0;

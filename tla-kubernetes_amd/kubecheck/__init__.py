@@ -69,9 +69,11 @@ class ModelConfig:
     # sharded runs at R > 1: claims in sequential-BFS order, so errors and
     # traces equal TLC -workers 1's (a per-level all-reduce and sort)
     tlc_order: bool = False
-    # single-GPU engine: the first inserter of a state owns it (TLC -workers N
-    # semantics: same counts and trace lengths, no settle passes; the winning
-    # copy of a same-level duplicate is not deterministic)
+    # the first inserter of a state owns it (TLC -workers N semantics: same
+    # counts and trace lengths, no settle passes; the winning copy of a
+    # same-level duplicate is not deterministic).  The engine's in-HBM wide
+    # levels and every counted level of the sharded loop (not with tlc_order
+    # or the seen-set spill there); CheckResult.claim_mode says what ran
     first_claim: bool = False
 
     def to_c(self) -> KcModelConfig:
@@ -124,12 +126,16 @@ class CheckResult:
     defer_fallback: bool = False   # the run was redone on the materialising path
     defer_redo_level: int = 0      # ... starting from this level (1 = Init; 0 = no redo)
     narrow_levels: int = 0         # levels run by the device-driven narrow kernel
+    claim_mode: str = "minimum"    # the claims that ran: "minimum" (sequential-BFS / rank-major), "first", "tlc"
     trace: List[List[int]] = field(default_factory=list)
     trace_text: str = ""
 
     @property
     def distinct_per_sec(self) -> float:
         return self.distinct / self.seconds if self.seconds > 0 else 0.0
+
+
+CLAIM_MODES = {0: "minimum", 1: "first", 2: "tlc"}
 
 
 def _result(r: KcResult) -> CheckResult:
@@ -153,7 +159,8 @@ def _result(r: KcResult) -> CheckResult:
         seen={f[0][5:]: getattr(r, f[0]) for f in KcResult._fields_ if f[0].startswith("seen_")},
         cand_overflow_records=r.cand_overflow_records, cand_buffer_peak_bytes=r.cand_buffer_peak_bytes,
         deferred_states=r.deferred_states, defer_fallback=bool(r.defer_fallback),
-        defer_redo_level=int(r.defer_redo_level), narrow_levels=int(r.narrow_levels))
+        defer_redo_level=int(r.defer_redo_level), narrow_levels=int(r.narrow_levels),
+        claim_mode=CLAIM_MODES.get(r.claim_mode, str(r.claim_mode)))
 
 
 class ModelChecker:

@@ -63,6 +63,7 @@ class KcResult(C.Structure):
         ("cand_overflow_records", C.c_uint64), ("cand_buffer_peak_bytes", C.c_uint64),
         ("deferred_states", C.c_uint64), ("defer_fallback", C.c_uint64),
         ("defer_redo_level", C.c_uint64), ("narrow_levels", C.c_uint64),
+        ("claim_mode", C.c_int),
     ]
 
 

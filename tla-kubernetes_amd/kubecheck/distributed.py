@@ -30,7 +30,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from . import ACTIONS, INVARIANTS, ModelConfig, Spec
+from . import ACTIONS, CLAIM_MODES, INVARIANTS, ModelConfig, Spec
 from ._lib import (HC_ALL_GATHER, HC_ALL_REDUCE, HC_BROADCAST, HC_EXCHANGE, KcHostComm, KcResult, check,
                    load)
 
@@ -117,7 +117,7 @@ class HipShard:
         return {"act_gen": [int(r.act_gen[i]) for i in range(len(ACTIONS))],
                 "act_dist": [int(r.act_dist[i]) for i in range(len(ACTIONS))],
                 "init": int(r.init), "generated": int(r.generated), "distinct": int(r.distinct),
-                "fpset_slots": int(r.fpset_slots)}
+                "fpset_slots": int(r.fpset_slots), "deferred": int(r.deferred_states)}
 
     def claim_times(self):
         """(k_claim ms, launches, parents) since the last call."""
@@ -282,6 +282,7 @@ class NativeShardedChecker:
             "act_dist": {a: int(r.act_dist[i]) for i, a in enumerate(ACTIONS)},
             "seconds": float(r.seconds), "error": None, "complete": bool(r.complete),
             "narrow_levels": int(r.narrow_levels),
+            "claim_mode": CLAIM_MODES.get(r.claim_mode, str(r.claim_mode)),
         }
         if self.cfg.seen_hbm_bytes:      # per-rank seen-set spill, summed over the ranks
             out.update(seen_flushes=int(r.seen_flushes), seen_cold_fps=int(r.seen_cold_fps),
@@ -315,7 +316,8 @@ class NativeShardedChecker:
     def shard_result(self, i: int = 0) -> dict:
         r = KcResult()
         check("kc_shard_result", self._lib.kc_shard_result(self._shards[i], C.byref(r)))
-        return {"generated": int(r.generated), "init": int(r.init), "distinct": int(r.distinct)}
+        return {"generated": int(r.generated), "init": int(r.init), "distinct": int(r.distinct),
+                "deferred": int(r.deferred_states)}
 
     def close(self) -> None:
         if self._g:
@@ -581,6 +583,21 @@ def pmc_ratio(workload: str):
     return None, None, None
 
 
+def claim_alg_bytes(parents: int, gen: int, deferred: int, records: int, S: int, record_bytes: int) -> int:
+    """Algorithmic HBM bytes of the sharded k_claim, the
+    engine's model (bench.py roofline_bfs) plus what only the sharded kernel
+    writes: per expanded parent S (its state read); per generated successor
+    64 (one probe line); on a deferred frontier per rebuilt parent S + 17 (its
+    state written, its 8-B link and its parent's 8-B plan read, as the
+    engine's 9-B trace entry + plan) and per parent 8 (its plan kept for the
+    next level's rebuild); per remote representative the record it stages
+    (record_bytes, written once by k_claim)."""
+    b = parents * S + gen * 64 + records * record_bytes
+    if deferred:
+        b += deferred * (S + 17) + parents * 8
+    return int(b)
+
+
 def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict]:
     """bench.py --gpus N: every rank checks its shard; rank 0 reports.  The
     counts are checked against the golden fixture (bench.golden_check); the
@@ -594,7 +611,12 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     rank, world = dist.get_rank(), dist.get_world_size()
-    cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20, timing=0 if args.no_timing else 2)
+    # the sharded loop's fast mode by default: the first
+    # inserter of a state owns it (TLC -workers N semantics; counts, widths and
+    # depth checked against the golden below); --deterministic-shards keeps the
+    # (rank, parent)-ordered minimum claims and their settle passes
+    first = not getattr(args, "deterministic_shards", False)
+    cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20, timing=0 if args.no_timing else 2, first_claim=first)
     native = os.environ.get("KC_PY_DRIVER", "0") != "1"
     if native:                                        # the C++ level loop over RCCL
         mc = be = NativeShardedChecker(cfg, rank, world)
@@ -622,9 +644,10 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     mine = be.shard_result() if native else be.result()
     S = 8 * Spec(cfg).state_words
     gen_local = mine["generated"] * args.steps        # successors of this rank's parents
-    claim_bytes = parents * S + gen_local * 64
     if native:
         sent = mc.records_sent * args.steps if rank == 0 else 0    # already summed over ranks
+    # (records: rank 0 adds every rank's staged records, `sent` being global there)
+    claim_bytes = claim_alg_bytes(parents, gen_local, mine.get("deferred", 0) * args.steps, sent, S, be.record_bytes)
     agg = torch.tensor([claim_bytes, int(ms * 1e6), launches, sent * be.record_bytes],
                        dtype=torch.int64, device="cuda")
     dist.all_reduce(agg, op=dist.ReduceOp.SUM)
@@ -670,7 +693,11 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
                        "xgmi_bytes_per_step": xgmi // max(args.steps, 1),
                        "xgmi_GBps_per_gpu": round(xgmi / max(args.steps, 1) / world
                                                   / (dt / args.steps) / 1e9, 2),
-                       "per_level_fixed_cost": fixed},
+                       "per_level_fixed_cost": fixed,
+                       "claims": ("first inserter (TLC -workers N semantics: same counts, widths and depth; "
+                                  "the winning copy of a same-level duplicate is not deterministic)" if first else
+                                  "(rank, parent, position) minimum (deterministic)"),
+                       "claim_mode": res.get("claim_mode")},
         }
         if tot_ns > 0:
             achieved = tot_bytes / (tot_ns * 1e-9) / 1e9

@@ -21,6 +21,7 @@
 #                                                               library, then the tlc_order mode's cost
 #   gpurun -- bash tools/gpu.sh attr   <tag> [R...]             per-rank, per-level kernel attribution
 #                                                               of the emulated sharded NP=2 check
+#                                                               (ATTR_ARGS=--first: first-claim mode)
 #   gpurun -- bash tools/gpu.sh levels <tag>                    per-level costs (tools/shard_levels.py --np2)
 #   gpurun -- bash tools/gpu.sh narrow <tag>                    Model_1 narrow-level phase trace
 #                                                               (KC_NARROW_TRACE=1)
@@ -177,10 +178,10 @@ attr)
   cat $O/engine.json
   for RK in $RS; do
     step "R=$RK"
-    timeout -k 10 300 python -u tools/shard_attr.py run $RK --checks 3 > $O/wall_R$RK.log 2>&1 || { echo WALL_FAIL; tail -20 $O/wall_R$RK.log; exit 1; }
+    timeout -k 10 300 python -u tools/shard_attr.py run $RK --checks 3 $ATTR_ARGS > $O/wall_R$RK.log 2>&1 || { echo WALL_FAIL; tail -20 $O/wall_R$RK.log; exit 1; }
     cat $O/wall_R$RK.log
     cd /tmp
-    KC_SERIAL=1 timeout -s KILL 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace_R$RK -o run -- python3 $R/tools/shard_attr.py run $RK --checks 2 > $O/serial_R$RK.log 2>&1 || { echo TRACE_FAIL; tail -20 $O/serial_R$RK.log; exit 1; }
+    KC_SERIAL=1 timeout -s KILL 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace_R$RK -o run -- python3 $R/tools/shard_attr.py run $RK --checks 2 $ATTR_ARGS > $O/serial_R$RK.log 2>&1 || { echo TRACE_FAIL; tail -20 $O/serial_R$RK.log; exit 1; }
     cd $R
     grep '^{' $O/serial_R$RK.log
     python3 tools/shard_attr.py summarize $O/trace_R$RK $RK --out $O/attr_R$RK.json > /dev/null || exit 1

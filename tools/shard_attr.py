@@ -1,13 +1,14 @@
 """Per-rank, per-kernel attribution of an emulated sharded NP=2 check
 (VERDICT r4 "next" item 1a).
 
-  run:        python tools/shard_attr.py run R [--checks K] [--tlc]
+  run:        python tools/shard_attr.py run R [--checks K] [--tlc | --first]
               K (default 2) sharded NP=2 checks with R ranks emulated on one
               GPU; with KC_SERIAL=1 in the environment every rank's stage is
               synchronised before the next rank's launches, so no two ranks'
               kernels overlap.  Prints one JSON line per check (wall ms,
               distinct).  Run it under rocprofv3 --kernel-trace.  --tlc:
-              with ModelConfig.tlc_order (TLC-ordered claims).
+              with ModelConfig.tlc_order (TLC-ordered claims); --first: with
+              ModelConfig.first_claim (first-inserter claims, no settle passes).
   summarize:  python tools/shard_attr.py summarize TRACE_DIR R [--out f.json]
               reads rocprofv3's *_kernel_trace.csv (and *_memory_copy_trace.csv
               if present), keeps the last check (from the last R
@@ -27,12 +28,12 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(R, checks, tlc=False):
+def run(R, checks, tlc=False, first=False):
     sys.path.insert(0, os.path.join(ROOT, "tla-kubernetes_amd"))
     import torch  # noqa: F401  (owns the HIP runtime first)
     from kubecheck import ModelConfig
     from kubecheck.distributed import NativeShardedChecker
-    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False, tlc_order=tlc), emulate=R)
+    mc = NativeShardedChecker(ModelConfig(np=2, keep_trace=False, tlc_order=tlc, first_claim=first), emulate=R)
     try:
         for k in range(checks):
             t0 = time.perf_counter()
@@ -40,6 +41,7 @@ def run(R, checks, tlc=False):
             dt = time.perf_counter() - t0
             print(json.dumps({"R": R, "check": k, "ms": round(dt * 1e3, 2), "distinct": r["distinct"],
                               "depth": r["depth"], "serial": os.environ.get("KC_SERIAL", "0"), "tlc": tlc,
+                              "first": first, "claim_mode": r.get("claim_mode"),
                               "lib": os.path.basename(os.environ.get("KUBECHECK_LIB", "libkubecheck.so"))}),
                   flush=True)
     finally:
@@ -116,7 +118,7 @@ def summarize(d, R, out):
 if __name__ == "__main__":
     a = sys.argv[1:]
     if a and a[0] == "run":
-        run(int(a[1]), int(a[a.index("--checks") + 1]) if "--checks" in a else 2, "--tlc" in a)
+        run(int(a[1]), int(a[a.index("--checks") + 1]) if "--checks" in a else 2, "--tlc" in a, "--first" in a)
     elif a and a[0] == "summarize":
         summarize(a[1], int(a[2]), a[a.index("--out") + 1] if "--out" in a else None)
     else:
