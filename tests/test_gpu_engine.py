@@ -147,6 +147,22 @@ def test_enlarged_full(fixtures, monkeypatch, defer):
     assert r.complete and r.error is None
 
 
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_enlarged_full_first_claim(fixtures, monkeypatch, defer):
+    # the bench's headline mode (round 6): the whole NP=2 model with the first
+    # inserter of every state as its owner, on both frontier paths — counts,
+    # depth, every level width and the per-action generated counts equal the
+    # golden; the distinct split is a valid one (it sums to the new states)
+    fx = fixtures["np2_full"]
+    monkeypatch.setenv("KC_DEFER", defer)
+    r = run(np=2, keep_trace=True, first_claim=True)
+    assert r.claim_mode == "first" and not r.defer_fallback
+    assert (r.distinct, r.generated, r.depth) == (fx["distinct"], fx["generated"], fx["depth"])
+    assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+    assert sum(r.act_dist.values()) + r.init == r.distinct
+    assert r.complete and r.error is None
+
+
 # --- error paths: every kind of violation the checker
 # reports, against the oracle's error, level and trace, state for state
 @pytest.mark.parametrize("key,kw,kind,what", [

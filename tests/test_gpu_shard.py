@@ -429,15 +429,14 @@ def test_native_tlc_order_np2(fixtures):
 def test_native_np2_prefix_switches(fixtures, monkeypatch):
     # the NP=2 40-level prefix at 4 emulated ranks with each round-5 path
     # switched off in turn (materialising emit, k_shard_pack, per-parent
-    # scans, one tile per settle workgroup): counts equal to the oracle's, and
-    # every per-action distinct count equal across the variants (the same
-    # claims win whichever path built, packed or positioned the states)
+    # scans): counts equal to the oracle's, and every per-action distinct
+    # count equal across the variants (the same claims win whichever path
+    # built, packed or positioned the states)
     fx = fixtures["np2_40levels"]
     runs = {}
     for name, env in (("default", {}), ("sdefer0", {"KC_SDEFER": "0"}), ("stage0", {"KC_STAGE": "0"}),
-                      ("tscan0", {"KC_SHARD_TSCAN": "0"}), ("tp1", {"KC_SETTLE_TP": "1"}),
-                      ("tp4", {"KC_SETTLE_TP": "4"})):
-        for k in ("KC_SDEFER", "KC_STAGE", "KC_SHARD_TSCAN", "KC_SETTLE_TP"):
+                      ("tscan0", {"KC_SHARD_TSCAN": "0"})):
+        for k in ("KC_SDEFER", "KC_STAGE", "KC_SHARD_TSCAN"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

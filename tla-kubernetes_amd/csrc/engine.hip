@@ -172,25 +172,13 @@ class EngineT final : public EngineBase {
     // seen-set spill: a fixed-size hot ClaimSet + the cold tier (coldset.h);
     // the chunked wide path with tile offsets only
     spill_ = cfg.seen_hbm_bytes > 0;
-    if (spill_) narrow_on_ = false;    // k_claim tile order (engine_kernels.h spread_tile; KC_TILE_SPREAD=0: block order)
-    const char* sp = getenv("KC_TILE_SPREAD");
-    if (sp) claim_args_.spread = (uint32_t)atoi(sp);
+    if (spill_) narrow_on_ = false;
     const char* ts = getenv("KC_TSCAN");
     tscan_ = spill_ || !(ts && ts[0] == '0');
-    const char* fz = getenv("KC_FUSE_SCAN");
-    fuse_scan_ = !(fz && fz[0] == '0');
     const char* nb = getenv("KC_NARROW_BATCH");   // narrow levels enqueued per host sync (A/B)
     if (nb && atoi(nb) > 0) narrow_batch_ = atoi(nb);
     const char* tr = getenv("KC_TSCAN_REG");
     tscan_reg_ = !(tr && tr[0] == '0');
-    // KC_SETTLE_TP: claim tiles per settle workgroup (1, 2, 4 or 8)
-    const char* tp = getenv("KC_SETTLE_TP");
-    if (tp) {
-      const int v = atoi(tp);
-      settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
-    }
-    const char* eo = getenv("KC_EMIT_OCC");
-    if (eo) emit_occ_ = atoi(eo);
     const char* hc = getenv("KC_HEADCOPY");
     headcopy_ = hc && hc[0] == '1';
     // deferred frontier (engine_kernels.h DeferArgs): the default wide path
@@ -199,8 +187,6 @@ class EngineT final : public EngineBase {
     defer_ = !(df && df[0] == '0') && !spill_ && !queued_ && !ablate_;
     // KC_DEFER_SLACK: the capacity estimate's factor over the measured
     // successors per state (tests shrink it to force the exact-path redo)
-    const char* dp = getenv("KC_DEFER_PC");
-    pc_pass_ = !(dp && dp[0] == '0');
     const char* dr = getenv("KC_DEFER_REDO");      // KC_DEFER_REDO=0: an anomaly redoes the run from Init
     redo_on_ = !(dr && dr[0] == '0');
     const char* dd = getenv("KC_DEFER_DIRECT");    // KC_DEFER_DIRECT=0: invariant anomalies are redone too (A/B)
@@ -464,7 +450,7 @@ class EngineT final : public EngineBase {
       }
       KC_TRY(grow_buffer(newmask_, mask_cap_, std::min(n, chunk), false, st_));
       DeferArgs df = mat ? DeferArgs{} : defer_args(level_gidx, prev_gidx);
-      if (dfr && pc_pass_) df.counts_out = pc_cur_;   // this level's plans, for the next level's rebuild
+      if (dfr) df.counts_out = pc_cur_;   // this level's plans, for the next level's rebuild
       if (!mat) res->deferred_states += n;
       uint64_t link_cap = ~0ull;
       if (dfr) {
@@ -525,7 +511,7 @@ class EngineT final : public EngineBase {
           });
         }
         // (a small chunk: the overflow list's pass B inside the tile scan's launch)
-        const bool fuse = tscan_ && fuse_scan_ && cn <= FUSE_OVF_SCAN_MAX && !first_claim_;
+        const bool fuse = tscan_ && cn <= FUSE_OVF_SCAN_MAX && !first_claim_;
         if (!first_claim_)
           timed(KK_RESOLVE,
                 [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr, fuse); });
@@ -577,14 +563,6 @@ class EngineT final : public EngineBase {
             hipLaunchKernelGGL(k_emit_links, dim3(grid), dim3(256), 0, st_, cn, start, newmask_, toff_, level_gidx,
                                next_gidx, cfg_.keep_trace ? parent_ : nullptr, cfg_.keep_trace ? ord_ : nullptr,
                                use_link ? link_next_ : nullptr, link_cap, d_ctr_);
-          else if (emit_occ_ == 7)
-            hipLaunchKernelGGL((k_emit_occ<M, 7>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
-                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                               cfg_.keep_trace, d_ctr_, toff);
-          else if (emit_occ_ == 6)
-            hipLaunchKernelGGL((k_emit_occ<M, 6>), dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
-                               flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
-                               cfg_.keep_trace, d_ctr_, toff);
           else
             hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
@@ -1108,6 +1086,10 @@ class EngineT final : public EngineBase {
     hipLaunchKernelGGL(k_nexpand<M>, dim3(NARROW_WG * NARROW_SUB), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
                        cfg_.check_deadlock, 0u, d_ns_, d_nsc_, d_ctr_, d_ntrace_);
     for (;;) {
+      // (round 6 captured a batch's launches into a hipGraph, replayed with
+      // one hipGraphLaunch: Model_1 2.79-2.82 ms against 2.80 — the cost of
+      // a level is its in-kernel chain, not the launches; removed,
+      // profiles/r06g_model1_narrow_graph_ab.log)
       timed(KK_NARROW, [&] {
         for (int k = 0; k < narrow_batch_; ++k, ++lev)
           hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
@@ -1164,7 +1146,7 @@ class EngineT final : public EngineBase {
       df.gidx0 = level_gidx;
       df.prev_gidx0 = prev_gidx;
     }
-    if (pc_valid_ && pc_pass_) df.prev_counts = pc_prev_;
+    if (pc_valid_) df.prev_counts = pc_prev_;
     return df;
   }
   // Materialise a deferred frontier of n states into cur_ (k_materialize):
@@ -1223,7 +1205,6 @@ class EngineT final : public EngineBase {
   unsigned long long* pc_prev_ = nullptr;
   uint64_t pc_cur_cap_ = 0, pc_prev_cap_ = 0;
   bool pc_valid_ = false;
-  bool pc_pass_ = true;              // KC_DEFER_PC=0: rebuilds plan their grandparent (A/B)
   static constexpr int kDeferRetry = -100000;
   bool defer_ = false, defer_now_ = false;
   double defer_slack_ = 1.25;
@@ -1355,11 +1336,11 @@ class EngineT final : public EngineBase {
   int spill_setup() {
     if (!cs_.t) {
       const uint64_t B = cfg_.seen_hbm_bytes;
-      // the hot table's share of the budget: 1/2 (KC_SEEN_HOT_DIV=4: 1/4, A/B)
-      const char* hd = getenv("KC_SEEN_HOT_DIV");
-      const uint64_t div = hd && atoi(hd) >= 2 ? (uint64_t)atoi(hd) : 2;
+      // the hot table's share of the budget: 1/2 (round 4 A/B: 1/4 leaves room
+      // for HBM copies of the newest cold runs but doubles the flushes,
+      // 6.0-6.6 s against 4.7-5.3 s on NP=2 at 4 GiB)
       uint64_t ns = 1ull << 12;
-      while (ns * 2 * sizeof(ClaimEntry) <= B / div) ns *= 2;
+      while (ns * 2 * sizeof(ClaimEntry) <= B / 2) ns *= 2;
       KC_TRY(cs_.init(ns, st_));
       hot_limit_ = ns / 2;
       q_max_ = std::max<uint64_t>(CLAIM_TILE * 32, hot_limit_ / 3) / 256 * 256;
@@ -1833,39 +1814,21 @@ class EngineT final : public EngineBase {
   bool tscan_ = false, headcopy_ = false;
   int narrow_batch_ = NARROW_BATCH;
   int tscan_reg_ = 1;   // KC_TSCAN_REG=0: k_tile_scan's loop path (levels > 65,536 tiles) at any width
-  int settle_tp_ = SETTLE_TP_DEFAULT;   // claim tiles per settle workgroup (KC_SETTLE_TP)
-  // settle passes A and B of a chunk's tiles (k_settle_rec, or k_settle_mt
-  // with settle_tp_ tiles per workgroup), then the overflow list's pass B
+  // settle passes A and B of a chunk's tiles (k_settle_rec, one workgroup
+  // per tile; round 5 measured 2 / 4 / 8 tiles per workgroup no faster,
+  // DESIGN §7.3), then the overflow list's pass B
   void launch_settle(uint64_t cn, uint64_t start, unsigned tiles, uint32_t succ_level, uint32_t* ttot,
                      bool ovf_in_scan = false) {
-    if (settle_tp_ == 1) {
-      hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
-                         cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
-                         (uint32_t*)nullptr, tiles, claim_args_.ovf);
-      hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t, cs_.nslots,
-                         succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u, ttot);
-    } else {
-#define KC_SETTLE_MT(TP)                                                                                          \
-  if (settle_tp_ == TP) {                                                                                         \
-    const unsigned tb = (tiles + TP - 1) / TP;                                                                    \
-    hipLaunchKernelGGL((k_settle_mt<0, TP>), dim3(tb + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,   \
-                       cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,            \
-                       (uint32_t*)nullptr, tiles, claim_args_.ovf);                                                \
-    hipLaunchKernelGGL((k_settle_mt<1, TP>), dim3(tb), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t, cs_.nslots,     \
-                       succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u, ttot, tiles, claim_args_.ovf); \
-  }
-      KC_SETTLE_MT(2)
-      KC_SETTLE_MT(4)
-      KC_SETTLE_MT(8)
-#undef KC_SETTLE_MT
-    }
+    hipLaunchKernelGGL(k_settle_rec<0>, dim3(tiles + SETTLE_OVF_BLOCKS), dim3(CLAIM_TILE), 0, st_, cn, start,
+                       cs_.t, cs_.nslots, succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u,
+                       (uint32_t*)nullptr, tiles, claim_args_.ovf);
+    hipLaunchKernelGGL(k_settle_rec<1>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cn, start, cs_.t, cs_.nslots,
+                       succ_level, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, 0u, ttot);
     if (!ovf_in_scan)   // (else k_ovf_tile_scan settles it)
       hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
                          cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
   }
   bool first_claim_ = false;   // KC_FIRST_CLAIM=1: k_claim FIRST, no settle passes (multi-worker TLC semantics)
-  bool fuse_scan_ = true;   // KC_FUSE_SCAN=0: small chunks keep the separate overflow pass B launch (A/B)
-  int emit_occ_ = 0;   // KC_EMIT_OCC=6|7: k_emit pinned to that many waves per SIMD instead of 8 (A/B)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;
   uint64_t ttot_cap_ = 0, toff_cap_ = 0;
   unsigned int *rcount_ = nullptr, *rec_lk_ = nullptr;

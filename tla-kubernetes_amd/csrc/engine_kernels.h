@@ -738,9 +738,6 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, ui
 // TLC (SH only): claims, records and keys by the parents' G (ClaimKeys; the
 // sharded loop's tlc_order mode), a variant of its own so the default one's
 // registers are untouched
-#ifndef KC_SH_WAVES
-#define KC_SH_WAVES 6
-#endif
 // Diagnostic builds (-DKC_CLAIM_TRACE): thread 0 of every k_claim workgroup
 // stamps the wall clock (100 MHz) at its phase boundaries and adds each
 // phase's duration to g_ctrace[1..7] ([0] workgroups, [8] the longest
@@ -764,7 +761,7 @@ static __device__ unsigned long long g_ctrace[16];
 // not deterministic, as in a multi-worker TLC run.
 template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false, bool FIRST = false>
 __global__ void __launch_bounds__(CLAIM_TILE)
-__attribute__((amdgpu_waves_per_eu(SH ? KC_SH_WAVES : 6, SH ? KC_SH_WAVES : 6)))
+__attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
         int check_deadlock, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
         uint32_t* __restrict__ scratch /* ABL builds only */, unsigned int* __restrict__ rcount,
@@ -1323,81 +1320,6 @@ __device__ __forceinline__ void settle_tile(uint32_t tile, uint64_t n, uint64_t 
     }
   }
 }
-// TP consecutive tiles per workgroup (round 5, KC_SETTLE_TP; 1 = settle_tile):
-// a tile holds ~40 candidates on NP=2, so one workgroup per tile spends
-// most of its life being dispatched (2.9M tiles x 2 passes per check).  The
-// TP tiles' candidates are dealt to the 256 lanes together (all their
-// atomics still in flight at once, unlike a persistent loop over tiles,
-// DESIGN §7.3), and PASS 1 counts each tile's new states as settle_tile.
-template <int PASS, int TP>
-__device__ __forceinline__ void settle_tiles(uint32_t t0, uint32_t ntiles, uint64_t n, uint64_t base,
-                                             ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-                                             const unsigned int* __restrict__ rcount,
-                                             const unsigned long long* __restrict__ rec_fp,
-                                             unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask,
-                                             Counters* __restrict__ C, ClaimKeys rank,
-                                             uint32_t* __restrict__ tile_total) {
-  __shared__ unsigned int sh_cnt[TP + 1];
-  __shared__ unsigned int sh_tot[CLAIM_TILE / 64][TP];
-  unsigned newc[TP];
-#pragma unroll
-  for (int j = 0; j < TP; ++j) newc[j] = 0;
-  if (threadIdx.x == 0) {
-    unsigned a = 0;
-    for (int j = 0; j < TP; ++j) {
-      sh_cnt[j] = a;
-      a += t0 + j < ntiles ? rcount[t0 + j] : 0u;
-    }
-    sh_cnt[TP] = a;
-  }
-  if (PASS == 1 && tile_total) {
-    // read before any of this pass's bit sets (the barrier below orders them)
-#pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      const uint64_t p = (uint64_t)(t0 + j) * CLAIM_TILE + threadIdx.x;
-      if (t0 + j < ntiles && p < n) newc[j] = (unsigned)__builtin_popcount(newmask[p]);
-    }
-  }
-  __syncthreads();
-  unsigned reads = 0;
-  const unsigned total = sh_cnt[TP];
-  for (unsigned k = threadIdx.x; k < total; k += CLAIM_TILE) {
-    int j = 0;
-#pragma unroll
-    for (int q = 1; q < TP; ++q)
-      if (k >= sh_cnt[q]) j = q;
-    const uint32_t tile = t0 + j;
-    const uint64_t r = (uint64_t)tile * CLAIM_RCAP + (k - sh_cnt[j]);
-    const int v = settle_record<PASS>(tile, rec_fp[r], &rec_lk[r], n, base, cs, nbuckets, level, newmask, C, rank);
-    reads += v ? 1u : 0u;
-    if (v == 2) {
-#pragma unroll
-      for (int q = 0; q < TP; ++q)
-        if (q == j) ++newc[q];
-    }
-  }
-  unsigned long long rw = reads;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) rw += __shfl_down(rw, off, 64);
-  if ((threadIdx.x & 63) == 0 && rw) atomicAdd(&stripe(C).settles, rw);
-  if (PASS == 1 && tile_total) {
-#pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      unsigned v = newc[j];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-      if ((threadIdx.x & 63) == 0) sh_tot[threadIdx.x >> 6][j] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < TP && t0 + threadIdx.x < ntiles) {
-      unsigned t = 0;
-#pragma unroll
-      for (int w = 0; w < CLAIM_TILE / 64; ++w) t += sh_tot[w][threadIdx.x];
-      tile_total[t0 + threadIdx.x] = t;
-    }
-  }
-}
-
 // The same passes over the chunk's overflow list (after k_settle_rec<PASS>:
 // a PASS-1 winner then adds itself to its tile's count).
 template <int PASS>
@@ -1428,7 +1350,6 @@ k_settle_ovf(CandOvf ovf, uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs
   settle_ovf_blocks<PASS>(blockIdx.x, gridDim.x, ovf, n, base, cs, nbuckets, level, newmask, C, rank, tile_total);
 }
 constexpr unsigned SETTLE_OVF_GRID = 1024;
-constexpr int SETTLE_TP_DEFAULT = 1;     // claim tiles per settle workgroup (engine KC_SETTLE_TP)
 // blocks of settle pass A's launch that take the overflow list (pass A needs
 // no counts, so its overflow work shares the tiles' launch; pass B's adds to
 // the tile counts the tile blocks compute, so it runs in a launch of its own)
@@ -1456,24 +1377,6 @@ k_settle_rec(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nb
 // is at most 2^27 parents, so the totals fit u32).  Each thread takes a
 // contiguous run of 16-B groups (4 tiles); up to TS_REG groups per thread
 // (T <= 65,536 tiles) stay in registers, all their loads in flight at once.
-// k_settle_rec with TP tiles per workgroup (PASS 0: the grid's blocks past
-// ceil(tiles / TP) take the overflow list, as k_settle_rec's past `tiles`)
-template <int PASS, int TP>
-static __global__ void __launch_bounds__(CLAIM_TILE)
-k_settle_mt(uint64_t n, uint64_t base, ClaimEntry* __restrict__ cs, uint64_t nbuckets, uint32_t level,
-            const unsigned int* __restrict__ rcount, const unsigned long long* __restrict__ rec_fp,
-            unsigned int* __restrict__ rec_lk, uint32_t* __restrict__ newmask, Counters* __restrict__ C,
-            ClaimKeys rank, uint32_t* __restrict__ tile_total, uint32_t tiles, CandOvf ovf) {
-  const uint32_t tb = (tiles + TP - 1) / TP;
-  if (PASS == 0 && blockIdx.x >= tb) {
-    settle_ovf_blocks<0>(blockIdx.x - tb, gridDim.x - tb, ovf, n, base, cs, nbuckets, level, newmask, C, rank,
-                         nullptr);
-    return;
-  }
-  settle_tiles<PASS, TP>(blockIdx.x * TP, tiles, n, base, cs, nbuckets, level, rcount, rec_fp, rec_lk, newmask, C,
-                         rank, tile_total);
-}
-
 constexpr int TSCAN_THREADS = 1024;
 // Marks of a tile scan (the sharded levels): the exclusive prefix at
 // positions m_k = k * stride for k = 0 .. nmark - 1, plus at `extra`, go to
@@ -1780,16 +1683,4 @@ k_emit(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fla
   emit_body<M, ABL>(cur, n, base, f, newmask, offsets, next, next_base, level_gidx, next_gidx, parent, ord,
                     keep_trace, C, tile_off);
 }
-// the same pinned to OCC waves per SIMD instead (KC_EMIT_OCC=6|7; A/B)
-template <class M, int OCC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
-k_emit_occ(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
-           const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ offsets,
-           typename M::State* __restrict__ next, uint64_t next_base, uint64_t level_gidx, uint64_t next_gidx,
-           unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
-           Counters* __restrict__ C, const uint32_t* __restrict__ tile_off) {
-  emit_body<M, 0>(cur, n, base, f, newmask, offsets, next, next_base, level_gidx, next_gidx, parent, ord,
-                  keep_trace, C, tile_off);
-}
-
 }  // namespace kc

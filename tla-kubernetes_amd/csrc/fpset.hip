@@ -105,8 +105,7 @@ int DevFpset::reserve(uint64_t extra, hipStream_t st) {
 // a plain store next to the CAS'd fp).
 // The per-run clear of the ClaimSet: 16-B non-temporal stores over a
 // grid-stride loop of 8192 workgroups (64 GiB in 9.9-10.1 ms against 10.8-10.9
-// for hipMemsetAsync, profiles/r03ap_clear.txt; KC_CS_CLEAR=memset or
-// kernel:<workgroups> for the A/B).
+// for hipMemsetAsync, profiles/r03ap_clear.txt).
 typedef unsigned int kc_u32x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_claimset_clear(ClaimEntry* __restrict__ t, uint64_t nslots) {
   kc_u32x4* p = reinterpret_cast<kc_u32x4*>(t);
@@ -164,17 +163,13 @@ int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
   return 0;
 }
 
+// (an 8,192-workgroup grid-stride clear kernel: 6.9 TB/s on the 64 GiB NP=2
+// table against hipMemsetAsync's 6.3, round 3)
 int DevClaimSet::clear(hipStream_t st) {
-  static const int mode = [] {
-    const char* e = getenv("KC_CS_CLEAR");          // memset | kernel (default) | kernel:<workgroups>
-    if (e && !strcmp(e, "memset")) return 0;
-    if (e && !strncmp(e, "kernel:", 7) && atoi(e + 7) > 0) return atoi(e + 7);
-    return 8192;
-  }();
-  if (mode == 0 || nslots < (1u << 20)) {
+  if (nslots < (1u << 20)) {
     KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * sizeof(ClaimEntry), st));
   } else {
-    hipLaunchKernelGGL(k_claimset_clear, dim3((unsigned)mode), dim3(256), 0, st, t, nslots);
+    hipLaunchKernelGGL(k_claimset_clear, dim3(8192u), dim3(256), 0, st, t, nslots);
     KC_HIP_TRY(hipGetLastError());
   }
   count = 0;
@@ -196,13 +191,10 @@ void DevClaimSet::release() {
 // larger clear included).  Past 1/3 load the table grows to
 // land at <= 1/4; when HBM cannot hold that, at <= 1/2.
 int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
-  // KC_CS_LOAD=k (A/B): grow once the reserved fill would pass 1/k of the
-  // slots, to at most 1/(k + 1) (default k = 3)
-  static const uint64_t ld = [] {
-    const char* e = getenv("KC_CS_LOAD");
-    const int v = e ? atoi(e) : 0;
-    return (uint64_t)(v >= 2 && v <= 8 ? v : 3);
-  }();
+  // grow once the reserved fill would pass 1/3 of the slots, to at most 1/4
+  // (round 5 A/B: growing at 1/2 halves the NP=2 table and its clear but
+  // costs k_claim 7-10 ms in longer probe runs; 1/4 gives the same table)
+  constexpr uint64_t ld = 3;
   const uint64_t need = count + extra;
   if (need * ld <= capacity()) return 0;
   uint64_t ns = nslots, ns_min = nslots;
@@ -388,62 +380,10 @@ k_stress_lookup(uint64_t seed, uint64_t n_ins, uint64_t start, uint64_t n,
   const unsigned long long b = __ballot(f != 0);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(&stat_row(stats)[2], (unsigned long long)__popcll(b));
 }
-// Windowed stress insert (KC_STRESS_WINDOW=<log2 slots per
-// window>, A/B): a super-batch of the insert stream is generated into
-// memory and bucketed by table window (bucket_of >> wbits: 2^27 slots =
-// 1 GiB) — per workgroup an LDS histogram, one atomic per (workgroup,
-// window) to reserve its ranges — so the inserts that follow sweep the table
-// one window after another instead of all of it at once (random CAS on a
-// <= 1 GB window ran 27 vs 19 G/s, profiles/r03d_random_probe.txt).  The
-// stream has no duplicates, so the order of the inserts changes nothing.
-constexpr int WIN_MAX = 1024;
-__global__ void __launch_bounds__(256)
-k_win_gen_count(uint64_t seed, uint64_t start, uint64_t n, uint64_t ns, int wbits, uint32_t nwin,
-                uint64_t* __restrict__ out, unsigned int* __restrict__ wcount) {
-  __shared__ unsigned int h[WIN_MAX];
-  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x) h[w] = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const uint64_t fp = stress_insert_fp(seed, start + i);
-    out[i] = fp;
-    atomicAdd(&h[(uint32_t)(bucket_of(fp, ns) >> wbits)], 1u);
-  }
-  __syncthreads();
-  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x)
-    if (h[w]) atomicAdd(&wcount[w], h[w]);
-}
-// exclusive scan of the window counts into cursors (one workgroup)
-__global__ void k_win_cursor(const unsigned int* __restrict__ wcount, uint32_t nwin,
-                             unsigned long long* __restrict__ cursor) {
-  if (threadIdx.x != 0) return;
-  unsigned long long a = 0;
-  for (uint32_t w = 0; w < nwin; ++w) {
-    cursor[w] = a;
-    a += wcount[w];
-  }
-}
-__global__ void __launch_bounds__(256)
-k_win_scatter(const uint64_t* __restrict__ in, uint64_t n, uint64_t ns, int wbits, uint32_t nwin,
-              unsigned long long* __restrict__ cursor, uint64_t* __restrict__ out) {
-  __shared__ unsigned int h[WIN_MAX];
-  __shared__ unsigned long long base[WIN_MAX];
-  for (uint32_t w = threadIdx.x; w < nwin; w += blockDim.x) h[w] = 0;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t fp = 0;
-  uint32_t w = 0, r = 0;
-  if (i < n) {
-    fp = in[i];
-    w = (uint32_t)(bucket_of(fp, ns) >> wbits);
-    r = atomicAdd(&h[w], 1u);
-  }
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < nwin; k += blockDim.x)
-    if (h[k]) base[k] = atomicAdd(&cursor[k], (unsigned long long)h[k]);
-  __syncthreads();
-  if (i < n) out[base[w] + r] = fp;
-}
+// (Round 5 measured windowed inserts — the stream bucketed by 1 GiB table
+// windows before the CASes — 4.4x slower: the bucketing pass writes and
+// re-reads every fingerprint, and a 1 GiB window is no more cache-resident
+// than the whole table; DESIGN §7.3.  Removed in round 6.)
 
 // The same streams written to memory (the sharded stress exchanges them).
 __global__ void k_stress_gen(uint64_t seed, int kind, uint64_t n_ins, uint64_t start, uint64_t n,
@@ -820,41 +760,11 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   KC_HIP_TRY(hipEventCreate(&e1));
   KC_HIP_TRY(hipEventCreate(&e2));
   KC_HIP_TRY(hipMemsetAsync(s->d_stats, 0, STAT_BYTES, st));
-  // windowed inserts (A/B): KC_STRESS_WINDOW = log2 of the slots per window;
-  // KC_STRESS_SUPER = inserts per super-batch (default 4 batches)
-  const char* we = getenv("KC_STRESS_WINDOW");
-  const int wbits = we ? atoi(we) : 0;
-  const uint64_t ns = s->fs.nbuckets * 8;
-  const uint32_t nwin = wbits > 0 ? (uint32_t)((ns + (1ull << wbits) - 1) >> wbits) : 0;
-  const char* se = getenv("KC_STRESS_SUPER");
-  const uint64_t sb = se && atoll(se) > 0 ? (uint64_t)atoll(se) : 4 * batch;
-  uint64_t *wa = nullptr, *wb = nullptr;
-  unsigned int* wcnt = nullptr;
-  unsigned long long* wcur = nullptr;
-  const bool windowed = wbits > 0 && nwin >= 2 && nwin <= (uint32_t)WIN_MAX;
-  if (windowed) {
-    KC_HIP_TRY(hipMalloc(&wa, std::min(sb, n) * 8));
-    KC_HIP_TRY(hipMalloc(&wb, std::min(sb, n) * 8));
-    KC_HIP_TRY(hipMalloc(&wcnt, WIN_MAX * 4));
-    KC_HIP_TRY(hipMalloc(&wcur, WIN_MAX * 8));
-  }
   KC_HIP_TRY(hipEventRecord(e0, st));
-  if (windowed) {
-    for (uint64_t off = 0; off < n; off += sb) {
-      const uint64_t m = std::min(sb, n - off);
-      const unsigned g = (unsigned)((m + 255) / 256);
-      KC_HIP_TRY(hipMemsetAsync(wcnt, 0, WIN_MAX * 4, st));
-      hipLaunchKernelGGL(k_win_gen_count, dim3(g), dim3(256), 0, st, seed, off, m, ns, wbits, nwin, wa, wcnt);
-      hipLaunchKernelGGL(k_win_cursor, dim3(1), dim3(64), 0, st, wcnt, nwin, wcur);
-      hipLaunchKernelGGL(k_win_scatter, dim3(g), dim3(256), 0, st, wa, m, ns, wbits, nwin, wcur, wb);
-      hipLaunchKernelGGL(k_insert_count, dim3(g), dim3(256), 0, st, wb, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
-    }
-  } else {
-    for (uint64_t off = 0; off < n; off += batch) {
-      const uint64_t m = std::min(batch, n - off);
-      hipLaunchKernelGGL(k_stress_insert, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, seed,
-                         off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
-    }
+  for (uint64_t off = 0; off < n; off += batch) {
+    const uint64_t m = std::min(batch, n - off);
+    hipLaunchKernelGGL(k_stress_insert, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, seed,
+                       off, m, s->fs.slots, s->fs.nbuckets, s->d_stats);
   }
   KC_HIP_TRY(hipEventRecord(e1, st));
   for (uint64_t off = 0; off < n_lookup; off += batch) {
@@ -872,8 +782,6 @@ int kc_fpset_stress(kc_fpset* s, uint64_t seed, uint64_t n, uint64_t batch, uint
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipEventDestroy(e2);
-  for (void* p : {(void*)wa, (void*)wb, (void*)wcnt, (void*)wcur})
-    if (p) (void)hipFree(p);
   s->fs.count += stats[0];
   if (insert_seconds) *insert_seconds = ms1 * 1e-3;
   if (lookup_seconds) *lookup_seconds = ms2 * 1e-3;

@@ -351,8 +351,7 @@ __device__ __forceinline__ void rec_settle(uint64_t blk, const Record<M>* __rest
 // wtot[tiles, tiles + rblocks) — k_win_scan's input — and the launch has no
 // overflow-list blocks: their pass B adds to the tile counts afterwards
 // (k_settle_ovf<1>), as the engine's does, so no winner is counted twice.
-// (TP own tiles per workgroup, settle_tiles: the first ceil(tiles / TP) blocks)
-template <class M, int PASS, int TP = 1>
+template <class M, int PASS>
 __global__ void __launch_bounds__(256)
 k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __restrict__ cs, uint64_t nslots,
               uint32_t level, ClaimKeys rank, const unsigned int* __restrict__ rcount,
@@ -362,14 +361,10 @@ k_settle_both(uint32_t tiles, uint32_t rblocks, uint64_t n_local, ClaimEntry* __
               uint32_t* __restrict__ isnew, Counters* __restrict__ C, CandOvf ovf, uint32_t* __restrict__ wtot) {
   static_assert(CLAIM_TILE == 256, "one block size for both halves");
   if (PASS == 0 && blockIdx.x == 0 && threadIdx.x == 0) C->err_key = ~0ull;   // (nothing before the emits sets it)
-  const uint32_t tb = (tiles + TP - 1) / TP;
+  const uint32_t tb = tiles;
   if (blockIdx.x < tb) {
-    if (TP == 1)
-      settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank,
-                        PASS == 1 ? wtot : nullptr);
-    else
-      settle_tiles<PASS, TP>(blockIdx.x * TP, tiles, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask,
-                             C, rank, PASS == 1 ? wtot : nullptr);
+    settle_tile<PASS>(blockIdx.x, n_local, 0, cs, nslots, level, rcount, rec_fp, rec_lk, newmask, C, rank,
+                      PASS == 1 ? wtot : nullptr);
   } else if (blockIdx.x < tb + rblocks) {
     rec_settle<M, PASS>(blockIdx.x - tb, in, n, cs, nslots, level, rank, rfp, flag, newmask, n_local, isnew, C,
                         PASS == 1 && wtot ? wtot + tiles : nullptr);
@@ -880,13 +875,6 @@ class ShardT final : public ShardBase {
     stage_on_ = !(sg && sg[0] == '0');
     const char* ts = getenv("KC_SHARD_TSCAN");
     tcount_ = !(ts && ts[0] == '0');
-    const char* tp = getenv("KC_SETTLE_TP");
-    if (tp) {
-      const int v = atoi(tp);
-      settle_tp_ = (v == 2 || v == 4 || v == 8) ? v : 1;
-    }
-    const char* fz = getenv("KC_FUSE_SCAN");       // KC_FUSE_SCAN=0: no fused overflow pass B + scan (A/B)
-    fuse_scan_ = !(fz && fz[0] == '0');
     const char* dc = getenv("KC_DEFER_CHECK");     // diagnostic: rebuilt states against materialised ones
     defer_check_ = dc && dc[0] == '1';
     tlc_ = cfg.tlc_order && world > 1;
@@ -1444,8 +1432,6 @@ class ShardT final : public ShardBase {
     // tile's and each record block's new states, the overflow list's pass B
     // adds its winners to their tiles, one scan positions them all
     const bool tc = tcount_ && !spill_;
-    // (KC_SETTLE_TP own tiles per settle workgroup on the tile-count path)
-    const int tp = tc ? settle_tp_ : 1;
     ClaimKeys ck((uint32_t)rank_);
     if (tlc_) {
       if (!(defer_on_ && tc)) {
@@ -1456,25 +1442,25 @@ class ShardT final : public ShardBase {
       ck.gbits = gbits_cur_;
       ck.grank = grank_cur_;
     }
+    // (one workgroup per own tile: round 5 measured 4 tiles per workgroup
+    // slower at R = 8)
     auto settle = [&](int pass, unsigned ob_blocks, uint32_t* wt) {
-      const unsigned tb = (lt + tp - 1) / tp, g = std::max(tb + rb + ob_blocks, 1u);
-#define KC_SB(P, T)                                                                                         \
-  hipLaunchKernelGGL((k_settle_both<M, P, T>), dim3(g), dim3(256), 0, st_, lt, rb, n_, cs_.t, cs_.nslots,   \
-                     succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, \
-                     isnew_, d_ctr_, ovf_, wt)
-      if (pass == 0) {
-        if (tp == 2) KC_SB(0, 2); else if (tp == 4) KC_SB(0, 4); else if (tp == 8) KC_SB(0, 8); else KC_SB(0, 1);
-      } else {
-        if (tp == 2) KC_SB(1, 2); else if (tp == 4) KC_SB(1, 4); else if (tp == 8) KC_SB(1, 8); else KC_SB(1, 1);
-      }
-#undef KC_SB
+      const unsigned g = std::max(lt + rb + ob_blocks, 1u);
+      if (pass == 0)
+        hipLaunchKernelGGL((k_settle_both<M, 0>), dim3(g), dim3(256), 0, st_, lt, rb, n_, cs_.t, cs_.nslots,
+                           succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, isnew_, d_ctr_,
+                           ovf_, wt);
+      else
+        hipLaunchKernelGGL((k_settle_both<M, 1>), dim3(g), dim3(256), 0, st_, lt, rb, n_, cs_.t, cs_.nslots,
+                           succ_level, ck, rcount_, rec_fp_, rec_lk_, newmask_, in, n, rfp_, flag_, isnew_, d_ctr_,
+                           ovf_, wt);
     };
     settle(0, ob, (uint32_t*)nullptr);
     if (tc) {
       KC_TRY(grow_buffer(wtot_, wtot_cap_, (uint64_t)lt + rb + 8, false, st_));
       KC_TRY(grow_buffer(woff_, woff_cap_, (uint64_t)lt + rb + 8, false, st_));
       if (lt + rb) settle(1, 0, wtot_);
-      if (n_ && fuse_scan_ && n_ <= FUSE_OVF_SCAN_MAX) {
+      if (n_ && n_ <= FUSE_OVF_SCAN_MAX) {
         hipLaunchKernelGGL(k_ovf_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ovf_, n_, cs_.t, cs_.nslots,
                            succ_level, newmask_, d_ctr_, ck, wtot_, lt, rb, woff_);
       } else {
@@ -2185,8 +2171,6 @@ class ShardT final : public ShardBase {
   double rec_ratio_ = 1.0;             // records sent per parent, last level (the staging estimate)
   // the tile-count insert path: own tiles' and record blocks' new-state counts, their scan
   bool tcount_ = true;
-  bool fuse_scan_ = true;              // small levels: k_ovf_win_scan (KC_FUSE_SCAN)
-  int settle_tp_ = SETTLE_TP_DEFAULT;
   uint32_t *wtot_ = nullptr, *woff_ = nullptr;
   uint64_t wtot_cap_ = 0, woff_cap_ = 0;
   // the deferred frontier (set_deferred; the native loop's counted levels)

@@ -615,7 +615,7 @@ def bench_sharded(args, kw: dict, desc: str, golden_check=None) -> Optional[dict
     # inserter of a state owns it (TLC -workers N semantics; counts, widths and
     # depth checked against the golden below); --deterministic-shards keeps the
     # (rank, parent)-ordered minimum claims and their settle passes
-    first = not getattr(args, "deterministic_shards", False)
+    first = not (getattr(args, "deterministic", False) or getattr(args, "deterministic_shards", False))
     cfg = ModelConfig(**kw, device=local, fpset_slots=1 << 20, timing=0 if args.no_timing else 2, first_claim=first)
     native = os.environ.get("KC_PY_DRIVER", "0") != "1"
     if native:                                        # the C++ level loop over RCCL

@@ -34,6 +34,50 @@ first)
   done
   ATTR_ARGS=--first bash tools/gpu.sh attr ${TAG}_attr 8 || exit 1
   ;;
+split)
+  # the split claim (KC_SPLIT): engine tests with it on, then same-box NP=2 A/B
+  step tests
+  KC_SPLIT=4 timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread -k "enlarged_full or first_claim or error_paths or deferred or model1" > $O/tests.log 2>&1 \
+    || { echo TESTS_FAIL; grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
+  tail -3 $O/tests.log
+  bash tools/gpu.sh ab-env ${TAG}_ab - KC_SPLIT=2 KC_SPLIT=4 KC_SPLIT=8 || exit 1
+  ;;
+trace)
+  # rocprofv3 kernel trace of one NP=2 bench check under the given env (e.g. KC_SPLIT=2)
+  cd /tmp
+  step trace
+  env $3 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-first-claim-line > $O/trace.log 2>&1 \
+    || { echo TRACE_FAIL; tail -20 $O/trace.log; exit 1; }
+  cd $R
+  f=$(ls $O/trace/*/*kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] && head -12 "$f"
+  ;;
+graph)
+  # the narrow batch as a hipGraph (KC_NARROW_GRAPH=1): Model_1 tests with it on, Model_1 A/B, the new NP=2 line
+  step tests
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $O/tests_all.log 2>&1 || { echo TESTS_FAIL; grep -E "FAIL|Error" $O/tests_all.log | head; tail -30 $O/tests_all.log; exit 1; }
+  tail -2 $O/tests_all.log
+  KC_NARROW_GRAPH=1 timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread -k "model1 or error_paths or narrow" > $O/tests.log 2>&1 \
+    || { echo TESTS_FAIL; grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
+  tail -2 $O/tests.log
+  i=0
+  for rep in 1 2; do
+    for v in - KC_NARROW_GRAPH=1; do
+      i=$((i+1)); step "model1 [$v] $rep"
+      if [ "$v" = "-" ]; then E=""; else E="$v"; fi
+      env $E timeout -k 10 300 python -u bench.py --workload model1 --steps 20 --warmup 2 --no-cpu-baseline \
+        > $O/m1_$i.json 2> $O/m1_$i.err || { echo M1_FAIL; tail -20 $O/m1_$i.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/m1_$i.json'));print(d['ms_per_step'], d.get('kernel_ms_per_step'))"
+    done
+  done
+  step bench_np2
+  timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_np2.json 2> $O/bench_np2.err \
+    || { echo BENCH_FAIL; tail -20 $O/bench_np2.err; exit 1; }
+  cat $O/bench_np2.json
+  ;;
 *)
   sed -n 1,8p tools/gpu_r06.sh
   exit 2
