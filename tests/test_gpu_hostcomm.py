@@ -54,6 +54,17 @@ CASES = [
     {"name": "variant3_tlc", "kw": {"variant": 3, "tlc_order": True}},
     {"name": "ns0_tlc", "kw": {"ns": 0, "tlc_order": True}},
     {"name": "lost_update_tlc", "kw": {"variant": 1, "invariants": 7, "tlc_order": True}},
+    # round 6: first-claim claims (ModelConfig.first_claim) across processes
+    {"name": "model1_first", "kw": {"first_claim": True}},
+    {"name": "model1_first_counted", "kw": {"first_claim": True}, "env": {"KC_SNARROW": "0"}},
+    {"name": "np2_40_first", "kw": {"np": 2, "max_levels": 40, "first_claim": True}},
+    {"name": "nc2_first", "kw": {"nc": 2, "first_claim": True}, "env": {"KC_SNARROW": "0"}},
+    {"name": "variant2_first", "kw": {"variant": 2, "first_claim": True}, "env": {"KC_SNARROW": "0"}},
+    {"name": "ns0_first", "kw": {"ns": 0, "first_claim": True}},
+    {"name": "lost_update_first", "kw": {"variant": 1, "invariants": 7, "first_claim": True},
+     "env": {"KC_SNARROW": "0"}},
+    {"name": "fault_first", "kw": {"first_claim": True}, "env": {"KC_FAULT": "1:7:2", "KC_SNARROW": "0"},
+     "all_ranks": True},
 ]
 
 
@@ -176,6 +187,40 @@ def test_deferred_counted_levels(results, fixtures):
         assert "exception" not in r, r.get("exception")
         assert r["error"] == "invariant" and r["error_invariant"] == "NoLostUpdate", name
         assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), name
+
+
+def test_first_claim(results, fixtures, oracle):
+    # first-claim claims over gloo: counts exact, every error at the fixture's
+    # level with a trace of the fixture's length that is a real behaviour
+    world, res = results
+    fx = fixtures["model1"]
+    for name in ("model1_first", "model1_first_counted"):
+        r = res[name][0]
+        assert "exception" not in r, (name, r.get("exception"))
+        assert r["claim_mode"] == "first" and r["complete"] and r["level_width"] == fx["level_width"], name
+        assert (r["distinct"], r["generated"]) == (fx["distinct"], fx["generated"]) and r["act_gen"] == fx["act_gen"]
+        assert sum(r["act_dist"].values()) + r["init"] == r["distinct"]
+    r, fk = res["np2_40_first"][0], fixtures["np2_40levels"]
+    assert "exception" not in r, r.get("exception")
+    assert r["level_width"] == fk["level_width"] and r["act_gen"] == fk["act_gen"]
+    for key, name, kind, kw in (("nc2", "nc2_first", "assertion", dict(nc=2)),
+                                ("variant2", "variant2_first", "invariant", dict(variant=2)),
+                                ("ns0", "ns0_first", "deadlock", dict(ns=0)),
+                                ("variant1_lost_update", "lost_update_first", "invariant",
+                                 dict(variant=1, invariants=7))):
+        r, fk = res[name][0], fixtures[key]
+        assert "exception" not in r, (name, r.get("exception"))
+        assert r["error"] == kind, name
+        assert (r["error_level"], r["trace_len"]) == (fk["err_level"], fk["trace_len"]), name
+        cfg = oracle.config(nc=kw.get("nc", 1), ns=kw.get("ns", 1), variant=kw.get("variant", 0),
+                            invariants=kw.get("invariants", 3))
+        for a, b in zip(r["trace"], r["trace"][1:]):
+            succ, _ = oracle.successors(cfg, a)
+            assert any(list(map(int, x)) == b for _, x in succ), name
+    got = res["fault_first"]
+    assert sorted(got) == list(range(world))
+    for rk, r in got.items():
+        assert "exception" in r and ("injected fault" in r["exception"] or "failed" in r["exception"])
 
 
 def test_fault_stops_every_rank(results):

@@ -78,6 +78,28 @@ graph)
     || { echo BENCH_FAIL; tail -20 $O/bench_np2.err; exit 1; }
   cat $O/bench_np2.json
   ;;
+abtest)
+  # tests under an env setting ($3), then same-box NP=2 benches: default vs $3 (twice each)
+  step tests
+  env $3 timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread -k "${TESTK:-first_claim}" > $O/tests.log 2>&1 \
+    || { echo TESTS_FAIL; grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -30 $O/tests.log; exit 1; }
+  tail -2 $O/tests.log
+  bash tools/gpu.sh ab-env ${TAG}_ab - "$3" || exit 1
+  ;;
+power)
+  # power and clocks sampled while NP=2 checks run (is k_claim power/clock-limited?)
+  step idle
+  timeout 20 rocm-smi --showpower --showclocks > $O/idle.txt 2>&1; grep -iE "power|sclk|mclk|fclk" $O/idle.txt | head -8
+  step run
+  ( for k in $(seq 1 60); do echo "== t $k"; timeout 5 rocm-smi --showpower --showclocks 2>&1 | grep -iE "power|sclk|mclk"; sleep 0.2; done ) > $O/busy.txt 2>&1 &
+  SP=$!
+  timeout -k 10 300 python -u bench.py --steps 40 --warmup 1 --no-cpu-baseline --no-second-line > $O/bench.json 2> $O/bench.err \
+    || { echo BENCH_FAIL; tail -20 $O/bench.err; kill $SP; exit 1; }
+  wait $SP
+  python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'], d['kernel_ms_per_step'])"
+  grep -iE "power|sclk" $O/busy.txt | sort | uniq -c | sort -rn | head -20
+  ;;
 *)
   sed -n 1,8p tools/gpu_r06.sh
   exit 2
