@@ -184,6 +184,12 @@ def claim_ceiling():
     return None, None
 
 
+def claimset_compact(first: bool) -> bool:
+    """The engine's first-claim ClaimSet holds 8-B fp words (round 6,
+    DevClaimSet::compact) unless KC_CLAIM_COMPACT=0."""
+    return first and os.environ.get("KC_CLAIM_COMPACT", "1") != "0"
+
+
 def op_rate_roofline(kclaim_ms: float, probes: int, inserts: int, checks: int, first: bool) -> dict:
     """The roofline that bounds k_claim: its random memory
     OPERATIONS — per check every ClaimSet claim is one first-slot 16-B load,
@@ -209,6 +215,8 @@ def op_rate_roofline(kclaim_ms: float, probes: int, inserts: int, checks: int, f
         out["source"] = "no committed claim-ceiling profile"
         return out
     mode = "first" if first else "deterministic"
+    if claimset_compact(first) and "first_compact" in cal["ceiling_ms"]:
+        mode = "first_compact"      # (the same claims on the compact table the engine uses)
     per_check = cal["ceiling_ms"][mode]
     ceil_ms = per_check * (probes / max(checks, 1)) / cal["per_check"]["claims"] * checks
     iso = cal["isolated_64GiB_G_per_s"]
@@ -418,6 +426,7 @@ def bench_single(args, kw, desc):
                               "the winning copy of a same-level duplicate is not deterministic)"
                               if r.claim_mode == "first" else "sequential-BFS minimum (TLC -workers 1 order)"),
                    "claim_mode": r.claim_mode,
+                   "claimset": f"{r.fpset_slots} slots x {8 if claimset_compact(r.claim_mode == 'first') else 16} B",
                    "cold_first_check_note": "the first (warmup) check of a fresh engine, its ClaimSet grown by "
                                             "rehash from 2^20 slots; the timed checks reuse the grown table "
                                             "(cleared each check), like TLC's -fpmem pre-sizing"},

@@ -443,3 +443,29 @@ def test_first_claim_errors(fixtures, oracle, monkeypatch, key, kw, kind):
     # from the states k_claim rebuilt, an invariant violation among them as
     # the level before's (no redo of the whole run from Init)
     assert r.claim_mode == "first" and not r.defer_fallback, (r.defer_fallback, r.defer_redo_level)
+
+
+# --- round 6: the compact ClaimSet of the first-claim mode (8-B fp-word
+# slots, DevClaimSet::compact; KC_CLAIM_COMPACT=0 keeps 16-B slots): the same
+# counts through the wide and narrow paths and the rehash growth (NP=2's 40
+# levels grow the table from 2^20 slots), and the same fingerprint set
+# (check_fps' minimum gap over every stored fingerprint equals the default
+# mode's, whose table holds the same states)
+def test_first_claim_compact(model1, fixtures, monkeypatch):
+    with ModelChecker(ModelConfig()) as mc:
+        mc.run()
+        gap0, _ = mc.check_fps()
+    fx = fixtures["np2_40levels"]
+    for compact in ("1", "0"):
+        monkeypatch.setenv("KC_CLAIM_COMPACT", compact)
+        with ModelChecker(ModelConfig(first_claim=True)) as mc:
+            r = mc.run()
+            gap, _ = mc.check_fps()
+            assert r.claim_mode == "first" and r.complete
+            assert (r.distinct, r.generated, r.depth) == (model1.distinct, model1.generated, model1.depth)
+            assert r.level_width == model1.level_width and gap == gap0
+            r = mc.run()                      # the kept table, cleared (compact: half the bytes)
+            assert r.level_width == model1.level_width
+        r = run(np=2, max_levels=40, first_claim=True)
+        assert r.level_width == fx["level_width"] and r.act_gen == fx["act_gen"]
+        assert r.fpset_slots >= 1 << 21       # grown by rehash

@@ -132,13 +132,15 @@ k_counters_restore(Counters* __restrict__ C, const CtrStripe* __restrict__ prev,
 }
 
 // fingerprints of a ClaimSet into a dense array (order irrelevant: sorted next)
-__global__ void k_claimset_fps(const ClaimEntry* __restrict__ t, uint64_t nslots,
+// (csh: slot i's fp word is word i << csh, DevClaimSet::word_shift)
+__global__ void k_claimset_fps(const unsigned long long* __restrict__ w, uint64_t nslots, uint32_t csh,
                                unsigned long long* __restrict__ out, uint64_t cap,
                                unsigned long long* __restrict__ n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (t[i].fp) {
+    const unsigned long long fp = w[i << csh];
+    if (fp) {
       const unsigned long long k = atomicAdd(n, 1ull);
-      if (k < cap) out[k] = t[i].fp;
+      if (k < cap) out[k] = fp;
     }
   }
 }
@@ -203,6 +205,10 @@ class EngineT final : public EngineBase {
     // dropped: a deferred-frontier capacity anomaly redoes the run from Init;
     // an Assert or deadlock key is reported directly, as on the exact path)
     if (first_claim_) redo_on_ = false;
+    // its ClaimSet holds fp words only (8-B slots: half the table to clear);
+    // KC_CLAIM_COMPACT=0 keeps 16-B slots (A/B)
+    const char* cc = getenv("KC_CLAIM_COMPACT");
+    cs_.compact = first_claim_ && !(cc && cc[0] == '0');
   }
   ~EngineT() override { release(); }
 
@@ -473,9 +479,14 @@ class EngineT final : public EngineBase {
           if (first_claim_) {
             ShardArgs fa = claim_args_;
             fa.ttot = ttot_;
-            hipLaunchKernelGGL((k_claim<M, 0, false, 0, false, true>), dim3(tiles), dim3(CLAIM_TILE), 0, st_,
-                               cur_ + start, cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
-                               abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, fa, df);
+            if (cs_.compact)
+              hipLaunchKernelGGL((k_claim<M, 0, false, 0, false, true, true>), dim3(tiles), dim3(CLAIM_TILE), 0, st_,
+                                 cur_ + start, cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
+                                 abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, fa, df);
+            else
+              hipLaunchKernelGGL((k_claim<M, 0, false, 0, false, true>), dim3(tiles), dim3(CLAIM_TILE), 0, st_,
+                                 cur_ + start, cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
+                                 abl_mask_, rcount_, rec_fp_, rec_lk_, newmask_, d_ctr_, fa, df);
           } else {
             hipLaunchKernelGGL(k_claim<M>, dim3(tiles), dim3(CLAIM_TILE), 0, st_, cur_ + start, cn,
                                start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
@@ -729,7 +740,7 @@ class EngineT final : public EngineBase {
       (void)hipMemsetAsync(d_n, 0, 8, st_);
       (void)hipMemcpyAsync(d_n + 1, &gap, 8, hipMemcpyHostToDevice, st_);
       hipLaunchKernelGGL(k_claimset_fps, dim3(table_grid(cs_.nslots)), dim3(256), 0, st_,
-                         cs_.t, cs_.nslots, a, cnt, d_n);
+                         cs_.words(), cs_.nslots, cs_.word_shift(), a, cnt, d_n);
       (void)hipMemcpyAsync(&n, d_n, 8, hipMemcpyDeviceToHost, st_);
       if (hipStreamSynchronize(st_) != hipSuccess || n > cnt) {
         set_error("kc_engine_check_fps: fingerprint count %llu > %llu", n, (unsigned long long)cnt);
@@ -975,7 +986,7 @@ class EngineT final : public EngineBase {
       res->seen_cold_hits = hits;
       res->seen_cold_runs = cst.runs;
       res->seen_disk_bytes = cst.disk_written;
-      res->seen_peak_hbm_bytes = cs_.nslots * sizeof(ClaimEntry) + sp_arena_bytes_ + cst.peak_meta_bytes;
+      res->seen_peak_hbm_bytes = cs_.nslots * cs_.slot_bytes() + sp_arena_bytes_ + cst.peak_meta_bytes;
       res->seen_filter_tests = cst.filter_tests;
       res->seen_filter_passed = cst.filter_passed;
       res->seen_merges = cst.merges;
@@ -1094,7 +1105,7 @@ class EngineT final : public EngineBase {
         for (int k = 0; k < narrow_batch_; ++k, ++lev)
           hipLaunchKernelGGL(k_nfinish<M>, dim3(NARROW_FWG), dim3(NARROW_THREADS), 0, st_, a, b, flags_,
                              cfg_.check_deadlock, parent_, ord_, cfg_.keep_trace, lev, d_ns_, d_nsc_, cs_.t,
-                             cs_.nslots, d_ctr_, d_ntrace_);
+                             cs_.nslots, d_ctr_, d_ntrace_, cs_.word_shift());
       });
       KC_HIP_TRY(hipGetLastError());
       KC_HIP_TRY(hipMemcpyAsync(h_ns_, d_ns_, offsetof(NarrowCtl, close_acc), hipMemcpyDeviceToHost, st_));

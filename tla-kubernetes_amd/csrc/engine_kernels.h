@@ -759,7 +759,9 @@ static __device__ unsigned long long g_ctrace[16];
 // Counts, widths and trace lengths are the exact path's; which copy of a
 // same-level duplicate wins (its parent, its action's distinct count) is
 // not deterministic, as in a multi-worker TLC run.
-template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false, bool FIRST = false>
+// C8 (FIRST only): the compact ClaimSet, u64 fp words (DevClaimSet::compact)
+template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false, bool FIRST = false,
+          bool C8 = false>
 __global__ void __launch_bounds__(CLAIM_TILE)
 __attribute__((amdgpu_waves_per_eu(6, 6)))
 k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Flags f,
@@ -768,6 +770,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh, DeferArgs df = DeferArgs{}) {
   constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
+  static_assert(!C8 || FIRST, "the compact ClaimSet holds no claim words");
+  unsigned long long* const cs8 = reinterpret_cast<unsigned long long*>(cs);
   // (one stripe of action counters on the sharded path: OWN's projections
   // take that LDS, and 6 workgroups per CU need it)
   constexpr int AS = OWN ? 1 : ACT_STRIPES;
@@ -1030,7 +1034,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         ++probes;
         const uint64_t pidx = base + tile0 + KC_LP;
         const uint64_t b = bucket_of(fp, nbuckets);
-        const int r = FIRST ? claimset_insert_from(cs, nbuckets, fp, b, cs[b].fp)
+        const int r = C8      ? fpslots_insert_from(cs8, nbuckets, fp, b, cs8[b])
+                    : FIRST ? claimset_insert_from(cs, nbuckets, fp, b, cs[b].fp)
                             : claimset_claim_store(cs, nbuckets, fp, make_claim(level, okey(pidx, (uint64_t)t)), level);
         KC_DIAG_OUT(r);
         if (r == CL_NEW)
@@ -1093,7 +1098,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       fpq[q] = k < nrep ? sh_fp[k] : 0ull;
       if (fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank)) {
         iq[q] = bucket_of(fpq[q], nbuckets);
-        eq[q] = claimset_first(cs, iq[q]);
+        eq[q] = C8 ? make_ulonglong2(cs8[iq[q]], 0ull) : claimset_first(cs, iq[q]);
       }
     }
 #if KC_CLAIM_PIPE
@@ -1103,7 +1108,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       const int k = k0 + q * CLAIM_TILE;
       cq[q] = ~0ull;
       if (k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank) && eq[q].x == 0ull)
-        cq[q] = atomicCAS(&cs[iq[q]].fp, 0ull, fpq[q]);
+        cq[q] = atomicCAS(C8 ? &cs8[iq[q]] : &cs[iq[q]].fp, 0ull, fpq[q]);
     }
 #endif
 #pragma unroll
@@ -1131,6 +1136,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
           __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         r = CL_NEW;
+      } else if (C8) {
+        r = fpslots_insert_from(cs8, nbuckets, fp, iq[q], cq[q] != ~0ull ? cq[q] : eq[q].x);
       } else if (FIRST) {
         r = claimset_insert_from(cs, nbuckets, fp, iq[q], cq[q] != ~0ull ? cq[q] : eq[q].x);
       } else {

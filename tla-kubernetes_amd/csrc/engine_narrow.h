@@ -322,7 +322,10 @@ __global__ void __launch_bounds__(NARROW_THREADS)
 k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ bufB, Flags f,
           int check_deadlock, unsigned long long* __restrict__ parent, uint8_t* __restrict__ ord, int keep_trace,
           uint32_t lev, NarrowCtl* __restrict__ ctl, NarrowScratch* __restrict__ sc, ClaimEntry* __restrict__ cs,
-          uint64_t nslots, Counters* __restrict__ C, unsigned long long* __restrict__ ntrace) {
+          uint64_t nslots, Counters* __restrict__ C, unsigned long long* __restrict__ ntrace, uint32_t csh = 1) {
+  // (csh: slot i's fp word is word i << csh — 1 for 16-B ClaimEntry slots,
+  // 0 for the compact set of the first-claim mode, which has no claim words)
+  unsigned long long* const csw = reinterpret_cast<unsigned long long*>(cs);
   using State = typename M::State;
   const uint64_t g = (uint64_t)blockIdx.x * NARROW_THREADS + threadIdx.x;
   const uint64_t i = g / NARROW_ESUB;
@@ -397,7 +400,7 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
       const bool first = t < tot && (unsigned int)~(unsigned int)e[k].y == key;
       e[k].x = first ? e[k].x : 0ull;
       ixs[k] = first ? bucket_of(e[k].x, nslots) : 0ull;
-      os[k] = first ? atomicCAS(&cs[ixs[k]].fp, 0ull, e[k].x) : 0ull;
+      os[k] = first ? atomicCAS(&csw[ixs[k] << csh], 0ull, e[k].x) : 0ull;
     }
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
@@ -409,10 +412,10 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
       unsigned long long o = os[k];
       for (uint64_t q = 1; o != 0ull && o != fp && q < nslots; ++q) {
         ix = (ix + 1 == nslots) ? 0 : ix + 1;
-        o = atomicCAS(&cs[ix].fp, 0ull, fp);
+        o = atomicCAS(&csw[ix << csh], 0ull, fp);
       }
       if (o == 0ull) {
-        cs[ix].nclaim = ~make_claim(succ_level, (i << 8) | (uint64_t)t);
+        if (csh) csw[(ix << 1) + 1] = ~make_claim(succ_level, (i << 8) | (uint64_t)t);
         mine |= 1u << t;
       } else if (o != fp) {
         atomicAdd(&C->overflow, 1ull);               // a full table: fail loudly (as shard_narrow.h)

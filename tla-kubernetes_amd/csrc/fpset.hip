@@ -107,11 +107,12 @@ int DevFpset::reserve(uint64_t extra, hipStream_t st) {
 // grid-stride loop of 8192 workgroups (64 GiB in 9.9-10.1 ms against 10.8-10.9
 // for hipMemsetAsync, profiles/r03ap_clear.txt).
 typedef unsigned int kc_u32x4 __attribute__((ext_vector_type(4)));
-__global__ void __launch_bounds__(256) k_claimset_clear(ClaimEntry* __restrict__ t, uint64_t nslots) {
+// (n16: the table's size in 16-B units — nslots, or nslots / 2 compact)
+__global__ void __launch_bounds__(256) k_claimset_clear(ClaimEntry* __restrict__ t, uint64_t n16) {
   kc_u32x4* p = reinterpret_cast<kc_u32x4*>(t);
   const kc_u32x4 z = {0u, 0u, 0u, 0u};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride)
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
     __builtin_nontemporal_store(z, &p[i]);
 }
 
@@ -146,9 +147,34 @@ __global__ void k_claimset_insert_list(const uint64_t* __restrict__ fps, uint64_
   }
 }
 
+// the compact table's rehash and list insert (fp words only)
+__global__ void k_fpslots_rehash(const unsigned long long* __restrict__ old, uint64_t old_slots,
+                                 unsigned long long* __restrict__ nw, uint64_t new_slots,
+                                 unsigned long long* __restrict__ fail) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < old_slots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long fp = old[i];
+    if (!fp) continue;
+    const uint64_t k = bucket_of(fp, new_slots);
+    if (fpslots_insert_from(nw, new_slots, fp, k, nw[k]) != CL_NEW) atomicAdd(fail, 1ull);
+  }
+}
+__global__ void k_fpslots_insert_list(const uint64_t* __restrict__ fps, uint64_t n, unsigned long long* __restrict__ t,
+                                      uint64_t nslots, int* __restrict__ result) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint64_t k = bucket_of(fps[i], nslots);
+    const int r = fpslots_insert_from(t, nslots, fps[i], k, t[k]);
+    if (result) result[i] = r;
+  }
+}
+
 void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevClaimSet& cs,
                                  uint32_t level, int* d_res, hipStream_t st) {
-  if (n)
+  if (n && cs.compact)
+    hipLaunchKernelGGL(k_fpslots_insert_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d_fps, n, cs.words(), cs.nslots, d_res);
+  else if (n)
     hipLaunchKernelGGL(k_claimset_insert_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        d_fps, n, cs.t, cs.nslots, level, d_res);
 }
@@ -156,8 +182,8 @@ void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevCla
 int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
   release();
   nslots = min_slots < 64 ? 64 : min_slots;
-  KC_HIP_TRY(hipMalloc(&t, nslots * sizeof(ClaimEntry)));
-  KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * sizeof(ClaimEntry), st));
+  KC_HIP_TRY(hipMalloc(&t, nslots * slot_bytes()));
+  KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * slot_bytes(), st));
   KC_HIP_TRY(hipMalloc(&d_fail, sizeof(unsigned long long)));
   count = 0;
   return 0;
@@ -167,9 +193,9 @@ int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
 // table against hipMemsetAsync's 6.3, round 3)
 int DevClaimSet::clear(hipStream_t st) {
   if (nslots < (1u << 20)) {
-    KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * sizeof(ClaimEntry), st));
+    KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * slot_bytes(), st));
   } else {
-    hipLaunchKernelGGL(k_claimset_clear, dim3(8192u), dim3(256), 0, st, t, nslots);
+    hipLaunchKernelGGL(k_claimset_clear, dim3(8192u), dim3(256), 0, st, t, nslots * slot_bytes() / 16);
     KC_HIP_TRY(hipGetLastError());
   }
   count = 0;
@@ -201,17 +227,21 @@ int DevClaimSet::reserve(uint64_t extra, hipStream_t st) {
   while (need * (ld + 1) > ns) ns *= 2;
   while (need * 2 > ns_min) ns_min *= 2;
   ClaimEntry* nt = nullptr;
-  if (hipMalloc(&nt, ns * sizeof(ClaimEntry)) != hipSuccess) {
+  if (hipMalloc(&nt, ns * slot_bytes()) != hipSuccess) {
     (void)hipGetLastError();
     nt = nullptr;
     ns = ns_min;
     if (ns == nslots) return 0;                    // (still <= 1/2 after this batch)
-    KC_HIP_TRY(hipMalloc(&nt, ns * sizeof(ClaimEntry)));
+    KC_HIP_TRY(hipMalloc(&nt, ns * slot_bytes()));
   }
-  KC_HIP_TRY(hipMemsetAsync(nt, 0, ns * sizeof(ClaimEntry), st));
+  KC_HIP_TRY(hipMemsetAsync(nt, 0, ns * slot_bytes(), st));
   KC_HIP_TRY(hipMemsetAsync(d_fail, 0, sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_claimset_rehash, dim3(table_grid(nslots)), dim3(256), 0, st,
-                     t, nslots, nt, ns, d_fail);
+  if (compact)
+    hipLaunchKernelGGL(k_fpslots_rehash, dim3(table_grid(nslots)), dim3(256), 0, st,
+                       words(), nslots, reinterpret_cast<unsigned long long*>(nt), ns, d_fail);
+  else
+    hipLaunchKernelGGL(k_claimset_rehash, dim3(table_grid(nslots)), dim3(256), 0, st,
+                       t, nslots, nt, ns, d_fail);
   KC_HIP_TRY(hipGetLastError());
   unsigned long long fail = 0;
   KC_HIP_TRY(hipMemcpyAsync(&fail, d_fail, sizeof fail, hipMemcpyDeviceToHost, st));

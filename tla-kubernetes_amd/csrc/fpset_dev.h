@@ -240,6 +240,24 @@ __device__ __forceinline__ int claimset_insert_from(ClaimEntry* __restrict__ t, 
   return CL_FULL;
 }
 
+// Compact ClaimSet (round 6; the engine's first-claim mode, DevClaimSet::
+// compact): the claim word is never read there, so a slot is the fp word
+// alone — 8 B instead of 16, half the table to allocate and clear per check
+// for the same slot count and load.  `t` is the u64 slot array.
+__device__ __forceinline__ int fpslots_insert_from(unsigned long long* __restrict__ t, uint64_t nslots, uint64_t fp,
+                                                   uint64_t i, unsigned long long f) {
+  for (uint64_t probe = 0; probe < nslots; ++probe) {
+    if (probe) f = t[i];
+    if (f == 0ull) {
+      f = atomicCAS(&t[i], 0ull, (unsigned long long)fp);
+      if (f == 0ull) return CL_NEW;
+    }
+    if (f == fp) return CL_OLD;
+    i = (i + 1 == nslots) ? 0 : i + 1;
+  }
+  return CL_FULL;
+}
+
 // Settle pass A of a CL_CUR candidate: fold its claim into the slot.
 // Returns the ~claim the slot held before (0 if fp is absent, which the
 // protocol never produces).

@@ -30,14 +30,19 @@ struct DevFpset {
   int reserve(uint64_t extra, hipStream_t st);
 };
 
-// Host owner of the engine's ClaimSet (fpset_dev.h): nslots 16-B entries.
+// Host owner of the engine's ClaimSet (fpset_dev.h): nslots 16-B entries,
+// or (compact, the first-claim mode) nslots u64 fp words at the same address.
 struct DevClaimSet {
   ClaimEntry* t = nullptr;
   uint64_t nslots = 0;
   uint64_t count = 0;                   // host-tracked number of stored fps
   unsigned long long* d_fail = nullptr;
+  bool compact = false;                 // set before init(); fixed for the owner's life
 
   uint64_t capacity() const { return nslots; }
+  uint64_t slot_bytes() const { return compact ? 8 : sizeof(ClaimEntry); }
+  unsigned long long* words() const { return reinterpret_cast<unsigned long long*>(t); }
+  uint32_t word_shift() const { return compact ? 0u : 1u; }   // slot i's fp word: words()[i << word_shift()]
   int init(uint64_t min_slots, hipStream_t st);
   int clear(hipStream_t st);
   void release();
@@ -45,7 +50,7 @@ struct DevClaimSet {
   int reserve(uint64_t extra, hipStream_t st);
 };
 // claim a device list of (normalised) fps at `level` with keys 0..n-1;
-// d_res[i] = ClaimResult (may be NULL)
+// d_res[i] = ClaimResult (may be NULL; a compact set reports CL_NEW / CL_OLD)
 void launch_claimset_insert_list(const uint64_t* d_fps, uint64_t n, const DevClaimSet& cs,
                                  uint32_t level, int* d_res, hipStream_t st);
 

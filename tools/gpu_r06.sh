@@ -100,6 +100,21 @@ power)
   python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'], d['kernel_ms_per_step'])"
   grep -iE "power|sclk" $O/busy.txt | sort | uniq -c | sort -rn | head -20
   ;;
+abk)
+  # same-box NP=2 A/B of env settings (args after the tag; "-" = none) with
+  # HIP events on every kernel, headline mode only, REPS rounds
+  shift 2
+  i=0
+  for rep in $(seq 1 ${REPS:-3}); do
+    for v in "$@"; do
+      i=$((i+1)); step "[$v] $rep"
+      if [ "$v" = "-" ]; then E=""; else E="$v"; fi
+      env $E timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 1 --no-cpu-baseline --no-second-line \
+        --all-kernel-timing $BARGS > $O/run_$i.json 2> $O/run_$i.err || { echo B_FAIL; tail -20 $O/run_$i.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/run_$i.json'));print(d['ms_per_step'], {k: round(v, 2) for k, v in d['kernel_ms_per_step'].items()})"
+    done
+  done
+  ;;
 *)
   sed -n 1,8p tools/gpu_r06.sh
   exit 2

@@ -62,10 +62,12 @@ struct Stats {
   unsigned long long n_new, n_old, n_other, loads;
 };
 
-__global__ void __launch_bounds__(256) k_prefill(ClaimEntry* t, uint64_t ns, uint64_t n0, Stats* st) {
+__global__ void __launch_bounds__(256) k_prefill(ClaimEntry* t, uint64_t ns, uint64_t n0, Stats* st, int compact) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n0) return;
-  const int r = claimset_claim_store(t, ns, fp_a(k), make_claim(1, k), 1);
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(t);
+  const uint64_t f = fp_a(k), b = bucket_of(f, ns);
+  const int r = compact ? fpslots_insert_from(w, ns, f, b, w[b]) : claimset_claim_store(t, ns, f, make_claim(1, k), 1);
   if (r != CL_NEW) atomicAdd(&st->n_other, 1ull);
 }
 
@@ -75,7 +77,9 @@ __device__ __forceinline__ int extras(uint64_t u, uint32_t thr) {
 }
 
 // FIRST = 0: the deterministic STORE-claim protocol (CAS + claim store per
-// new state); 1: first-claim mode (CAS only).
+// new state); 1: first-claim mode (CAS only); 2 (round 6): first-claim mode
+// on the compact ClaimSet of the engine (u64 fp words, fpslots_insert_from,
+// 8-B first-slot loads; `t` is then the u64 slot array).
 template <int K, int FIRST>
 __global__ void __launch_bounds__(256) k_mixed(ClaimEntry* __restrict__ t, uint64_t ns, uint64_t units, uint64_t n0,
                                                uint32_t thr, Stats* st) {
@@ -104,13 +108,15 @@ __global__ void __launch_bounds__(256) k_mixed(ClaimEntry* __restrict__ t, uint6
   for (int q = 0; q < Q; ++q)
     if (q < nq) {
       iq[q] = bucket_of(fq[q], ns);
-      eq[q] = claimset_first(t, iq[q]);
+      eq[q] = FIRST == 2 ? make_ulonglong2(reinterpret_cast<const unsigned long long*>(t)[iq[q]], 0ull)
+                         : claimset_first(t, iq[q]);
     }
   unsigned long long nn = 0, no = 0, nx = 0;
 #pragma unroll
   for (int q = 0; q < Q; ++q)
     if (q < nq) {
-      const int r = FIRST ? claimset_insert_from(t, ns, fq[q], iq[q], eq[q].x)
+      const int r = FIRST == 2 ? fpslots_insert_from(reinterpret_cast<unsigned long long*>(t), ns, fq[q], iq[q], eq[q].x)
+                  : FIRST ? claimset_insert_from(t, ns, fq[q], iq[q], eq[q].x)
                           : claimset_claim_store_from(t, ns, fq[q], make_claim(2, u0 * 4 + q), 2, iq[q], eq[q]);
       if (r == CL_NEW) ++nn;
       else if (r == CL_OLD) ++no;
@@ -195,19 +201,22 @@ int main(int argc, char** argv) {
          (unsigned long long)ns, (unsigned long long)niso, niso / ms_load / 1e6, niso / ms_cas / 1e6,
          niso / ms_store / 1e6);
   fflush(stdout);
-  double best[2] = {1e30, 1e30};
-  int bestk[2] = {0, 0};
-  for (int first = 0; first < 2; ++first) {
+  double best[3] = {1e30, 1e30, 1e30};
+  int bestk[3] = {0, 0, 0};
+  for (int first = 0; first < 3; ++first) {
     for (int K : {1, 2, 4}) {
       for (int rep = 0; rep < 2; ++rep) {
         CK(hipMemset(t, 0, ns * sizeof(ClaimEntry)));
         CK(hipMemset(st, 0, 64 * sizeof(Stats)));
-        hipLaunchKernelGGL(k_prefill, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, 0, t, ns, n0, st);
+        hipLaunchKernelGGL(k_prefill, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, 0, t, ns, n0, st,
+                           first == 2 ? 1 : 0);
         CK(hipDeviceSynchronize());
         const unsigned g = (unsigned)((units + 256ull * K - 1) / (256ull * K));
         const double ms = timed([&] {
 #define KC_MX(KK, FF) hipLaunchKernelGGL((k_mixed<KK, FF>), dim3(g), dim3(256), 0, 0, t, ns, units, n0, thr, st)
-          if (first) {
+          if (first == 2) {
+            if (K == 1) KC_MX(1, 2); else if (K == 2) KC_MX(2, 2); else KC_MX(4, 2);
+          } else if (first) {
             if (K == 1) KC_MX(1, 1); else if (K == 2) KC_MX(2, 1); else KC_MX(4, 1);
           } else {
             if (K == 1) KC_MX(1, 0); else if (K == 2) KC_MX(2, 0); else KC_MX(4, 0);
@@ -224,7 +233,7 @@ int main(int argc, char** argv) {
         }
         printf("{\"mode\": \"%s\", \"K\": %d, \"rep\": %d, \"ms\": %.3f, \"units\": %llu, \"new\": %llu, "
                "\"old\": %llu, \"other\": %llu, \"claims\": %llu, \"claims_G_per_s\": %.3f}\n",
-               first ? "first" : "deterministic", K, rep, ms, (unsigned long long)units, nn, no, nx,
+               first == 2 ? "first_compact" : first ? "first" : "deterministic", K, rep, ms, (unsigned long long)units, nn, no, nx,
                nn + no + nx, (nn + no + nx) / ms / 1e6);
         fflush(stdout);
         if (nn != units || nx != 0) {
@@ -241,9 +250,10 @@ int main(int argc, char** argv) {
   }
   printf("{\"summary\": true, \"table_slots\": %llu, \"prefill\": %llu, \"units\": %llu, \"probes\": %llu, "
          "\"deterministic_ms\": %.3f, \"deterministic_K\": %d, \"first_ms\": %.3f, \"first_K\": %d, "
+         "\"first_compact_ms\": %.3f, \"first_compact_K\": %d, "
          "\"iso_load_G_per_s\": %.3f, \"iso_cas_G_per_s\": %.3f, \"iso_store_G_per_s\": %.3f}\n",
          (unsigned long long)ns, (unsigned long long)n0, (unsigned long long)units, (unsigned long long)probes,
-         best[0], bestk[0], best[1], bestk[1], niso / ms_load / 1e6, niso / ms_cas / 1e6, niso / ms_store / 1e6);
+         best[0], bestk[0], best[1], bestk[1], best[2], bestk[2], niso / ms_load / 1e6, niso / ms_cas / 1e6, niso / ms_store / 1e6);
   CK(hipFree(t));
   CK(hipFree(st));
   CK(hipFree(out));
