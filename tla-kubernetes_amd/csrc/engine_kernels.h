@@ -770,7 +770,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh, DeferArgs df = DeferArgs{}) {
   constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
-  static_assert(!C8 || FIRST, "the compact ClaimSet holds no claim words");
+  static_assert(!C8 || (FIRST && !SH), "the compact ClaimSet holds no claim words (the engine's first-claim mode)");
   unsigned long long* const cs8 = reinterpret_cast<unsigned long long*>(cs);
   // (one stripe of action counters on the sharded path: OWN's projections
   // take that LDS, and 6 workgroups per CU need it)
@@ -1033,8 +1033,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         }
         ++probes;
         const uint64_t pidx = base + tile0 + KC_LP;
-        const uint64_t b = bucket_of(fp, nbuckets);
-        const int r = C8      ? fpslots_insert_from(cs8, nbuckets, fp, b, cs8[b])
+        const uint64_t b = C8 ? fpslots_home(fp, nbuckets) : bucket_of(fp, nbuckets);
+        const int r = C8      ? fpslots_insert_pair(cs8, nbuckets, fp, b, fpslots_first(cs8, b))
                     : FIRST ? claimset_insert_from(cs, nbuckets, fp, b, cs[b].fp)
                             : claimset_claim_store(cs, nbuckets, fp, make_claim(level, okey(pidx, (uint64_t)t)), level);
         KC_DIAG_OUT(r);
@@ -1097,8 +1097,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       const int k = k0 + q * CLAIM_TILE;
       fpq[q] = k < nrep ? sh_fp[k] : 0ull;
       if (fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank)) {
-        iq[q] = bucket_of(fpq[q], nbuckets);
-        eq[q] = C8 ? make_ulonglong2(cs8[iq[q]], 0ull) : claimset_first(cs, iq[q]);
+        iq[q] = C8 ? fpslots_home(fpq[q], nbuckets) : bucket_of(fpq[q], nbuckets);
+        eq[q] = C8 ? fpslots_first(cs8, iq[q]) : claimset_first(cs, iq[q]);
       }
     }
 #if KC_CLAIM_PIPE
@@ -1107,8 +1107,12 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     for (int q = 0; q < KC_CLAIM_BATCH; ++q) {
       const int k = k0 + q * CLAIM_TILE;
       cq[q] = ~0ull;
-      if (k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank) && eq[q].x == 0ull)
-        cq[q] = atomicCAS(C8 ? &cs8[iq[q]] : &cs[iq[q]].fp, 0ull, fpq[q]);
+      if (C8) {                                   // (the pair's first empty slot)
+        const uint64_t j = k < nrep && fpq[q] ? fpslots_pair_target(iq[q], eq[q], fpq[q]) : ~0ull;
+        if (j < ~1ull) cq[q] = atomicCAS(&cs8[j], 0ull, fpq[q]);
+      } else if (k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank) && eq[q].x == 0ull) {
+        cq[q] = atomicCAS(&cs[iq[q]].fp, 0ull, fpq[q]);
+      }
     }
 #endif
 #pragma unroll
@@ -1131,13 +1135,13 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
 #if KC_CLAIM_PIPE
       int r;
       const uint64_t claim = make_claim(level, okey(pidx, t));
-      if (cq[q] == 0ull) {                        // this lane's CAS inserted fp (fingerprints are never ~0)
+      if (C8) {
+        r = fpslots_insert_pair(cs8, nbuckets, fp, iq[q], eq[q], cq[q]);
+      } else if (cq[q] == 0ull) {                 // this lane's CAS inserted fp (fingerprints are never ~0)
         if (!FIRST)
           __hip_atomic_store(&cs[iq[q]].nclaim, ~(unsigned long long)claim, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         r = CL_NEW;
-      } else if (C8) {
-        r = fpslots_insert_from(cs8, nbuckets, fp, iq[q], cq[q] != ~0ull ? cq[q] : eq[q].x);
       } else if (FIRST) {
         r = claimset_insert_from(cs, nbuckets, fp, iq[q], cq[q] != ~0ull ? cq[q] : eq[q].x);
       } else {

@@ -399,7 +399,7 @@ k_nfinish(typename M::State* __restrict__ bufA, typename M::State* __restrict__ 
       // (an earlier copy of the level holds the entry: not this lane's)
       const bool first = t < tot && (unsigned int)~(unsigned int)e[k].y == key;
       e[k].x = first ? e[k].x : 0ull;
-      ixs[k] = first ? bucket_of(e[k].x, nslots) : 0ull;
+      ixs[k] = first ? (csh ? bucket_of(e[k].x, nslots) : fpslots_home(e[k].x, nslots)) : 0ull;
       os[k] = first ? atomicCAS(&csw[ixs[k] << csh], 0ull, e[k].x) : 0ull;
     }
 #pragma unroll

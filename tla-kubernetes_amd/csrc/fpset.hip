@@ -155,16 +155,16 @@ __global__ void k_fpslots_rehash(const unsigned long long* __restrict__ old, uin
        i += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long fp = old[i];
     if (!fp) continue;
-    const uint64_t k = bucket_of(fp, new_slots);
-    if (fpslots_insert_from(nw, new_slots, fp, k, nw[k]) != CL_NEW) atomicAdd(fail, 1ull);
+    const uint64_t k = fpslots_home(fp, new_slots);
+    if (fpslots_insert_pair(nw, new_slots, fp, k, fpslots_first(nw, k)) != CL_NEW) atomicAdd(fail, 1ull);
   }
 }
 __global__ void k_fpslots_insert_list(const uint64_t* __restrict__ fps, uint64_t n, unsigned long long* __restrict__ t,
                                       uint64_t nslots, int* __restrict__ result) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const uint64_t k = bucket_of(fps[i], nslots);
-    const int r = fpslots_insert_from(t, nslots, fps[i], k, t[k]);
+    const uint64_t k = fpslots_home(fps[i], nslots);
+    const int r = fpslots_insert_pair(t, nslots, fps[i], k, fpslots_first(t, k));
     if (result) result[i] = r;
   }
 }

@@ -243,7 +243,16 @@ __device__ __forceinline__ int claimset_insert_from(ClaimEntry* __restrict__ t, 
 // Compact ClaimSet (round 6; the engine's first-claim mode, DevClaimSet::
 // compact): the claim word is never read there, so a slot is the fp word
 // alone — 8 B instead of 16, half the table to allocate and clear per check
-// for the same slot count and load.  `t` is the u64 slot array.
+// for the same slot count and load.  `t` is the u64 slot array.  A
+// fingerprint's home is an even slot (fpslots_home), so the first probe is
+// one aligned 16-B load of the pair {home, home + 1} (fpslots_insert_pair):
+// a probe run of two slots costs one round trip instead of two.
+__device__ __forceinline__ uint64_t fpslots_home(uint64_t fp, uint64_t nslots) {
+  return bucket_of(fp, nslots >> 1) << 1;
+}
+__device__ __forceinline__ ulonglong2 fpslots_first(const unsigned long long* __restrict__ t, uint64_t home) {
+  return *reinterpret_cast<const ulonglong2*>(t + home);
+}
 __device__ __forceinline__ int fpslots_insert_from(unsigned long long* __restrict__ t, uint64_t nslots, uint64_t fp,
                                                    uint64_t i, unsigned long long f) {
   for (uint64_t probe = 0; probe < nslots; ++probe) {
@@ -256,6 +265,30 @@ __device__ __forceinline__ int fpslots_insert_from(unsigned long long* __restric
     i = (i + 1 == nslots) ? 0 : i + 1;
   }
   return CL_FULL;
+}
+
+// From the pair e = {t[home], t[home + 1]} loaded together (home even):
+// CL_OLD when either holds fp; else the CAS into the first that read empty,
+// then linear probing on.  `cas` (~0: not issued) is the result of that CAS
+// when the caller issued it already (fpslots_pair_target).
+__device__ __forceinline__ uint64_t fpslots_pair_target(uint64_t home, ulonglong2 e, uint64_t fp) {
+  if (e.x == fp || e.y == fp) return ~0ull;                       // present: no CAS
+  return e.x == 0ull ? home : e.y == 0ull ? home + 1 : ~1ull;      // ~1: both held other fps
+}
+__device__ __forceinline__ int fpslots_insert_pair(unsigned long long* __restrict__ t, uint64_t nslots, uint64_t fp,
+                                                   uint64_t home, ulonglong2 e, unsigned long long cas = ~0ull) {
+  const uint64_t j = fpslots_pair_target(home, e, fp);
+  if (j == ~0ull) return CL_OLD;
+  if (j == ~1ull) {
+    const uint64_t k = home + 2 == nslots ? 0 : home + 2;
+    return fpslots_insert_from(t, nslots, fp, k, t[k]);
+  }
+  const unsigned long long f = cas != ~0ull ? cas : atomicCAS(&t[j], 0ull, (unsigned long long)fp);
+  if (f == 0ull) return CL_NEW;
+  if (f == fp) return CL_OLD;
+  if (j == home) return fpslots_insert_from(t, nslots, fp, home + 1, e.y);   // (a stale e.y is re-checked by its CAS)
+  const uint64_t k = j + 1 == nslots ? 0 : j + 1;
+  return fpslots_insert_from(t, nslots, fp, k, t[k]);
 }
 
 // Settle pass A of a CL_CUR candidate: fold its claim into the slot.

@@ -66,8 +66,9 @@ __global__ void __launch_bounds__(256) k_prefill(ClaimEntry* t, uint64_t ns, uin
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n0) return;
   unsigned long long* w = reinterpret_cast<unsigned long long*>(t);
-  const uint64_t f = fp_a(k), b = bucket_of(f, ns);
-  const int r = compact ? fpslots_insert_from(w, ns, f, b, w[b]) : claimset_claim_store(t, ns, f, make_claim(1, k), 1);
+  const uint64_t f = fp_a(k), b = fpslots_home(f, ns);
+  const int r = compact ? fpslots_insert_pair(w, ns, f, b, fpslots_first(w, b))
+                        : claimset_claim_store(t, ns, f, make_claim(1, k), 1);
   if (r != CL_NEW) atomicAdd(&st->n_other, 1ull);
 }
 
@@ -78,8 +79,9 @@ __device__ __forceinline__ int extras(uint64_t u, uint32_t thr) {
 
 // FIRST = 0: the deterministic STORE-claim protocol (CAS + claim store per
 // new state); 1: first-claim mode (CAS only); 2 (round 6): first-claim mode
-// on the compact ClaimSet of the engine (u64 fp words, fpslots_insert_from,
-// 8-B first-slot loads; `t` is then the u64 slot array).
+// on the compact ClaimSet of the engine (u64 fp words from an even home
+// slot, fpslots_insert_pair: one aligned 16-B load of the home pair; `t` is
+// then the u64 slot array).
 template <int K, int FIRST>
 __global__ void __launch_bounds__(256) k_mixed(ClaimEntry* __restrict__ t, uint64_t ns, uint64_t units, uint64_t n0,
                                                uint32_t thr, Stats* st) {
@@ -107,15 +109,15 @@ __global__ void __launch_bounds__(256) k_mixed(ClaimEntry* __restrict__ t, uint6
 #pragma unroll
   for (int q = 0; q < Q; ++q)
     if (q < nq) {
-      iq[q] = bucket_of(fq[q], ns);
-      eq[q] = FIRST == 2 ? make_ulonglong2(reinterpret_cast<const unsigned long long*>(t)[iq[q]], 0ull)
+      iq[q] = FIRST == 2 ? fpslots_home(fq[q], ns) : bucket_of(fq[q], ns);
+      eq[q] = FIRST == 2 ? fpslots_first(reinterpret_cast<const unsigned long long*>(t), iq[q])
                          : claimset_first(t, iq[q]);
     }
   unsigned long long nn = 0, no = 0, nx = 0;
 #pragma unroll
   for (int q = 0; q < Q; ++q)
     if (q < nq) {
-      const int r = FIRST == 2 ? fpslots_insert_from(reinterpret_cast<unsigned long long*>(t), ns, fq[q], iq[q], eq[q].x)
+      const int r = FIRST == 2 ? fpslots_insert_pair(reinterpret_cast<unsigned long long*>(t), ns, fq[q], iq[q], eq[q])
                   : FIRST ? claimset_insert_from(t, ns, fq[q], iq[q], eq[q].x)
                           : claimset_claim_store_from(t, ns, fq[q], make_claim(2, u0 * 4 + q), 2, iq[q], eq[q]);
       if (r == CL_NEW) ++nn;
