@@ -759,7 +759,8 @@ static __device__ unsigned long long g_ctrace[16];
 // Counts, widths and trace lengths are the exact path's; which copy of a
 // same-level duplicate wins (its parent, its action's distinct count) is
 // not deterministic, as in a multi-worker TLC run.
-// C8 (FIRST only): the compact ClaimSet, u64 fp words (DevClaimSet::compact)
+// C8 (FIRST only): the compact ClaimSet, u64 fp words (DevClaimSet::compact;
+// the engine's and the sharded loop's first-claim mode)
 template <class M, int ABL = 0, bool SH = false, int OWN = SH ? 1 : 0, bool TLC = false, bool FIRST = false,
           bool C8 = false>
 __global__ void __launch_bounds__(CLAIM_TILE)
@@ -770,7 +771,7 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
         unsigned long long* __restrict__ rec_fp, unsigned int* __restrict__ rec_lk,
         uint32_t* __restrict__ newmask, Counters* __restrict__ C, ShardArgs sh, DeferArgs df = DeferArgs{}) {
   constexpr int NT = SH ? CLAIM_LDS_SH : CLAIM_LDS;
-  static_assert(!C8 || (FIRST && !SH), "the compact ClaimSet holds no claim words (the engine's first-claim mode)");
+  static_assert(!C8 || (FIRST && !TLC), "the compact ClaimSet holds no claim words (first-claim mode)");
   unsigned long long* const cs8 = reinterpret_cast<unsigned long long*>(cs);
   // (one stripe of action counters on the sharded path: OWN's projections
   // take that LDS, and 6 workgroups per CU need it)
@@ -1108,7 +1109,8 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
       const int k = k0 + q * CLAIM_TILE;
       cq[q] = ~0ull;
       if (C8) {                                   // (the pair's first empty slot)
-        const uint64_t j = k < nrep && fpq[q] ? fpslots_pair_target(iq[q], eq[q], fpq[q]) : ~0ull;
+        const uint64_t j = k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank)
+                               ? fpslots_pair_target(iq[q], eq[q], fpq[q]) : ~0ull;
         if (j < ~1ull) cq[q] = atomicCAS(&cs8[j], 0ull, fpq[q]);
       } else if (k < nrep && fpq[q] && (!SH || owner_of(fpq[q], sh.world) == sh.rank) && eq[q].x == 0ull) {
         cq[q] = atomicCAS(&cs[iq[q]].fp, 0ull, fpq[q]);

@@ -277,7 +277,8 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
 template <class M>
 __global__ void __launch_bounds__(256)
 k_rec_claim_first(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs, uint64_t nslots,
-                  uint32_t* __restrict__ isnew, uint32_t* __restrict__ rtot, Counters* __restrict__ C) {
+                  uint32_t* __restrict__ isnew, uint32_t* __restrict__ rtot, Counters* __restrict__ C,
+                  int compact) {
   __shared__ unsigned int sh_rw[4];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t w = 0;
@@ -286,8 +287,10 @@ k_rec_claim_first(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __re
     uint64_t key;
     load_record<M>(in, i, x, key);
     const uint64_t fp = M::template fingerprint<1>(x);
-    const uint64_t b = bucket_of(fp, nslots);
-    const int r = claimset_insert_from(cs, nslots, fp, b, cs[b].fp);
+    unsigned long long* const w8 = reinterpret_cast<unsigned long long*>(cs);
+    const uint64_t b = compact ? fpslots_home(fp, nslots) : bucket_of(fp, nslots);
+    const int r = compact ? fpslots_insert_pair(w8, nslots, fp, b, fpslots_first(w8, b))
+                          : claimset_insert_from(cs, nslots, fp, b, cs[b].fp);
     if (r == CL_FULL) atomicAdd(&C->overflow, 1ull);
     w = r == CL_NEW ? 1u : 0u;
     isnew[i] = w;
@@ -882,6 +885,9 @@ class ShardT final : public ShardBase {
     // no candidates, no settle passes): the first inserter owns a state, as in
     // a TLC -workers N run
     first_ = cfg.first_claim != 0;
+    // (its ClaimSet holds fp words only, as the engine's in this mode: 8-B
+    // slots, half the table to clear; the narrow levels write no claim words)
+    cs_.compact = first_;
   }
   ~ShardT() override { release(); }
 
@@ -1150,7 +1156,7 @@ class ShardT final : public ShardBase {
       // one rank owns everything: the single-GPU engine's claim kernel (no
       // owner counting; claim keys then carry rank 0, which they do anyway)
       if (first_)
-        hipLaunchKernelGGL((k_claim<M, 0, false, 1, false, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
+        hipLaunchKernelGGL((k_claim<M, 0, false, 1, false, true, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), 0, st_,
                            cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                            (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                            d_ctr_, sh, df);
@@ -1160,7 +1166,7 @@ class ShardT final : public ShardBase {
                            (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                            d_ctr_, sh, df);
     } else if (first_) {
-      hipLaunchKernelGGL((k_claim<M, 0, true, 1, false, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
+      hipLaunchKernelGGL((k_claim<M, 0, true, 1, false, true, true>), dim3((unsigned)tiles), dim3(CLAIM_TILE), dyn, st_,
                          cur_, n_, (uint64_t)0, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots,
                          (uint32_t)level_ + 1, (uint32_t*)nullptr, rcount_, rec_fp_, rec_lk_, newmask_,
                          d_ctr_, sh, df);
@@ -1409,7 +1415,7 @@ class ShardT final : public ShardBase {
       if (n) {
         KC_TRY(grow_buffer(isnew_, isnew_cap_, n, false, st_));
         hipLaunchKernelGGL(k_rec_claim_first<M>, dim3(rgrid), dim3(256), 0, st_, in, n, cs_.t, cs_.nslots, isnew_,
-                           wtot_ + lt, d_ctr_);
+                           wtot_ + lt, d_ctr_, cs_.compact ? 1 : 0);
       }
       hipLaunchKernelGGL(k_win_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, wtot_, lt, rb, woff_, d_ctr_);
       return insert_emit(in, n, true, n_new, err_key);
@@ -1831,7 +1837,7 @@ class ShardT final : public ShardBase {
     if (world_ > 1)
       hipLaunchKernelGGL(k_sn_recv<M>, dim3(rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_, d_ctr_);
     hipLaunchKernelGGL(k_sn_claim<M>, dim3(SN_CWG + rgrid), dim3(SN_THREADS), 0, st_, lev, d_snc_, d_sns_, sn_recv_,
-                       cs_.t, cs_.nslots, d_ctr_);
+                       cs_.t, cs_.nslots, d_ctr_, cs_.word_shift());
     hipLaunchKernelGGL(k_sn_emit<M>, dim3(SN_EWG + rgrid), dim3(SN_THREADS), 0, st_, cur_, next_, flags_, lev, d_snc_,
                        d_sns_, sn_recv_, pkeys_, d_ctr_);
     KC_HIP_TRY(hipGetLastError());

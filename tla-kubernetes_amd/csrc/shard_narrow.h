@@ -469,8 +469,12 @@ k_sn_recv(uint32_t lev, const SNCtl* __restrict__ ctl, SNScratch* __restrict__ s
 template <class M>
 __global__ void __launch_bounds__(SN_THREADS)
 k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, const uint64_t* __restrict__ recv,
-           ClaimEntry* __restrict__ cs, uint64_t nslots, Counters* __restrict__ C) {
+           ClaimEntry* __restrict__ cs, uint64_t nslots, Counters* __restrict__ C, uint32_t csh = 1) {
   constexpr int RW = Record<M>::RW;
+  // (csh: slot i's fp word is word i << csh — 0 for the compact set of the
+  // first-claim mode, DevClaimSet::compact, which has no claim words and
+  // even home slots)
+  unsigned long long* const csw = reinterpret_cast<unsigned long long*>(cs);
   if (!ctl->active) return;
   const uint64_t n = ctl->n;
   const uint32_t world = ctl->world, rank = ctl->rank, cap = ctl->slot_cap, level = ctl->level;
@@ -503,11 +507,11 @@ k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, co
   const NarrowLT* __restrict__ lt = sc->lt[lev % SN_NLT];
   const uint32_t succ_level = level + 1;
   auto insert = [&](uint64_t fp, uint64_t ckey) -> bool {
-    uint64_t ix = bucket_of(fp, nslots);
+    uint64_t ix = csh ? bucket_of(fp, nslots) : fpslots_home(fp, nslots);
     for (uint64_t q = 0; q < nslots; ++q) {
-      const unsigned long long o = atomicCAS(&cs[ix].fp, 0ull, (unsigned long long)fp);
+      const unsigned long long o = atomicCAS(&csw[ix << csh], 0ull, (unsigned long long)fp);
       if (o == 0ull) {
-        cs[ix].nclaim = ~make_claim(succ_level, ckey);
+        if (csh) csw[(ix << 1) + 1] = ~make_claim(succ_level, ckey);
         return true;
       }
       if (o == fp) return false;
@@ -544,8 +548,8 @@ k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, co
             if (~e.nkey == sn_key(rank, i, (uint32_t)t)) fps[k] = e.fp;
           }
         }
-        ixs[k] = fps[k] ? bucket_of(fps[k], nslots) : 0ull;
-        os[k] = fps[k] ? atomicCAS(&cs[ixs[k]].fp, 0ull, (unsigned long long)fps[k]) : 0ull;
+        ixs[k] = fps[k] ? (csh ? bucket_of(fps[k], nslots) : fpslots_home(fps[k], nslots)) : 0ull;
+        os[k] = fps[k] ? atomicCAS(&csw[ixs[k] << csh], 0ull, (unsigned long long)fps[k]) : 0ull;
       }
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
@@ -558,10 +562,11 @@ k_sn_claim(uint32_t lev, SNCtl* __restrict__ ctl, SNScratch* __restrict__ sc, co
         uint64_t q = 1;
         for (; o != 0ull && o != fp && q < nslots; ++q) {
           ix = (ix + 1 == nslots) ? 0 : ix + 1;
-          o = atomicCAS(&cs[ix].fp, 0ull, (unsigned long long)fp);
+          o = atomicCAS(&csw[ix << csh], 0ull, (unsigned long long)fp);
         }
         if (o == 0ull) {
-          cs[ix].nclaim = ~make_claim(succ_level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | (i << 8) | (uint64_t)t);
+          if (csh)
+            csw[(ix << 1) + 1] = ~make_claim(succ_level, ((uint64_t)rank << CLAIM_RANK_SHIFT) | (i << 8) | (uint64_t)t);
           mine |= 1u << t;
         } else if (o != fp) {
           atomicAdd(&C->overflow, 1ull);               // a full table
