@@ -47,21 +47,30 @@ const char* kActionNames[A_COUNT] = {
 // (the level's last chunk): the level's head goes straight into pinned host
 // memory and the device head is reset for the next level (no copy launch,
 // no separate reset launch).
-__global__ void __launch_bounds__(64)
+// (K_ADVANCE_THREADS lanes: the 64-KiB snapshot copy is 16 loads per lane,
+// all in flight at once; round 5's 64 lanes ran it as 8 dependent batches)
+constexpr int K_ADVANCE_THREADS = 256;
+__global__ void __launch_bounds__(K_ADVANCE_THREADS)
 k_advance(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ newmask, uint64_t n,
           Counters* __restrict__ C, const uint32_t* __restrict__ tile_off, uint64_t tiles,
           unsigned long long* __restrict__ host, unsigned long long* __restrict__ ovf_count = nullptr,
           CtrStripe* __restrict__ snap = nullptr) {
   static_assert(CTR_STRIPES == 64, "one lane per stripe");
+  constexpr int UNITS = (int)(CTR_STRIPES * sizeof(CtrStripe) / 16), PER = UNITS / K_ADVANCE_THREADS;
+  static_assert(UNITS % K_ADVANCE_THREADS == 0, "whole 16-B units per lane");
   if (ovf_count && threadIdx.x == 0) *ovf_count = 0;   // the next chunk's candidate overflow list starts empty
   // the level's last chunk: the counters as the level leaves them, kept for
-  // a deferred-frontier redo from the next level (lane k copies stripe k)
+  // a deferred-frontier redo from the next level
   if (snap) {
-    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&C->s[threadIdx.x]);
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(&snap[threadIdx.x]);
-#pragma unroll 8
-    for (int k = 0; k < (int)(sizeof(CtrStripe) / 16); ++k) dst[k] = src[k];
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(C->s);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(snap);
+    ulonglong2 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = src[k * K_ADVANCE_THREADS + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) dst[k * K_ADVANCE_THREADS + threadIdx.x] = v[k];
   }
+  if (threadIdx.x >= 64) return;
   unsigned long long v = C->s[threadIdx.x].next_cand;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -580,7 +589,7 @@ class EngineT final : public EngineBase {
                                cfg_.keep_trace, d_ctr_, toff);
         });
         const bool last = start + cn >= n;
-        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, cn, d_ctr_,
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(K_ADVANCE_THREADS), 0, st_, offsets_, newmask_, cn, d_ctr_,
                            tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)tiles,
                            last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr,
                            claim_args_.ovf.count,
@@ -1677,7 +1686,7 @@ class EngineT final : public EngineBase {
                              next_gidx, parent_, ord_, cfg_.keep_trace, d_ctr_,
                              spill_ ? (const uint32_t*)toff_ : (const uint32_t*)nullptr);
         });
-        hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, st_, offsets_, newmask_, m, d_ctr_,
+        hipLaunchKernelGGL(k_advance, dim3(1), dim3(K_ADVANCE_THREADS), 0, st_, offsets_, newmask_, m, d_ctr_,
                            spill_ ? (const uint32_t*)toff_ : (const uint32_t*)nullptr, (uint64_t)(spill_ ? tiles : 0),
                            (unsigned long long*)nullptr, claim_args_.ovf.count);
         KC_HIP_TRY(hipGetLastError());
