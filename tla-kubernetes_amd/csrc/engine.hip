@@ -308,10 +308,12 @@ class EngineT final : public EngineBase {
     KC_TRY(grow_buffer(cur_, cur_cap_, (uint64_t)ni, false, st_));
     KC_TRY(grow_trace((uint64_t)ni + cand, false));
     KC_HIP_TRY(hipMemcpyAsync(cur_, init.data(), ni * sizeof(State), hipMemcpyHostToDevice, st_));
-    uint64_t* d_fps = nullptr;
-    int* d_res = nullptr;
-    KC_HIP_TRY(hipMalloc(&d_fps, ni * 8));
-    KC_HIP_TRY(hipMalloc(&d_res, ni * sizeof(int)));
+    // (the Init fingerprints' device buffers are kept across runs: a
+    // hipMalloc / hipFree pair per run cost a device-wide sync)
+    KC_TRY(grow_buffer(init_fps_, init_fps_cap_, (uint64_t)ni, false, st_));
+    KC_TRY(grow_buffer(init_res_, init_res_cap_, (uint64_t)ni, false, st_));
+    uint64_t* const d_fps = init_fps_;
+    int* const d_res = init_res_;
     KC_HIP_TRY(hipMemcpyAsync(d_fps, fps.data(), ni * 8, hipMemcpyHostToDevice, st_));
     launch_claimset_insert_list(d_fps, (uint64_t)ni, cs_, 1u, d_res, st_);
     std::vector<int> ires(ni);
@@ -328,8 +330,6 @@ class EngineT final : public EngineBase {
       KC_HIP_TRY(hipMemcpyAsync(ord_, iord.data(), ni, hipMemcpyHostToDevice, st_));
     }
     KC_HIP_TRY(hipStreamSynchronize(st_));
-    (void)hipFree(d_fps);
-    (void)hipFree(d_res);
     for (int k = 0; k < ni; ++k) {
       if (ires[k] != CL_NEW) {
         set_error("kubecheck: init states not distinct");
@@ -580,7 +580,8 @@ class EngineT final : public EngineBase {
         }
         timed(KK_EMIT, [&] {
           if (dfr)
-            hipLaunchKernelGGL(k_emit_links, dim3(grid), dim3(256), 0, st_, cn, start, newmask_, toff_, level_gidx,
+            hipLaunchKernelGGL(k_emit_links, dim3((tiles + EMIT_TPB - 1) / EMIT_TPB), dim3(256), 0, st_, cn, start,
+                               newmask_, toff_, level_gidx,
                                next_gidx, cfg_.keep_trace ? parent_ : nullptr, cfg_.keep_trace ? ord_ : nullptr,
                                use_link ? link_next_ : nullptr, link_cap, d_ctr_);
           else
@@ -1041,7 +1042,8 @@ class EngineT final : public EngineBase {
     if (h_tsum_) (void)hipHostFree(h_tsum_);
     if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
-                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_})
+                    (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_,
+                    (void*)init_fps_, (void*)init_res_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_chain_) (void)hipHostFree(h_chain_);
@@ -1848,6 +1850,9 @@ class EngineT final : public EngineBase {
       hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
                          cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
   }
+  uint64_t* init_fps_ = nullptr;
+  int* init_res_ = nullptr;
+  uint64_t init_fps_cap_ = 0, init_res_cap_ = 0;
   bool first_claim_ = false;   // KC_FIRST_CLAIM=1: k_claim FIRST, no settle passes (multi-worker TLC semantics)
   uint32_t *ttot_ = nullptr, *toff_ = nullptr;
   uint64_t ttot_cap_ = 0, toff_cap_ = 0;

@@ -1623,57 +1623,77 @@ __device__ __forceinline__ void emit_body(const typename M::State* __restrict__ 
 // are not written and set DF_CAPACITY: the host re-runs on the exact path.
 // Same wave-balanced dealing as emit_body: lane g of a round writes entry
 // obase + g, so a round's stores are contiguous.
+// A workgroup takes EMIT_TPB consecutive 256-parent tiles (round 6): all
+// their masks and tile offsets are loaded at once, then the tiles are dealt
+// one after another — one dependent round trip per workgroup instead of one
+// per tile (a tile's work is a few stores; its time was its round trips).
+constexpr int EMIT_TPB = 4;
 static __global__ void __launch_bounds__(256)
 k_emit_links(uint64_t n, uint64_t base, const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ tile_off,
              uint64_t level_gidx, uint64_t next_gidx, unsigned long long* __restrict__ parent,
              uint8_t* __restrict__ ord, unsigned long long* __restrict__ link, uint64_t cap,
              Counters* __restrict__ C) {
   __shared__ unsigned int sh_deg[OUTDEG_BINS * ACT_STRIPES];   // (striped by lane, as k_claim's counters)
-  __shared__ unsigned int sh_wtot[4];
+  __shared__ unsigned int sh_wtot[EMIT_TPB][4];
+  const uint64_t cb = C->chunk_base;
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  uint32_t mask[EMIT_TPB], toff[EMIT_TPB];
+#pragma unroll
+  for (int k = 0; k < EMIT_TPB; ++k) {
+    const uint64_t tile = (uint64_t)blockIdx.x * EMIT_TPB + k;
+    const uint64_t i = tile * 256 + threadIdx.x;
+    mask[k] = i < n ? newmask[i] : 0u;
+    toff[k] = tile * 256 < n ? tile_off[tile] : 0u;
+  }
   if (threadIdx.x < OUTDEG_BINS * ACT_STRIPES) sh_deg[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t mask = i < n ? newmask[i] : 0u;
-  const int cnt = __builtin_popcount(mask);
-  if (i < n) atomicAdd(&sh_deg[(cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1) * ACT_STRIPES + (threadIdx.x & (ACT_STRIPES - 1))], 1u);
-  const int lane = (int)(threadIdx.x & 63);
-  int incl = cnt;
+  int excl[EMIT_TPB], wtot[EMIT_TPB];
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
+  for (int k = 0; k < EMIT_TPB; ++k) {
+    const uint64_t i = ((uint64_t)blockIdx.x * EMIT_TPB + k) * 256 + threadIdx.x;
+    const int cnt = __builtin_popcount(mask[k]);
+    if (i < n) atomicAdd(&sh_deg[(cnt < OUTDEG_BINS ? cnt : OUTDEG_BINS - 1) * ACT_STRIPES + (threadIdx.x & (ACT_STRIPES - 1))], 1u);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    wtot[k] = __shfl(incl, 63, 64);
+    excl[k] = incl - cnt;
+    if (lane == 0) sh_wtot[k][wv] = (unsigned int)wtot[k];
   }
-  const int wtot = __shfl(incl, 63, 64);
-  const int excl = incl - cnt;
-  if (lane == 0) sh_wtot[threadIdx.x >> 6] = (unsigned int)wtot;
   __syncthreads();
-  uint64_t obase = C->chunk_base + tile_off[blockIdx.x];
-  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) obase += sh_wtot[w];
-  const uint64_t wave0 = i - (uint64_t)lane;
   bool over = false;
-  for (int r = 0; r < wtot; r += 64) {
-    const int g = r + lane;
-    int p = 0;                                       // last lane with excl <= g
 #pragma unroll
-    for (int b = 32; b > 0; b >>= 1) {
-      const int e = __shfl(excl, p + b, 64);
-      if (e <= g) p += b;
-    }
-    int k = g - __shfl(excl, p, 64);
-    uint32_t m = (uint32_t)__shfl((int)mask, p, 64);
-    if (g >= wtot) continue;
-    for (; k > 0; --k) m &= m - 1;
-    const int t = __ffs(m) - 1;
-    const uint64_t pidx = base + wave0 + (uint64_t)p;
-    const uint64_t o = obase + (uint64_t)g;
-    if (o >= cap) {
-      over = true;
-      continue;
-    }
-    if (link) link[o] = (pidx << 8) | (uint64_t)t;
-    if (parent) {
-      parent[next_gidx + o] = level_gidx + pidx;
-      ord[next_gidx + o] = (uint8_t)t;
+  for (int k = 0; k < EMIT_TPB; ++k) {
+    uint64_t obase = cb + toff[k];
+    for (int w = 0; w < wv; ++w) obase += sh_wtot[k][w];
+    const uint64_t wave0 = ((uint64_t)blockIdx.x * EMIT_TPB + k) * 256 + (uint64_t)(threadIdx.x - lane);
+    for (int r = 0; r < wtot[k]; r += 64) {
+      const int g = r + lane;
+      int p = 0;                                       // last lane with excl <= g
+#pragma unroll
+      for (int b = 32; b > 0; b >>= 1) {
+        const int e = __shfl(excl[k], p + b, 64);
+        if (e <= g) p += b;
+      }
+      int q = g - __shfl(excl[k], p, 64);
+      uint32_t m = (uint32_t)__shfl((int)mask[k], p, 64);
+      if (g >= wtot[k]) continue;
+      for (; q > 0; --q) m &= m - 1;
+      const int t = __ffs(m) - 1;
+      const uint64_t pidx = base + wave0 + (uint64_t)p;
+      const uint64_t o = obase + (uint64_t)g;
+      if (o >= cap) {
+        over = true;
+        continue;
+      }
+      if (link) link[o] = (pidx << 8) | (uint64_t)t;
+      if (parent) {
+        parent[next_gidx + o] = level_gidx + pidx;
+        ord[next_gidx + o] = (uint8_t)t;
+      }
     }
   }
   if (over) atomicOr(&C->defer_flags, DF_CAPACITY);

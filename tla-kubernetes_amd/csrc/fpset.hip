@@ -190,9 +190,11 @@ int DevClaimSet::init(uint64_t min_slots, hipStream_t st) {
 }
 
 // (an 8,192-workgroup grid-stride clear kernel: 6.9 TB/s on the 64 GiB NP=2
-// table against hipMemsetAsync's 6.3, round 3)
+// table against hipMemsetAsync's 6.3, round 3; on the 32 GiB
+// compact table hipMemsetAsync is the faster, 5.8 against 6.5-7.3 ms,
+// profiles/r06u_clear_bench.log)
 int DevClaimSet::clear(hipStream_t st) {
-  if (nslots < (1u << 20)) {
+  if (nslots < (1u << 20) || compact) {
     KC_HIP_TRY(hipMemsetAsync(t, 0, nslots * slot_bytes(), st));
   } else {
     hipLaunchKernelGGL(k_claimset_clear, dim3(8192u), dim3(256), 0, st, t, nslots * slot_bytes() / 16);
