@@ -405,7 +405,7 @@ def _valid_trace(oracle, cfg, trace):
         assert any(list(map(int, x)) == b for _, x in succ)
 
 
-@pytest.mark.parametrize("env", [{}, {"KC_DEFER": "0"}, {"KC_DEFER_SLACK": "0.001"}])
+@pytest.mark.parametrize("env", [{}, {"KC_DEFER": "0"}, {"KC_DEFER_SLACK": "0.001"}, {"KC_CHUNK_SCAN": "0"}])
 def test_first_claim_counts(model1, fixtures, monkeypatch, env):
     monkeypatch.setenv("KC_FIRST_CLAIM", "1")
     for k, v in env.items():

@@ -218,6 +218,8 @@ class EngineT final : public EngineBase {
     // KC_CLAIM_COMPACT=0 keeps 16-B slots (A/B)
     const char* cc = getenv("KC_CLAIM_COMPACT");
     cs_.compact = first_claim_ && !(cc && cc[0] == '0');
+    const char* ck = getenv("KC_CHUNK_SCAN");
+    chunk_scan_ = !(ck && ck[0] == '0');
   }
   ~EngineT() override { release(); }
 
@@ -458,6 +460,11 @@ class EngineT final : public EngineBase {
         if (tscan_) {
           KC_TRY(grow_buffer(ttot_, ttot_cap_, tiles + 4, false, st_));
           KC_TRY(grow_buffer(toff_, toff_cap_, tiles + 4, false, st_));
+          if (first_claim_ && chunk_scan_) {
+            const uint64_t old = csum_cap_;
+            KC_TRY(grow_buffer(csum_, csum_cap_, tiles / CSUM_TILES + 4, false, st_));
+            if (csum_cap_ != old) KC_HIP_TRY(hipMemsetAsync(csum_, 0, csum_cap_ * sizeof(uint32_t), st_));
+          }
         }
         KC_TRY(grow_buffer(rec_fp_, rec_fp_cap_, tiles * CLAIM_RCAP, false, st_));
         KC_TRY(grow_buffer(rec_lk_, rec_lk_cap_, tiles * CLAIM_RCAP, false, st_));
@@ -484,10 +491,16 @@ class EngineT final : public EngineBase {
         ++res->levels_chunks;
         const unsigned grid = (unsigned)((cn + 255) / 256);
         const unsigned tiles = (unsigned)((cn + CLAIM_TILE - 1) / CLAIM_TILE);
+        // first-claim levels with the link emit: tile counts summed per chunk
+        // of CSUM_TILES tiles by k_claim, k_chunk_scan over the chunks
+        // (KC_CHUNK_SCAN=0: k_tile_scan over every tile)
+        const bool cscan = first_claim_ && chunk_scan_ && tscan_ && dfr;
+        const unsigned nchunk = (tiles + CSUM_TILES - 1) / CSUM_TILES;
         timed(KK_EXPAND, [&] {
           if (first_claim_) {
             ShardArgs fa = claim_args_;
             fa.ttot = ttot_;
+            if (cscan) fa.csum = csum_;
             if (cs_.compact)
               hipLaunchKernelGGL((k_claim<M, 0, false, 0, false, true, true>), dim3(tiles), dim3(CLAIM_TILE), 0, st_,
                                  cur_ + start, cn, start, flags_, cfg_.check_deadlock, cs_.t, cs_.nslots, succ_level,
@@ -535,7 +548,11 @@ class EngineT final : public EngineBase {
         if (!first_claim_)
           timed(KK_RESOLVE,
                 [&] { launch_settle(cn, start, tiles, succ_level, tscan_ ? ttot_ : (uint32_t*)nullptr, fuse); });
-        if (tscan_) {
+        if (cscan) {
+          timed(KK_SCAN, [&] {
+            hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, csum_, nchunk, toff_, tscan_reg_);
+          });
+        } else if (tscan_) {
           timed(KK_SCAN, [&] {
             if (fuse)
               hipLaunchKernelGGL(k_ovf_tile_scan, dim3(1), dim3(TSCAN_THREADS), 0, st_, claim_args_.ovf, cn, start,
@@ -583,7 +600,8 @@ class EngineT final : public EngineBase {
             hipLaunchKernelGGL(k_emit_links, dim3((tiles + EMIT_TPB - 1) / EMIT_TPB), dim3(256), 0, st_, cn, start,
                                newmask_, toff_, level_gidx,
                                next_gidx, cfg_.keep_trace ? parent_ : nullptr, cfg_.keep_trace ? ord_ : nullptr,
-                               use_link ? link_next_ : nullptr, link_cap, d_ctr_);
+                               use_link ? link_next_ : nullptr, link_cap, d_ctr_,
+                               cscan ? ttot_ : (const uint32_t*)nullptr);
           else
             hipLaunchKernelGGL(k_emit<M>, dim3(grid), dim3(256), 0, st_, cur_ + start, cn, start,
                                flags_, newmask_, offsets_, next_, 0ull, level_gidx, next_gidx, parent_, ord_,
@@ -591,7 +609,7 @@ class EngineT final : public EngineBase {
         });
         const bool last = start + cn >= n;
         hipLaunchKernelGGL(k_advance, dim3(1), dim3(K_ADVANCE_THREADS), 0, st_, offsets_, newmask_, cn, d_ctr_,
-                           tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)tiles,
+                           tscan_ ? toff_ : (const uint32_t*)nullptr, (uint64_t)(cscan ? nchunk : tiles),
                            last && !headcopy_ ? reinterpret_cast<unsigned long long*>(h_ctr_) : nullptr,
                            claim_args_.ovf.count,
                            last && defer_now_ && !headcopy_ ? d_snap_[level % 3].s : (CtrStripe*)nullptr);
@@ -1043,7 +1061,7 @@ class EngineT final : public EngineBase {
     if (h_spctr_) (void)hipHostFree(h_spctr_);
     for (void* p : {(void*)cur_, (void*)next_, (void*)parent_, (void*)ord_, (void*)newmask_, (void*)abl_mask_, (void*)rcount_, (void*)rec_fp_, (void*)rec_lk_,
                     (void*)offsets_, (void*)scan_tmp_, (void*)d_ctr_, (void*)d_ctr_abl_, (void*)ttot_, (void*)toff_,
-                    (void*)init_fps_, (void*)init_res_})
+                    (void*)init_fps_, (void*)init_res_, (void*)csum_})
       if (p) (void)hipFree(p);
     if (h_ctr_) (void)hipHostFree(h_ctr_);
     if (h_chain_) (void)hipHostFree(h_chain_);
@@ -1850,6 +1868,10 @@ class EngineT final : public EngineBase {
       hipLaunchKernelGGL(k_settle_ovf<1>, dim3(SETTLE_OVF_GRID), dim3(256), 0, st_, claim_args_.ovf, cn, start, cs_.t,
                          cs_.nslots, succ_level, newmask_, d_ctr_, 0u, ttot);
   }
+  // k_chunk_scan's chunk sums (zeroed at allocation and by each scan)
+  bool chunk_scan_ = true;
+  uint32_t* csum_ = nullptr;
+  uint64_t csum_cap_ = 0;
   uint64_t* init_fps_ = nullptr;
   int* init_res_ = nullptr;
   uint64_t init_fps_cap_ = 0, init_res_cap_ = 0;

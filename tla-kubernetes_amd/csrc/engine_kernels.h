@@ -358,7 +358,12 @@ struct ShardArgs {
   // first-claim mode (k_claim FIRST; the engine, KC_FIRST_CLAIM): each tile's
   // new-state count, the input of k_tile_scan (no settle passes run)
   uint32_t* ttot = nullptr;
+  // (round 6, the engine's first-claim levels) each tile's count also added
+  // into its chunk of CSUM_TILES tiles: k_chunk_scan then scans T / 64 sums
+  // instead of T counts, and the link emit finishes a tile's offset itself
+  uint32_t* csum = nullptr;
 };
+constexpr uint32_t CSUM_TILES = 64;
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
 // workgroups resident together (~1,536: 6 per CU) work on tiles spread over
 // the whole level, and each of the S columns of tiles is walked in order.
@@ -1182,7 +1187,10 @@ k_claim(const typename M::State* __restrict__ cur, uint64_t n, uint64_t base, Fl
     for (int off = 32; off > 0; off >>= 1) c += (unsigned)__shfl_xor((int)c, off, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(&sh_rc, c);   // (sh_rc is 0: no candidates)
     __syncthreads();
-    if (threadIdx.x == 0) sh.ttot[tile] = sh_rc;
+    if (threadIdx.x == 0) {
+      sh.ttot[tile] = sh_rc;
+      if (sh.csum && sh_rc) atomicAdd(&sh.csum[tile / CSUM_TILES], sh_rc);
+    }
   }
   if (SH && live) {
     sh.repmask[i] = sh_rep[threadIdx.x];
@@ -1483,6 +1491,17 @@ k_tile_scan(const uint32_t* __restrict__ tot, uint32_t T, uint32_t* __restrict__
   tile_scan_body(tot, T, off, reg_ok, ScanMarks{}, nullptr);
 }
 
+// The chunk-sum scan (round 6; the engine's first-claim levels): coff =
+// exclusive prefix of the CSUM_TILES-tile chunk sums k_claim accumulated
+// (coff[C] the total), and the sums zeroed for the next level.  The link
+// emit adds a tile's offset inside its chunk from the tile counts.  One
+// workgroup, as k_tile_scan, over 64x fewer cells.
+static __global__ void __launch_bounds__(TSCAN_THREADS)
+k_chunk_scan(uint32_t* __restrict__ csum, uint32_t nchunk, uint32_t* __restrict__ coff, int reg_ok) {
+  tile_scan_body(csum, nchunk, coff, reg_ok, ScanMarks{}, nullptr);
+  for (uint32_t c = threadIdx.x; c < nchunk; c += TSCAN_THREADS) csum[c] = 0u;
+}
+
 // A small chunk's settle pass B over its candidate overflow list and the
 // tile scan in one workgroup (round 5): the list of a chunk of <= 2^16
 // parents is short (usually empty), so the 1,024-workgroup k_settle_ovf<1>
@@ -1632,18 +1651,41 @@ static __global__ void __launch_bounds__(256)
 k_emit_links(uint64_t n, uint64_t base, const uint32_t* __restrict__ newmask, const uint32_t* __restrict__ tile_off,
              uint64_t level_gidx, uint64_t next_gidx, unsigned long long* __restrict__ parent,
              uint8_t* __restrict__ ord, unsigned long long* __restrict__ link, uint64_t cap,
-             Counters* __restrict__ C) {
+             Counters* __restrict__ C, const uint32_t* __restrict__ ttot = nullptr) {
+  // tile offsets: tile_off[tile] (k_tile_scan), or with ttot (k_chunk_scan)
+  // tile_off[chunk] + the tile counts of its chunk before it (each wave
+  // scans the chunk's <= 64 counts; a workgroup's tiles share one chunk)
+  static_assert(CSUM_TILES == 64 && CSUM_TILES % EMIT_TPB == 0, "a workgroup's tiles in one chunk");
   __shared__ unsigned int sh_deg[OUTDEG_BINS * ACT_STRIPES];   // (striped by lane, as k_claim's counters)
   __shared__ unsigned int sh_wtot[EMIT_TPB][4];
   const uint64_t cb = C->chunk_base;
   const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  const uint64_t T = (n + 255) / 256, tile0 = (uint64_t)blockIdx.x * EMIT_TPB;
   uint32_t mask[EMIT_TPB], toff[EMIT_TPB];
+  uint32_t cnt_in_chunk = 0, coff = 0;
+  if (ttot) {
+    const uint64_t c0 = tile0 / CSUM_TILES * CSUM_TILES;
+    cnt_in_chunk = c0 + lane < T ? ttot[c0 + lane] : 0u;
+    coff = tile_off[tile0 / CSUM_TILES];
+  }
 #pragma unroll
   for (int k = 0; k < EMIT_TPB; ++k) {
-    const uint64_t tile = (uint64_t)blockIdx.x * EMIT_TPB + k;
+    const uint64_t tile = tile0 + k;
     const uint64_t i = tile * 256 + threadIdx.x;
     mask[k] = i < n ? newmask[i] : 0u;
-    toff[k] = tile * 256 < n ? tile_off[tile] : 0u;
+    toff[k] = !ttot && tile < T ? tile_off[tile] : 0u;
+  }
+  if (ttot) {
+    uint32_t x = cnt_in_chunk;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = (uint32_t)__shfl_up((int)x, off, 64);
+      if (lane >= off) x += v;
+    }
+    const int j0 = (int)(tile0 % CSUM_TILES);
+#pragma unroll
+    for (int k = 0; k < EMIT_TPB; ++k)
+      toff[k] = coff + (uint32_t)__shfl((int)(x - cnt_in_chunk), j0 + k, 64);
   }
   if (threadIdx.x < OUTDEG_BINS * ACT_STRIPES) sh_deg[threadIdx.x] = 0;
   __syncthreads();

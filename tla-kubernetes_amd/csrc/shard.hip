@@ -633,6 +633,7 @@ k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint
   bool over = false;
   if (blockIdx.x < lblocks) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t tbase = woff[blockIdx.x];         // (loaded with the masks: one round trip less)
     const uint32_t mask = i < n_local ? newmask[i] : 0u;
     const int cnt = __builtin_popcount(mask);
     const int lane = (int)(threadIdx.x & 63);
@@ -646,7 +647,7 @@ k_shard_emit_links(uint64_t n_local, uint32_t lblocks, uint64_t rank, const uint
     const int excl = incl - cnt;
     if (lane == 0) sh_wtot[threadIdx.x >> 6] = (unsigned int)wtot;
     __syncthreads();
-    uint64_t obase = woff[blockIdx.x];
+    uint64_t obase = tbase;
     for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) obase += sh_wtot[w];
     const uint64_t wave0 = i - (uint64_t)lane;
     for (int r = 0; r < wtot; r += 64) {
