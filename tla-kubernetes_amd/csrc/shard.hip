@@ -274,6 +274,9 @@ k_rec_claim(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict
 // settle passes (a copy this rank's own k_claim inserted at expand, or an
 // earlier record's, makes it old).  isnew[i] directly, and each block's
 // winners into rtot[blk] (the record half of k_win_scan's input).
+// (Two records per lane, their loads, probes and CASes issued together,
+// measured slower at R = 8: Σ over the ranks 23.3 -> 26.5 ms, r06z — half
+// the workgroups on the small levels.)
 template <class M>
 __global__ void __launch_bounds__(256)
 k_rec_claim_first(const Record<M>* __restrict__ in, uint64_t n, ClaimEntry* __restrict__ cs, uint64_t nslots,

@@ -11,9 +11,10 @@
               ModelConfig.first_claim (first-inserter claims, no settle passes).
   summarize:  python tools/shard_attr.py summarize TRACE_DIR R [--out f.json]
               reads rocprofv3's *_kernel_trace.csv (and *_memory_copy_trace.csv
-              if present), keeps the last check (from the last R
-              k_claimset_clear launches, one per rank at its init), maps each
-              Stream_Id to its rank by the order of those clears, and reports
+              if present), keeps the last check (from the last R ClaimSet
+              clears, one per rank at its init: the clear kernel or, on the
+              compact table, a > 300 us fill), maps each Stream_Id to its rank
+              by the order of those clears, and reports
               per rank the summed kernel time and the per-kernel split, the
               sum over ranks, the max over ranks (the critical path an R-GPU
               run would have, communication aside) and the check's span."""
@@ -66,9 +67,14 @@ def summarize(d, R, out):
             rows.append(("c", "copy " + r.get("Direction", "?"), int(r.get("Stream_Id", -1)),
                          int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     rows.sort(key=lambda x: x[3])
-    clears = [i for i, r in enumerate(rows) if "k_claimset_clear" in r[1]]
+    # every rank's check starts with its ClaimSet clear: the k_claimset_clear
+    # kernel, or on the compact table of the first-claim mode a
+    # hipMemsetAsync fill (the only fill of a warm check that runs > 300 us:
+    # a rank's share of the table)
+    clears = [i for i, r in enumerate(rows)
+              if "k_claimset_clear" in r[1] or ("fillBuffer" in r[1] and r[4] - r[3] > 300_000)]
     if len(clears) < R:
-        raise SystemExit(f"found {len(clears)} k_claimset_clear launches, need >= {R}")
+        raise SystemExit(f"found {len(clears)} ClaimSet clears, need >= {R}")
     start = clears[-R]
     rank_of = {}
     for i in clears[-R:]:
