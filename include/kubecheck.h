@@ -240,7 +240,9 @@ typedef struct {
    * the seen-set spill or a frontier HBM budget; KC_FIRST_CLAIM=1 sets it
    * too).  Sharded loop (kc_shard_*, kc_group_*): every counted level, at any
    * world; kc_shard_create fails with -EINVAL together with tlc_order or the
-   * seen-set spill.  kc_result.claim_mode reports what ran. */
+   * seen-set spill.  kc_result.claim_mode reports what ran.  The seen-set
+   * then holds 8-B fingerprint words (16-B {fp, claim} slots otherwise): the
+   * same slot count and load in half the HBM, half the per-run clear. */
   int first_claim;
 } kc_model_config;
 
