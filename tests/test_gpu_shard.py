@@ -496,6 +496,23 @@ def test_native_first_claim(fixtures, oracle, monkeypatch, R, snarrow):
         _first_trace_ok(oracle, kw, r["trace"])
 
 
+@pytest.mark.parametrize("first", [True, False])
+def test_native_owner_chunk_scan_off(fixtures, monkeypatch, first):
+    # round 6: the staged records' positions come from owner x 64-tile chunk
+    # sums (k_owner_cscan, k_shard_gather's in-chunk prefix) by default;
+    # KC_CHUNK_SCAN=0 keeps the per-tile owner scan — same counts and widths
+    # at R = 3 with every level counted
+    monkeypatch.setenv("KC_CHUNK_SCAN", "0")
+    monkeypatch.setenv("KC_SNARROW", "0")
+    fx = fixtures["model1"]
+    r = native(3, first_claim=first)
+    assert r["complete"] and r["error"] is None and r["level_width"] == fx["level_width"]
+    assert (r["distinct"], r["generated"], r["depth"]) == (fx["distinct"], fx["generated"], fx["depth"])
+    fx = fixtures["np2_40levels"]
+    r = native(4, np=2, max_levels=40, first_claim=first)
+    assert r["level_width"] == fx["level_width"] and r["act_gen"] == fx["act_gen"]
+
+
 def test_native_first_claim_np2(fixtures):
     # NP=2: the 40-level prefix at 4 emulated ranks, and the seeded race's
     # NoLostUpdate violation at depth 25 (wide, deferred levels) at 3

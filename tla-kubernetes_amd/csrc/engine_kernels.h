@@ -362,6 +362,10 @@ struct ShardArgs {
   // into its chunk of CSUM_TILES tiles: k_chunk_scan then scans T / 64 sums
   // instead of T counts, and the link emit finishes a tile's offset itself
   uint32_t* csum = nullptr;
+  // (round 6, the sharded staging) each tile's per-owner record counts also
+  // added into ocsum[owner][chunk of CSUM_TILES tiles]: k_owner_cscan scans
+  // those, k_shard_gather finishes a tile's positions itself
+  uint32_t* ocsum = nullptr;
 };
 constexpr uint32_t CSUM_TILES = 64;
 // Tile order of k_claim.  Block b takes tile (b % S) * share + b / S: the
@@ -667,7 +671,11 @@ __device__ __forceinline__ void stage_records(const ShardArgs& sh, bool live, ui
     seg[1] = (unsigned int)(b >> 32);
     sh.stoff[tile] = b;
   }
-  if (tid < R) sh.tcnt[(uint64_t)tid * gridDim.x + tile] = tt[tid];
+  if (tid < R) {
+    sh.tcnt[(uint64_t)tid * gridDim.x + tile] = tt[tid];
+    if (sh.ocsum && tt[tid])
+      atomicAdd(&sh.ocsum[(uint64_t)tid * ((gridDim.x + CSUM_TILES - 1) / CSUM_TILES) + tile / CSUM_TILES], tt[tid]);
+  }
   __syncthreads();
   const unsigned long long sb = (unsigned long long)seg[0] | ((unsigned long long)seg[1] << 32);
   const uint32_t total = rwave[0] + rwave[1] + rwave[2] + rwave[3];

@@ -205,28 +205,79 @@ k_owner_tscan(const uint32_t* __restrict__ tcnt, uint32_t T, uint32_t world, uin
               init_err);
   }
 }
+// The same over the owner x chunk sums (round 6, ShardArgs::ocsum): world x
+// C cells (C = ceil(T / CSUM_TILES)) instead of world x T; coff[o][chunk] is
+// the send-buffer position of the chunk's first record of owner o, and the
+// sums are zeroed for the next level.  k_shard_gather adds a tile's offset
+// inside its chunk.
+__global__ void __launch_bounds__(TSCAN_THREADS)
+k_owner_cscan(uint32_t* __restrict__ ocsum, uint32_t C_, uint32_t world, uint32_t* __restrict__ coff,
+              uint64_t* __restrict__ tot, const Counters* __restrict__ C, uint64_t* __restrict__ host_tot,
+              unsigned long long* __restrict__ host_head, uint64_t* __restrict__ row, uint64_t status_new,
+              uint64_t status_err, int level1, uint64_t init_err) {
+  __shared__ unsigned int sh_mark[17];
+  const uint32_t cells = world * C_;
+  tile_scan_body(ocsum, cells, coff, 1, ScanMarks{C_, world, cells}, sh_mark);
+  for (uint32_t c = threadIdx.x; c < cells; c += TSCAN_THREADS) ocsum[c] = 0u;
+  if (threadIdx.x < 64) {
+    const uint32_t o = threadIdx.x;
+    const uint64_t v = o < world ? (uint64_t)(sh_mark[o + 1 < world ? o + 1 : world] - sh_mark[o]) : 0ull;
+    owner_row(o, world > 1 ? v : 0ull, world, tot, C, host_tot, host_head, row, status_new, status_err, level1,
+              init_err);
+  }
+}
 // The staged records into the send buffer (pack without re-expansion): one
-// workgroup per tile moves its segment, owner by owner, to toff[o][tile].
+// workgroup per tile moves its segment, owner by owner, to toff[o][tile]
+// (chunked: coff[o][chunk] + the tile counts of owner o before it in its
+// chunk, one wave prefix per owner).
 template <class M>
 __global__ void __launch_bounds__(256)
 k_shard_gather(const Record<M>* __restrict__ stage, const unsigned long long* __restrict__ stoff,
                const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ toff, uint32_t T, uint32_t world,
-               Record<M>* __restrict__ out) {
+               Record<M>* __restrict__ out, int chunked) {
   constexpr int U = Record<M>::RW / 2;     // 16-B units per record
   __shared__ uint32_t sh_n[16], sh_src[16], sh_dst[16];
   const uint32_t tile = blockIdx.x;
-  if (threadIdx.x == 0) {
+  const unsigned long long b = stoff[tile];      // (loaded with the counts: one round trip less)
+  if (!chunked) {
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      for (uint32_t o = 0; o < world; ++o) {
+        const uint32_t c = tcnt[(uint64_t)o * T + tile];
+        sh_n[o] = c;
+        sh_src[o] = acc;
+        sh_dst[o] = toff[(uint64_t)o * T + tile];
+        acc += c;
+      }
+    }
+  } else if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x, c0 = tile / CSUM_TILES * CSUM_TILES, j = tile - c0;
+    const uint32_t nC = (T + CSUM_TILES - 1) / CSUM_TILES;
+    uint32_t v[16], base[16];
+#pragma unroll
+    for (uint32_t o = 0; o < 16; ++o) {          // (world <= 15) every owner's counts and chunk base at once
+      v[o] = o < world && c0 + lane < T ? tcnt[(uint64_t)o * T + c0 + lane] : 0u;
+      base[o] = o < world ? toff[(uint64_t)o * nC + tile / CSUM_TILES] : 0u;
+    }
     uint32_t acc = 0;
-    for (uint32_t o = 0; o < world; ++o) {
-      const uint32_t c = tcnt[(uint64_t)o * T + tile];
-      sh_n[o] = c;
-      sh_src[o] = acc;
-      sh_dst[o] = toff[(uint64_t)o * T + tile];
-      acc += c;
+#pragma unroll
+    for (uint32_t o = 0; o < 16; ++o) {
+      if (o >= world) break;
+      uint32_t x = v[o];
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, off, 64);
+        if (lane >= (uint32_t)off) x += y;
+      }
+      if (lane == j) {
+        sh_n[o] = v[o];
+        sh_src[o] = acc;
+        sh_dst[o] = base[o] + x - v[o];
+      }
+      acc += (uint32_t)__shfl((int)v[o], (int)j, 64);
     }
   }
   __syncthreads();
-  const unsigned long long b = stoff[tile];
   if (b == ~0ull) return;
   const ulonglong2* src = reinterpret_cast<const ulonglong2*>(stage + b);
   ulonglong2* dst = reinterpret_cast<ulonglong2*>(out);
@@ -889,6 +940,8 @@ class ShardT final : public ShardBase {
     // no candidates, no settle passes): the first inserter owns a state, as in
     // a TLC -workers N run
     first_ = cfg.first_claim != 0;
+    const char* ck = getenv("KC_CHUNK_SCAN");
+    ocscan_ = !(ck && ck[0] == '0');
     // (its ClaimSet holds fp words only, as the engine's in this mode: 8-B
     // slots, half the table to clear; the narrow levels write no claim words)
     cs_.compact = first_;
@@ -1115,6 +1168,13 @@ class ShardT final : public ShardBase {
       KC_TRY(grow_buffer(tcnt_, tcnt_cap_, cells + 8, false, st_));
       KC_TRY(grow_buffer(toff_, toff_cap_, cells + 8, false, st_));
       KC_TRY(grow_buffer(stoff_, stoff_cap_, tiles, false, st_));
+      ocscan_level_ = ocscan_;
+      if (ocscan_level_) {
+        const uint64_t old = ocsum_cap_;
+        KC_TRY(grow_buffer(ocsum_, ocsum_cap_, (tiles / CSUM_TILES + 1) * (uint64_t)world_ + 8, false, st_));
+        if (ocsum_cap_ != old) KC_HIP_TRY(hipMemsetAsync(ocsum_, 0, ocsum_cap_ * sizeof(uint32_t), st_));
+        sh.ocsum = ocsum_;
+      }
       sh.stage = stage_;
       sh.stage_cur = d_stage_cur_;
       sh.stage_cap = stage_cap_;
@@ -1210,6 +1270,12 @@ class ShardT final : public ShardBase {
         set_error("kc_shard_expand: %llu tile x owner cells exceed one scan", (unsigned long long)(tiles * world_));
         return -ENOMEM;
       }
+      if (ocscan_level_)
+        hipLaunchKernelGGL(k_owner_cscan, dim3(1), dim3(TSCAN_THREADS), 0, st_, ocsum_,
+                           (uint32_t)((tiles + CSUM_TILES - 1) / CSUM_TILES), (uint32_t)world_, toff_, d_owner_base_,
+                           d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_), d_row, status_new,
+                           status_err, (int)level1, dev_init_err_);
+      else
       hipLaunchKernelGGL(k_owner_tscan, dim3(1), dim3(TSCAN_THREADS), 0, st_, tcnt_, (uint32_t)tiles, (uint32_t)world_,
                          toff_, d_owner_base_, d_ctr_, h_owner_base_, reinterpret_cast<unsigned long long*>(h_exp_),
                          d_row, status_new, status_err, (int)level1, dev_init_err_);
@@ -1362,7 +1428,7 @@ class ShardT final : public ShardBase {
       // the tiles' staged segments, in tile order per owner
       const unsigned tiles = (unsigned)((n_ + CLAIM_TILE - 1) / CLAIM_TILE);
       hipLaunchKernelGGL(k_shard_gather<M>, dim3(tiles), dim3(256), 0, st_, stage_, stoff_, tcnt_, toff_, tiles,
-                         (uint32_t)world_, (Rec*)send);
+                         (uint32_t)world_, (Rec*)send, ocscan_level_ ? 1 : 0);
       KC_HIP_TRY(hipGetLastError());
     } else if (n_ && send_total_) {
       if (stage_level_) {
@@ -2118,7 +2184,7 @@ class ShardT final : public ShardBase {
                     (void*)repmask_, (void*)newmask_, (void*)offsets_, (void*)rcount_, (void*)rec_fp_,
                     (void*)rec_lk_, (void*)rfp_, (void*)flag_, (void*)isnew_, (void*)ioff_,
                     (void*)scan_tmp_, (void*)d_ctr_, (void*)d_owner_base_, (void*)stage_, (void*)d_stage_cur_,
-                    (void*)tcnt_, (void*)toff_, (void*)stoff_, (void*)wtot_, (void*)woff_, (void*)link_cur_,
+                    (void*)tcnt_, (void*)toff_, (void*)stoff_, (void*)ocsum_, (void*)wtot_, (void*)woff_, (void*)link_cur_,
                     (void*)link_next_, (void*)pc_cur_, (void*)pc_prev_, (void*)d_dchk_, (void*)d_ctr_dbg_,
                     (void*)pk_dbg_, (void*)gpos_all_, (void*)gbits_cur_, (void*)grank_cur_, (void*)gbits_next_,
                     (void*)grank_next_, (void*)wmask_, (void*)wbase_, (void*)gnew_, (void*)link_tmp_,
@@ -2173,6 +2239,11 @@ class ShardT final : public ShardBase {
   unsigned long long* d_stage_cur_ = nullptr;
   uint32_t *tcnt_ = nullptr, *toff_ = nullptr;
   uint64_t tcnt_cap_ = 0, toff_cap_ = 0;
+  // owner x chunk sums of the staged record counts (k_owner_cscan; zeroed at
+  // allocation and by each scan); KC_CHUNK_SCAN=0: k_owner_tscan per tile
+  bool ocscan_ = true, ocscan_level_ = false;
+  uint32_t* ocsum_ = nullptr;
+  uint64_t ocsum_cap_ = 0;
   unsigned long long* stoff_ = nullptr;
   uint64_t stoff_cap_ = 0;
   bool stage_on_ = true, stage_level_ = false, staged_ = false;
