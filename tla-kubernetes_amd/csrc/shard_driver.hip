@@ -640,20 +640,22 @@ class HostComm final : public Comm {
     return 0;
   }
   int broadcast(int root, uint64_t* v) override { return call(ops_.broadcast(ops_.ctx, root, v), "broadcast"); }
-  // (the caller's all_reduce_sum works on 64-bit host words)
+  // (the caller's all_reduce_sum works on 64-bit host words: two u32 words
+  // travel in each.  The only caller is tlc_order's mask words, whose bits
+  // are disjoint across ranks — each new state has one winner — so a word's
+  // sum is its OR, never above 2^32 - 1, and the low half cannot carry into
+  // the high one)
   int all_reduce_dev_u32(const std::vector<uint32_t*>& buf, uint64_t n) override {
     if (n == 0) return 0;
     hipStream_t st = s_->stream();
-    std::vector<uint32_t> h(n, 0);
+    std::vector<uint64_t> w((n + 1) / 2, 0);
     if (buf[0]) {
-      KC_HIP_TRY(hipMemcpyAsync(h.data(), buf[0], n * 4, hipMemcpyDeviceToHost, st));
+      KC_HIP_TRY(hipMemcpyAsync(w.data(), buf[0], n * 4, hipMemcpyDeviceToHost, st));
       KC_HIP_TRY(hipStreamSynchronize(st));
     }
-    std::vector<uint64_t> w(h.begin(), h.end());
     KC_TRY(call(ops_.all_reduce_sum(ops_.ctx, w.data(), w.size()), "all_reduce_sum"));
     if (!buf[0]) return 0;
-    for (uint64_t k = 0; k < n; ++k) h[k] = (uint32_t)w[k];
-    KC_HIP_TRY(hipMemcpyAsync(buf[0], h.data(), n * 4, hipMemcpyHostToDevice, st));
+    KC_HIP_TRY(hipMemcpyAsync(buf[0], w.data(), n * 4, hipMemcpyHostToDevice, st));
     KC_HIP_TRY(hipStreamSynchronize(st));
     return 0;
   }
